@@ -1,0 +1,123 @@
+/*
+ * nsh_hip.h -- C-ABI of libnsh_hip.so, the MI355X (gfx950) kernel shim behind the
+ * newsched block-execution path.
+ *
+ * Plain C, POD arguments only (device pointers as void* or float*, sizes as size_t/int64_t,
+ * streams and events as opaque void*). No C++ or torch types cross this boundary, so the
+ * newsched C++17 host (meson or otherwise) links it directly, and Python reaches it with
+ * ctypes.
+ *
+ * Every entry point returns 0 on success or a nonzero hipError_t-style code; it never
+ * throws. The text of the last failure on the calling thread is in nsh_last_error().
+ * The C++ wrappers (gr::hip_buffer, gr::hip::* blocks) turn nonzero codes into
+ * std::runtime_error, because WORK_ERROR would spin forever in the reference executor
+ * (schedulers/mt/lib/graph_executor.cpp:102-131).
+ *
+ * Reference interfaces each group replaces (paths relative to the reference tree):
+ *   streams/events     cudaStreamCreate per buffer/block (runtime/lib/cudabuffer.cu:37,
+ *                      blocklib/cuda/lib/copy.cpp:33) and cudaStreamSynchronize per work()
+ *                      (copy.cpp:58, cudabuffer.cu:175) -> one stream per GPU partition,
+ *                      event-ordered edges, no host syncs in steady state.
+ *   ring memory        cuda_buffer's 2x cudaMalloc + mirror copies (cudabuffer.cu:27-35,
+ *                      :116-176) -> one HIP-VMM allocation mapped twice back to back.
+ *   nsh_memcpy_async   cuda_buffer::post_write H2D/D2H copies (cudabuffer.cu:129-157) and
+ *                      copy_items (cudabuffer.cu:179-183, a host memcpy on device memory).
+ *   nsh_copy           apply_copy_kernel (blocklib/cuda/lib/copy.cu:6-33), one launch per
+ *                      1024-sample vector (copy.cpp:49-57) -> one launch per work().
+ *   nsh_mul_const_*    multiply_const_kernel (blocklib/cuda/lib/multiply_const.cu:1-18, ff
+ *                      only) and the CPU multiply_const<T>::work (blocklib/blocks/lib/
+ *                      multiply_const.cpp:17-46, VOLK 32fc_s32fc / 32f_s32f).
+ *   nsh_add_cc, nsh_mul_cc, nsh_fir_*, nsh_fft1024_c2c, nsh_channelizer1024
+ *                      no reference counterpart; GNU Radio semantics.
+ */
+#ifndef NSH_HIP_H
+#define NSH_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NSH_ABI_VERSION 1
+
+/* ---- errors / device ---------------------------------------------------------- */
+int nsh_abi_version(void);
+const char* nsh_last_error(void);          /* thread-local; "" when no error */
+int nsh_get_device_count(int* count);
+int nsh_set_device(int dev);
+int nsh_device_info(int dev, int* n_cu, int* clock_khz, size_t* hbm_bytes, char* arch, int arch_len);
+int nsh_device_sync(void);
+
+/* ---- streams and events (opaque hipStream_t / hipEvent_t) ---------------------- */
+int nsh_stream_create(int dev, void** stream);
+int nsh_stream_destroy(void* stream);
+int nsh_stream_sync(void* stream);
+int nsh_event_create(void** event);
+int nsh_event_destroy(void* event);
+int nsh_event_record(void* event, void* stream);
+int nsh_event_query(void* event);          /* 0 complete, 1 not ready, <0 error */
+int nsh_event_sync(void* event);
+int nsh_event_elapsed_ms(void* start, void* stop, float* ms);
+int nsh_stream_wait_event(void* stream, void* event);
+
+/* ---- memory ----------------------------------------------------------------------- */
+enum nsh_copy_kind { NSH_H2D = 0, NSH_D2H = 1, NSH_D2D = 2, NSH_DEFAULT = 3 };
+int nsh_malloc(int dev, size_t bytes, void** ptr);
+int nsh_free(void* ptr);
+int nsh_host_alloc(size_t bytes, void** ptr);       /* pinned, device-visible */
+int nsh_host_free(void* ptr);
+int nsh_memcpy_async(void* dst, const void* src, size_t bytes, int kind, void* stream);
+int nsh_memset_async(void* ptr, int value, size_t bytes, void* stream);
+
+/* Device ring for gr::hip_buffer: one physical allocation of *actual_bytes (>= min_bytes,
+ * rounded to the VMM granularity) mapped twice back to back, so [base, base+2*actual)
+ * aliases [base, base+actual) -- read_ptr()/write_ptr() spans are always contiguous and
+ * no mirror copy is ever made. *double_mapped = 0 means VMM was unavailable and a plain
+ * allocation was returned; the caller must then cap spans at the wrap point. */
+int nsh_ring_alloc(int dev, size_t min_bytes, void** base, size_t* actual_bytes, int* double_mapped);
+int nsh_ring_free(void* base);
+
+/* ---- stream kernels (n counts complex samples unless the name ends in _ff) --------- */
+int nsh_copy(const void* in, void* out, size_t bytes, void* stream);
+int nsh_mul_const_cc(const float* in, float* out, int64_t n, float k_re, float k_im, void* stream);
+int nsh_mul_const_ff(const float* in, float* out, int64_t n, float k, void* stream);
+/* m multiply_const_cc stages fused into one pass: k holds m (re,im) pairs, applied in
+ * order with the same per-stage float rounding as m separate launches. */
+int nsh_mul_const_chain_cc(const float* in, float* out, int64_t n, const float* k_host, int m, void* stream);
+int nsh_add_cc(const float* a, const float* b, float* out, int64_t n, void* stream);
+int nsh_mul_cc(const float* a, const float* b, float* out, int64_t n, void* stream);
+
+/* Counter-based synthetic stream: x[i] = (u(2i), u(2i+1)),
+ * u(j) = 24-bit uniform in [-1,1) from splitmix64(seed ^ j), j counted from first_index*2. */
+int nsh_synth_cf32(float* out, int64_t n, uint64_t first_index, uint64_t seed, void* stream);
+
+/* ---- FIR (fir_filter_ccf, optionally decimating) ----------------------------------
+ * y[m] = sum_{k<ntaps} h[k] * x[m*decim - k], x complex fp32, h real fp32. The block keeps
+ * its own (ntaps-1)-sample history because the reference block API has none
+ * (runtime/include/gnuradio/sync_block.hpp:36-86). Per call:
+ *   in       : n_out*decim input samples (device)
+ *   hist_in  : ntaps-1 samples that precede in[0] (device; zeros at stream start)
+ *   hist_out : receives the ntaps-1 samples that precede the NEXT call's in[0]
+ *              (must not alias hist_in -- ping-pong two buffers)
+ * algo: NSH_FIR_AUTO picks by measurement, NSH_FIR_DIRECT is the fp32 VALU
+ * direct form, NSH_FIR_MFMA is the f16x3 split-precision Toeplitz MFMA form (decim 1). */
+enum nsh_fir_algo { NSH_FIR_AUTO = 0, NSH_FIR_DIRECT = 1, NSH_FIR_MFMA = 2 };
+int nsh_fir_plan_create(int dev, const float* taps_host, int ntaps, int decim, int algo, void** plan);
+int nsh_fir_plan_destroy(void* plan);
+int nsh_fir_plan_algo(void* plan);          /* the algorithm AUTO resolved to */
+int nsh_fir_ccf(void* plan, const float* in, const float* hist_in, float* hist_out,
+                float* out, int64_t n_out, void* stream);
+
+/* ---- FFT (fft_vcc, 1024-point, unnormalised both ways) ------------------------------
+ * frames of 1024 complex samples; inverse=1 computes sum_k X[k] e^{+2 pi i kn/1024}
+ * (= 1024 * numpy.fft.ifft). nsh_channelizer1024 fuses fft -> multiply by w[1024]
+ * (complex, device) -> ifft in one pass over HBM. */
+int nsh_fft1024_c2c(const float* in, float* out, int64_t nframes, int inverse, void* stream);
+int nsh_channelizer1024(const float* in, float* out, const float* w, int64_t nframes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NSH_HIP_H */

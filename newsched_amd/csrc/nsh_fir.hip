@@ -1,0 +1,206 @@
+// libnsh_hip.so: fir_filter_ccf (complex fp32 stream, real fp32 taps, optional decimation).
+//
+//   y[m] = sum_{k<L} h[k] * x[m*D - k]          (GNU Radio fir_filter_ccf convention with
+//                                                 zero initial history)
+//
+// The reference has no FIR block; its block API has no history
+// (runtime/include/gnuradio/sync_block.hpp:36-86), so each call receives the L-1 samples
+// that precede in[0] (hist_in) and hands the next call its own (hist_out).
+//
+// Two algorithms (nsh_fir_algo):
+//  * DIRECT -- fp32 VALU direct form. A 256-thread workgroup stages its input window
+//    (T-1)*D + Lp samples in LDS (one HBM read per sample), each thread keeps R
+//    consecutive outputs in registers and slides an 8-tap register window over the
+//    staged samples; taps come from the scalar cache (s_load, uniform index). LDS rows
+//    are padded by one sample every R*D samples so the per-lane ds_read_b64 of the window
+//    is bank-conflict-free. Exact fp32 products, fp32 accumulation in tap order.
+//  * MFMA -- bf16x3 split-precision Toeplitz MFMA (nsh_fir_mfma.hip), decim 1.
+#include "nsh_common.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+#include "nsh_fir_plan.hpp"
+
+namespace {
+
+constexpr int kThreads = 256;
+
+__device__ __forceinline__ float2 virt(const float2* __restrict__ in,
+                                       const float2* __restrict__ hist,
+                                       int64_t g,
+                                       int64_t n_in,
+                                       int L)
+{
+    if (g >= 0) return g < n_in ? in[g] : make_float2(0.f, 0.f);
+    if (g >= -(int64_t)(L - 1)) return hist[g + (L - 1)];
+    return make_float2(0.f, 0.f);
+}
+
+template <int D, int R>
+__global__ __launch_bounds__(kThreads) void k_fir_direct(const float2* __restrict__ in,
+                                                         const float2* __restrict__ hist_in,
+                                                         float2* __restrict__ hist_out,
+                                                         float2* __restrict__ out,
+                                                         const float* __restrict__ taps, // Lp, zero padded
+                                                         int L,
+                                                         int Lp,
+                                                         int64_t n_out)
+{
+    extern __shared__ __attribute__((aligned(16))) float2 xs[];
+    constexpr int T = kThreads * R;          // outputs per workgroup
+    constexpr int W = 8 + (R - 1) * D;       // register window (samples)
+    constexpr int PAD = R * D;               // one pad sample every PAD samples
+    const int tid = threadIdx.x;
+    const int64_t n_in = n_out * D;
+    const int64_t m0 = (int64_t)blockIdx.x * T;
+    const int64_t g0 = m0 * D - (Lp - 1);    // global index of staged sample 0
+    const int count = (T - 1) * D + Lp;
+
+    for (int i = tid; i < count; i += kThreads) xs[i + i / PAD] = virt(in, hist_in, g0 + i, n_in, L);
+
+    if (blockIdx.x == 0) { // history for the next call: the L-1 samples before in[n_in]
+        for (int j = tid; j < L - 1; j += kThreads) hist_out[j] = virt(in, hist_in, n_in - (L - 1) + j, n_in, L);
+    }
+    __syncthreads();
+
+    float2 acc[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] = make_float2(0.f, 0.f);
+
+    // window w[o] = xs[t*R*D + Lp - 8 - 8*kb + o]
+    int base = tid * R * D + Lp - 8;
+    float2 w[W];
+#pragma unroll
+    for (int o = 0; o < W; ++o) {
+        const int s = base + o;
+        w[o] = xs[s + s / PAD];
+    }
+    const int nkb = Lp / 8;
+    for (int kb = 0; kb < nkb; ++kb) {
+        float h[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) h[j] = taps[8 * kb + j];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const float2 x = w[r * D + 7 - j];
+                acc[r].x = __builtin_fmaf(h[j], x.x, acc[r].x);
+                acc[r].y = __builtin_fmaf(h[j], x.y, acc[r].y);
+            }
+        }
+        if (kb + 1 < nkb) {
+#pragma unroll
+            for (int o = W - 1; o >= 8; --o) w[o] = w[o - 8];
+            base -= 8;
+#pragma unroll
+            for (int o = 0; o < 8; ++o) {
+                const int s = base + o;
+                w[o] = xs[s + s / PAD];
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int64_t m = m0 + (int64_t)tid * R + r;
+        if (m < n_out) out[m] = acc[r];
+    }
+}
+
+template <int D, int R>
+int launch_direct(const nsh_fir_plan* p, const float2* in, const float2* hin, float2* hout, float2* out, int64_t n_out, hipStream_t s)
+{
+    constexpr int T = kThreads * R;
+    const int count = (T - 1) * D + p->Lp;
+    const size_t lds = (size_t)(count + count / (R * D) + 1) * sizeof(float2);
+    const int64_t grid = (n_out + T - 1) / T;
+    if (grid > 0x7fffffff) return nsh::fail_msg("nsh_fir_ccf: too many outputs for one call");
+    hipLaunchKernelGGL((k_fir_direct<D, R>), dim3((unsigned)grid), dim3(kThreads), lds, s,
+                       in, hin, hout, out, p->taps_dev, p->L, p->Lp, n_out);
+    NSH_CK_LAUNCH("nsh_fir_ccf(direct)");
+    return 0;
+}
+
+// History-only update for n_out == 0 calls is a no-op: no input consumed.
+int run_direct(const nsh_fir_plan* p, const float2* in, const float2* hin, float2* hout, float2* out, int64_t n_out, hipStream_t s)
+{
+    switch (p->D) {
+    case 1: return launch_direct<1, 8>(p, in, hin, hout, out, n_out, s);
+    case 2: return launch_direct<2, 8>(p, in, hin, hout, out, n_out, s);
+    case 4: return launch_direct<4, 4>(p, in, hin, hout, out, n_out, s);
+    case 8: return launch_direct<8, 2>(p, in, hin, hout, out, n_out, s);
+    default: return nsh::fail_msg("nsh_fir_ccf(direct): decimation must be 1, 2, 4 or 8");
+    }
+}
+
+} // namespace
+
+extern "C" {
+
+int nsh_fir_plan_create(int dev, const float* taps_host, int ntaps, int decim, int algo, void** plan)
+{
+    if (ntaps < 1 || ntaps > 4096) return nsh::fail_msg("nsh_fir_plan_create: ntaps must be in [1, 4096]");
+    if (decim != 1 && decim != 2 && decim != 4 && decim != 8)
+        return nsh::fail_msg("nsh_fir_plan_create: decimation must be 1, 2, 4 or 8");
+    NSH_CK(hipSetDevice(dev));
+    auto* p = new nsh_fir_plan();
+    p->dev = dev;
+    p->L = ntaps;
+    p->D = decim;
+    p->Lp = (ntaps + 7) / 8 * 8;
+    p->taps_host.assign(taps_host, taps_host + ntaps);
+    std::vector<float> padded(p->Lp, 0.f);
+    std::copy(taps_host, taps_host + ntaps, padded.begin());
+    hipError_t e = hipMalloc(&p->taps_dev, p->Lp * sizeof(float));
+    if (e == hipSuccess) e = hipMemcpy(p->taps_dev, padded.data(), p->Lp * sizeof(float), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        delete p;
+        return nsh::fail(e, "nsh_fir_plan_create: taps upload");
+    }
+    int resolved = algo;
+    if (algo == NSH_FIR_AUTO) resolved = nsh_fir_mfma_supported(p) ? NSH_FIR_MFMA : NSH_FIR_DIRECT;
+    if (resolved == NSH_FIR_MFMA) {
+        if (!nsh_fir_mfma_supported(p)) {
+            (void)hipFree(p->taps_dev);
+            delete p;
+            return nsh::fail_msg("nsh_fir_plan_create: MFMA form needs decim 1 and ntaps <= 513");
+        }
+        const int rc = nsh_fir_mfma_prepare(p);
+        if (rc) {
+            (void)hipFree(p->taps_dev);
+            delete p;
+            return rc;
+        }
+    }
+    p->algo = resolved;
+    *plan = p;
+    return 0;
+}
+
+int nsh_fir_plan_destroy(void* plan)
+{
+    auto* p = static_cast<nsh_fir_plan*>(plan);
+    if (!p) return 0;
+    if (p->taps_dev) (void)hipFree(p->taps_dev);
+    if (p->frag_dev) (void)hipFree(p->frag_dev);
+    delete p;
+    return 0;
+}
+
+int nsh_fir_plan_algo(void* plan) { return static_cast<nsh_fir_plan*>(plan)->algo; }
+
+int nsh_fir_ccf(void* plan, const float* in, const float* hist_in, float* hist_out, float* out, int64_t n_out, void* stream)
+{
+    auto* p = static_cast<nsh_fir_plan*>(plan);
+    if (!p) return nsh::fail_msg("nsh_fir_ccf: null plan");
+    if (n_out <= 0) return 0;
+    if (hist_in == hist_out && p->L > 1) return nsh::fail_msg("nsh_fir_ccf: hist_out must not alias hist_in");
+    hipStream_t s = nsh::S(stream);
+    if (p->algo == NSH_FIR_MFMA)
+        return nsh_fir_mfma_run(p, (const float2*)in, (const float2*)hist_in, (float2*)hist_out, (float2*)out, n_out, s);
+    return run_direct(p, (const float2*)in, (const float2*)hist_in, (float2*)hist_out, (float2*)out, n_out, s);
+}
+
+} // extern "C"

@@ -1,0 +1,24 @@
+// Internal FIR plan shared by nsh_fir.hip (direct form, dispatch) and nsh_fir_mfma.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <vector>
+
+struct nsh_fir_plan {
+    int dev = 0;
+    int L = 0;            // taps
+    int Lp = 0;           // taps rounded up to a multiple of 8 (zero padded) for DIRECT
+    int D = 1;            // decimation
+    int algo = 0;         // resolved nsh_fir_algo
+    std::vector<float> taps_host;
+    float* taps_dev = nullptr;
+    // MFMA form: Q tap blocks of 32, S = 2Q k-steps of 16; B fragments in lane order,
+    // [part(3)][kstep(S)][lane(64)][8] bf16.
+    int Q = 0;
+    int S = 0;
+    void* frag_dev = nullptr;
+};
+
+bool nsh_fir_mfma_supported(const nsh_fir_plan* p);
+int nsh_fir_mfma_prepare(nsh_fir_plan* p);
+int nsh_fir_mfma_run(const nsh_fir_plan* p, const float2* in, const float2* hist_in, float2* hist_out,
+                     float2* out, int64_t n_out, hipStream_t s);

@@ -1,0 +1,49 @@
+"""CPU: the C-ABI libraries build, load, and export every symbol their headers declare
+(no compute calls -- there is no GPU in the build container)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from tests.conftest import ROOT
+
+
+def declared(header):
+    txt = open(os.path.join(ROOT, "include", header)).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(nsh_\w+|nsr_\w+)\s*\(", txt)))
+
+
+def exported(so):
+    out = subprocess.run(["nm", "-D", "--defined-only", so], capture_output=True, text=True, check=True).stdout
+    return {l.split()[-1] for l in out.splitlines() if l.strip()}
+
+
+def test_hip_shim_exports_header():
+    from newsched_amd import nsh
+
+    syms = exported(nsh.HIP_LIB)
+    missing = [s for s in declared("nsh_hip.h") if s not in syms]
+    assert not missing, missing
+    # the Python binding covers exactly the header
+    assert sorted(nsh.SIGNATURES) == declared("nsh_hip.h")
+
+
+def test_hip_shim_loads_and_reports():
+    from newsched_amd import nsh
+
+    L = nsh.lib()
+    assert L.nsh_abi_version() == 1
+    assert L.nsh_last_error() == b""
+
+
+def test_hip_shim_is_gfx950_code_object():
+    from newsched_amd import nsh
+
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", nsh.HIP_LIB],
+                         capture_output=True, text=True)
+    if out.returncode != 0:
+        pytest.skip("llvm-objdump --offloading unavailable")
+    assert "gfx950" in out.stdout + out.stderr

@@ -1,0 +1,281 @@
+"""GPU parity: each kernel of libnsh_hip.so, called through the C-ABI, against the CPU
+oracle on the same seeded inputs, plus golden fixtures and size-independent properties.
+
+Tolerances: bit-exact for copy / identity multiplies / per-stage-rounded complex
+products (same formula, no FMA); FIR and FFT within the north-star 1e-5 relative bound
+(norm-wise max|dy| <= 1e-5 max|y_ref| and per element, oracle.tol_ok)."""
+import numpy as np
+import pytest
+
+from oracle import oracle as orc
+from newsched_amd import nsh
+
+pytestmark = pytest.mark.gpu
+
+
+def dev(torch, a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def host(t):
+    import torch
+
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+def test_synth_bit_exact(torch_cuda):
+    torch = torch_cuda
+    for n, first in [(1, 0), (1000, 0), (4097, 123456789)]:
+        y = torch.empty(n, dtype=torch.complex64, device="cuda")
+        nsh.synth(y, n, first)
+        np.testing.assert_array_equal(host(y), orc.synth(n, first))
+
+
+@pytest.mark.parametrize("nbytes", [8, 16, 24, 8 * 1023, 8 * (1 << 20) + 8])
+@pytest.mark.parametrize("offset", [0, 8])
+def test_copy_bit_exact(torch_cuda, nbytes, offset):
+    torch = torch_cuda
+    x = orc.synth(nbytes // 8 + 2)
+    dx = dev(torch, x)
+    dy = torch.zeros_like(dx)
+    base_x = dx.data_ptr() + offset
+    base_y = dy.data_ptr() + offset
+    nsh.copy(base_x, base_y, nbytes)
+    y = host(dy)
+    o = offset // 8
+    np.testing.assert_array_equal(y[o:o + nbytes // 8], x[o:o + nbytes // 8])
+    assert np.all(y[:o] == 0) and np.all(y[o + nbytes // 8:] == 0)
+
+
+def test_mul_const_identity_reference_vector(torch_cuda):
+    """BlockFanout vector (qa_scheduler_mt.cpp:79-135): x=(2i,2i+1), k=1 -> identity."""
+    torch = torch_cuda
+    n = 1_000_000
+    x = (2 * np.arange(n) + 1j * (2 * np.arange(n) + 1)).astype(np.complex64)
+    dx = dev(torch, x)
+    dy = torch.empty_like(dx)
+    nsh.mul_const_cc(dx, dy, n, 1.0 + 0.0j)
+    np.testing.assert_array_equal(host(dy), x)
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 1000, 262145])
+@pytest.mark.parametrize("k", [0.5 - 0.25j, complex(np.exp(0.3j))])
+def test_mul_const_cc_bit_exact(torch_cuda, n, k):
+    torch = torch_cuda
+    x = orc.synth(n, 99)
+    dx = dev(torch, x)
+    dy = torch.empty_like(dx)
+    nsh.mul_const_cc(dx, dy, n, k)
+    np.testing.assert_array_equal(host(dy), orc.mul_const_cc(x, np.complex64(k)))
+
+
+def test_mul_const_cc_unaligned(torch_cuda):
+    torch = torch_cuda
+    n = 5001
+    x = orc.synth(n + 1)
+    dx = dev(torch, x)
+    dy = torch.zeros_like(dx)
+    nsh.mul_const_cc(dx.data_ptr() + 8, dy.data_ptr() + 8, n, 0.25 + 2j)
+    np.testing.assert_array_equal(host(dy)[1:], orc.mul_const_cc(x[1:], np.complex64(0.25 + 2j)))
+
+
+def test_mul_const_ff_bit_exact(torch_cuda):
+    torch = torch_cuda
+    x = orc.synth(4099).view(np.float32)
+    dx = dev(torch, x)
+    dy = torch.empty_like(dx)
+    nsh.mul_const_ff(dx, dy, x.size, 1.7)
+    np.testing.assert_array_equal(host(dy), orc.mul_const_ff(x, 1.7))
+
+
+def test_mul_chain_golden(torch_cuda, golden):
+    torch = torch_cuda
+    g = golden("mulchain4.npz")
+    dx = dev(torch, g["x"])
+    dy = torch.empty_like(dx)
+    nsh.mul_const_chain_cc(dx, dy, g["x"].size, list(g["k"]))
+    np.testing.assert_array_equal(host(dy), g["y"])
+    for m in (1, 2, 3, 7):
+        ks = [complex(np.exp(0.1j * (i + 1))) for i in range(m)]
+        nsh.mul_const_chain_cc(dx, dy, g["x"].size, ks)
+        np.testing.assert_array_equal(host(dy), orc.mul_const_chain_cc(g["x"], [np.complex64(k) for k in ks]))
+
+
+@pytest.mark.parametrize("n", [1, 777, 1 << 18])
+def test_add_mul_cc_bit_exact(torch_cuda, n):
+    torch = torch_cuda
+    a, b = orc.synth(n, 1), orc.synth(n, 10 ** 6)
+    da, db = dev(torch, a), dev(torch, b)
+    dy = torch.empty_like(da)
+    nsh.add_cc(da, db, dy, n)
+    np.testing.assert_array_equal(host(dy), orc.add_cc(a, b))
+    nsh.mul_cc(da, db, dy, n)
+    np.testing.assert_array_equal(host(dy), orc.mul_cc(a, b))
+
+
+ALGOS = [("direct", nsh.FIR_DIRECT), ("mfma", nsh.FIR_MFMA)]
+
+
+def run_fir(torch, plan, x, n_out, hist=None):
+    L = plan.ntaps
+    dx = dev(torch, x)
+    hin = dev(torch, hist if hist is not None else np.zeros(max(L - 1, 1), np.complex64))
+    hout = torch.zeros(max(L - 1, 1), dtype=torch.complex64, device="cuda")
+    dy = torch.empty(max(n_out, 1), dtype=torch.complex64, device="cuda")
+    plan(dx, hin, hout, dy, n_out)
+    return host(dy)[:n_out], host(hout)[: L - 1]
+
+
+@pytest.mark.parametrize("name,algo", ALGOS)
+def test_fir127_golden(torch_cuda, golden, name, algo):
+    torch = torch_cuda
+    g = golden("fir127.npz")
+    plan = nsh.FirPlan(g["taps"], 1, algo)
+    assert plan.algo == algo
+    y, hist = run_fir(torch, plan, g["x"], g["x"].size)
+    ok, err, scale = orc.tol_ok(y, g["y"])
+    assert ok, (name, err, scale)
+    np.testing.assert_array_equal(hist, g["x"][-126:])
+    y2, _ = run_fir(torch, plan, g["x_next"], g["x_next"].size, hist=hist)
+    ok, err, scale = orc.tol_ok(y2, g["y_next"])
+    assert ok, (name, err, scale)
+
+
+@pytest.mark.parametrize("name,algo", ALGOS)
+@pytest.mark.parametrize("ntaps", [1, 2, 31, 32, 33, 64, 127, 128, 161])
+@pytest.mark.parametrize("n", [1, 100, 2047, 2048, 2049, 70001])
+def test_fir_vs_oracle_shapes(torch_cuda, name, algo, ntaps, n):
+    torch = torch_cuda
+    rng = np.random.default_rng(ntaps * 1000 + n)
+    h = rng.standard_normal(ntaps).astype(np.float32) * 0.1
+    x = orc.synth(n, 5 + n)
+    hist = orc.synth(max(ntaps - 1, 1), 10 ** 7)[: ntaps - 1]
+    plan = nsh.FirPlan(h, 1, algo)
+    y, hout = run_fir(torch, plan, x, n, hist=hist if ntaps > 1 else None)
+    y_ref, h_ref = orc.fir_ccf(x, h, hist=hist if ntaps > 1 else None, return_hist=True)
+    ok, err, scale = orc.tol_ok(y, y_ref)
+    assert ok, (name, ntaps, n, err, scale)
+    np.testing.assert_array_equal(hout, h_ref)
+
+
+@pytest.mark.parametrize("decim", [2, 4, 8])
+def test_fir_decim_vs_oracle(torch_cuda, decim):
+    torch = torch_cuda
+    h = np.hanning(127).astype(np.float32) / 64
+    for n_out in (1, 513, 40001):
+        x = orc.synth(n_out * decim, 3)
+        hist = orc.synth(126, 4 * 10 ** 6)
+        plan = nsh.FirPlan(h, decim, nsh.FIR_DIRECT)
+        y, hout = run_fir(torch, plan, x, n_out, hist=hist)
+        y_ref, h_ref = orc.fir_ccf(x, h, decim=decim, hist=hist, return_hist=True)
+        ok, err, scale = orc.tol_ok(y, y_ref)
+        assert ok, (decim, n_out, err, scale)
+        np.testing.assert_array_equal(hout, h_ref)
+
+
+def test_fir_decim2_golden_chain(torch_cuda, golden):
+    torch = torch_cuda
+    g = golden("fir127_decim2.npz")
+    plan = nsh.FirPlan(g["taps"], 2)
+    y, _ = run_fir(torch, plan, g["x"], g["x"].size // 2)
+    ok, err, scale = orc.tol_ok(y, g["y"])
+    assert ok, (err, scale)
+    z = g["x"]
+    for _ in range(4):
+        z, _ = run_fir(torch, plan, z, z.size // 2)
+    ok, err, scale = orc.tol_ok(z, g["y_chain4"])
+    assert ok, (err, scale)
+
+
+@pytest.mark.parametrize("name,algo", ALGOS)
+def test_fir_chunked_stream_equals_one_shot(torch_cuda, name, algo):
+    """Call-splitting invariance: the history hand-off makes any chunking exact for the
+    direct form (tap order is position independent). The MFMA form sums each output in an
+    order set by its phase within the call's 32-sample blocks, so chunking changes the
+    rounding: equal within the 1e-5 bound, not bitwise."""
+    torch = torch_cuda
+    h = np.hamming(127).astype(np.float32) / 70
+    x = orc.synth(300_000, 42)
+    plan = nsh.FirPlan(h, 1, algo)
+    y_all, _ = run_fir(torch, plan, x, x.size)
+    hist = np.zeros(126, np.complex64)
+    parts = []
+    for a, b in [(0, 5), (5, 4101), (4101, 4102), (4102, 150_000), (150_000, 300_000)]:
+        yp, hist = run_fir(torch, plan, x[a:b], b - a, hist=hist)
+        parts.append(yp)
+    if algo == nsh.FIR_DIRECT:
+        np.testing.assert_array_equal(np.concatenate(parts), y_all)
+    else:
+        ok, err, scale = orc.tol_ok(np.concatenate(parts), y_all)
+        assert ok and err <= 1e-6 * scale, (err, scale)
+
+
+@pytest.mark.parametrize("name,algo", ALGOS)
+def test_fir_linearity_large(torch_cuda, name, algo):
+    """Size-independent property at 2^24 samples: FIR(a x1 + x2) == a FIR(x1) + FIR(x2)
+    within fp32 rounding, and a windowed oracle check at the start, middle and end."""
+    torch = torch_cuda
+    n = 1 << 24
+    h = np.asarray(__import__("scipy.signal", fromlist=["firwin"]).firwin(127, 0.2), np.float32)
+    plan = nsh.FirPlan(h, 1, algo)
+    x = torch.empty(n, dtype=torch.complex64, device="cuda")
+    nsh.synth(x, n, 0)
+    hin = torch.zeros(126, dtype=torch.complex64, device="cuda")
+    hout = torch.zeros_like(hin)
+    y = torch.empty_like(x)
+    plan(x, hin, hout, y, n)
+    torch.cuda.synchronize()
+    xs = x.cpu().numpy()
+    ys = y.cpu().numpy()
+    for a in (0, n // 2 - 5000, n - 10000):
+        ref = orc.fir_ccf(xs[a:a + 10000], h, hist=xs[a - 126:a] if a > 0 else None)
+        ok, err, scale = orc.tol_ok(ys[a:a + 10000], ref)
+        assert ok, (name, a, err, scale)
+    x2 = torch.empty_like(x)
+    nsh.synth(x2, n, 1 << 30)
+    y2 = torch.empty_like(x)
+    plan(x2, hin, hout, y2, n)
+    x3 = (0.5 * x + x2).contiguous()
+    y3 = torch.empty_like(x)
+    plan(x3, hin, hout, y3, n)
+    torch.cuda.synchronize()
+    lin = (0.5 * y + y2 - y3).abs().max().item()
+    scale = y3.abs().max().item()
+    assert lin <= 2e-6 * scale, (lin, scale)
+
+
+def test_fft_golden(torch_cuda, golden):
+    torch = torch_cuda
+    g = golden("fft1024.npz")
+    dx = dev(torch, g["x"])
+    dy = torch.empty_like(dx)
+    nf = g["x"].size // 1024
+    nsh.fft1024(dx, dy, nf)
+    ok, err, scale = orc.tol_ok(host(dy), g["X"])
+    assert ok, (err, scale)
+    nsh.fft1024(dx, dy, nf, inverse=True)
+    ok, err, scale = orc.tol_ok(host(dy), g["Xi"])
+    assert ok, (err, scale)
+    dw = dev(torch, g["w"])
+    nsh.channelizer1024(dx, dy, dw, nf)
+    ok, err, scale = orc.tol_ok(host(dy), g["y_chan"])
+    assert ok, (err, scale)
+
+
+def test_fft_roundtrip_large(torch_cuda):
+    """ifft(fft(x)) == 1024 x (size-independent property) at 2^22 samples."""
+    torch = torch_cuda
+    n = 1 << 22
+    x = torch.empty(n, dtype=torch.complex64, device="cuda")
+    nsh.synth(x, n, 77)
+    X = torch.empty_like(x)
+    xr = torch.empty_like(x)
+    nsh.fft1024(x, X, n // 1024)
+    nsh.fft1024(X, xr, n // 1024, inverse=True)
+    torch.cuda.synchronize()
+    err = (xr / 1024 - x).abs().max().item()
+    assert err <= 1e-5 * x.abs().max().item(), err
+    sub = x[: 64 * 1024].cpu().numpy()
+    ok, e, s = orc.tol_ok(X[: 64 * 1024].cpu().numpy(), orc.fft1024(sub))
+    assert ok, (e, s)
