@@ -1,0 +1,43 @@
+// gr::hip::fir_filter_ccf -- the MI355X hot path (BASELINE config C3/C5).
+// Complex fp32 stream, real fp32 taps, optional decimation D (n_consumed = D*n_produced).
+// The block owns the device tap plan and two (ntaps-1)-sample history buffers it
+// ping-pongs between work() calls, because the block API has no history (reference
+// runtime/include/gnuradio/sync_block.hpp:36-86). Device state is created on the first
+// start() on the partition thread (right device and stream) and the history is zeroed on
+// every start() (a fresh stream). Algorithm: nsh_fir_algo (AUTO = MFMA for D = 1).
+#pragma once
+#include <gnuradio/block.hpp>
+
+namespace gr {
+namespace hip {
+class fir_filter_ccf : public block
+{
+public:
+    using sptr = std::shared_ptr<fir_filter_ccf>;
+    static sptr make(const std::vector<float>& taps, int decim = 1, int algo = 0)
+    {
+        auto p = std::make_shared<fir_filter_ccf>(taps, decim, algo);
+        p->add_port(port<gr_complex>::make("in", port_direction_t::INPUT));
+        p->add_port(port<gr_complex>::make("out", port_direction_t::OUTPUT));
+        return p;
+    }
+    fir_filter_ccf(const std::vector<float>& taps, int decim, int algo);
+    ~fir_filter_ccf() override;
+    bool start() override;
+    work_return_code_t work(std::vector<block_work_input>& in, std::vector<block_work_output>& out) override;
+    int decimation() const { return _decim; }
+    int algo() const; // resolved algorithm (after start())
+    uint64_t launches() const { return _launches; }
+
+private:
+    void release();
+    std::vector<float> _taps;
+    int _decim, _algo;
+    int _dev = -1;
+    void* _plan = nullptr;
+    void* _hist[2] = { nullptr, nullptr };
+    int _cur = 0;
+    uint64_t _launches = 0;
+};
+} // namespace hip
+} // namespace gr

@@ -1,0 +1,203 @@
+// gr::hip::* block work() implementations: argument plumbing from block_work_io to the
+// libnsh_hip.so C-ABI on the thread's HIP stream. Nonzero codes throw (hip::check).
+#include <gnuradio/blocklib/hip/arith.hpp>
+#include <gnuradio/blocklib/hip/copy.hpp>
+#include <gnuradio/blocklib/hip/fft.hpp>
+#include <gnuradio/blocklib/hip/fir_filter_ccf.hpp>
+#include <gnuradio/blocklib/hip/multiply_const.hpp>
+#include <gnuradio/blocklib/hip/synth_source.hpp>
+#include <gnuradio/hip_context.hpp>
+
+#include <algorithm>
+#include <stdexcept>
+
+#include "nsh_hip.h"
+
+namespace gr {
+namespace hip {
+
+work_return_code_t copy::work(std::vector<block_work_input>& in, std::vector<block_work_output>& out)
+{
+    const size_t n = (size_t)out[0].n_items;
+    check(nsh_copy(in[0].buffer->read_ptr(), out[0].buffer->write_ptr(), n * d_batch_size * sizeof(gr_complex),
+                   current_stream()),
+          "hip::copy");
+    out[0].n_produced = out[0].n_items;
+    return work_return_code_t::WORK_OK;
+}
+
+template <>
+work_return_code_t multiply_const<gr_complex>::work(std::vector<block_work_input>& in, std::vector<block_work_output>& out)
+{
+    check(nsh_mul_const_cc((const float*)in[0].buffer->read_ptr(), (float*)out[0].buffer->write_ptr(),
+                           (int64_t)out[0].n_items * (int64_t)d_vlen, d_k.real(), d_k.imag(), current_stream()),
+          "hip::multiply_const_cc");
+    out[0].n_produced = out[0].n_items;
+    return work_return_code_t::WORK_OK;
+}
+
+template <>
+work_return_code_t multiply_const<float>::work(std::vector<block_work_input>& in, std::vector<block_work_output>& out)
+{
+    check(nsh_mul_const_ff((const float*)in[0].buffer->read_ptr(), (float*)out[0].buffer->write_ptr(),
+                           (int64_t)out[0].n_items * (int64_t)d_vlen, d_k, current_stream()),
+          "hip::multiply_const_ff");
+    out[0].n_produced = out[0].n_items;
+    return work_return_code_t::WORK_OK;
+}
+template class multiply_const<gr_complex>;
+template class multiply_const<float>;
+
+work_return_code_t multiply_const_chain_cc::work(std::vector<block_work_input>& in, std::vector<block_work_output>& out)
+{
+    std::vector<float> k;
+    k.reserve(2 * d_ks.size());
+    for (auto& c : d_ks) {
+        k.push_back(c.real());
+        k.push_back(c.imag());
+    }
+    check(nsh_mul_const_chain_cc((const float*)in[0].buffer->read_ptr(), (float*)out[0].buffer->write_ptr(),
+                                 (int64_t)out[0].n_items * (int64_t)d_vlen, k.data(), (int)d_ks.size(), current_stream()),
+          "hip::multiply_const_chain_cc");
+    out[0].n_produced = out[0].n_items;
+    return work_return_code_t::WORK_OK;
+}
+
+template <int OP>
+work_return_code_t arith_cc<OP>::work(std::vector<block_work_input>& in, std::vector<block_work_output>& out)
+{
+    const int64_t n = (int64_t)out[0].n_items * (int64_t)_vlen;
+    float* o = (float*)out[0].buffer->write_ptr();
+    void* s = current_stream();
+    if (_nports == 1) {
+        check(nsh_copy(in[0].buffer->read_ptr(), o, (size_t)n * 8, s), "hip::arith_cc");
+    } else {
+        for (size_t p = 1; p < _nports; ++p) {
+            const float* a = p == 1 ? (const float*)in[0].buffer->read_ptr() : o;
+            const float* b = (const float*)in[p].buffer->read_ptr();
+            check(OP == 0 ? nsh_add_cc(a, b, o, n, s) : nsh_mul_cc(a, b, o, n, s), OP == 0 ? "hip::add_cc" : "hip::multiply_cc");
+        }
+    }
+    out[0].n_produced = out[0].n_items;
+    return work_return_code_t::WORK_OK;
+}
+template class arith_cc<0>;
+template class arith_cc<1>;
+
+// ---- FIR ---------------------------------------------------------------------------
+fir_filter_ccf::fir_filter_ccf(const std::vector<float>& taps, int decim, int algo)
+    : block("fir_filter_ccf (hip)"), _taps(taps), _decim(decim), _algo(algo)
+{
+    if (taps.empty()) throw std::invalid_argument("hip::fir_filter_ccf: no taps");
+    if (decim != 1 && decim != 2 && decim != 4 && decim != 8)
+        throw std::invalid_argument("hip::fir_filter_ccf: decimation must be 1, 2, 4 or 8");
+}
+
+fir_filter_ccf::~fir_filter_ccf() { release(); }
+
+void fir_filter_ccf::release()
+{
+    if (_plan) nsh_fir_plan_destroy(_plan);
+    for (auto& h : _hist)
+        if (h) nsh_free(h);
+    _plan = nullptr;
+    _hist[0] = _hist[1] = nullptr;
+}
+
+int fir_filter_ccf::algo() const { return _plan ? nsh_fir_plan_algo(_plan) : _algo; }
+
+bool fir_filter_ccf::start()
+{
+    const int dev = current_device();
+    if (_plan && dev != _dev) release();
+    const size_t hbytes = std::max<size_t>(_taps.size() - 1, 1) * sizeof(gr_complex);
+    if (!_plan) {
+        _dev = dev;
+        check(nsh_fir_plan_create(dev, _taps.data(), (int)_taps.size(), _decim, _algo, &_plan), "hip::fir_filter_ccf plan");
+        check(nsh_malloc(dev, hbytes, &_hist[0]), "hip::fir_filter_ccf history");
+        check(nsh_malloc(dev, hbytes, &_hist[1]), "hip::fir_filter_ccf history");
+    }
+    void* s = current_stream();
+    check(nsh_memset_async(_hist[0], 0, hbytes, s), "hip::fir_filter_ccf history reset");
+    check(nsh_memset_async(_hist[1], 0, hbytes, s), "hip::fir_filter_ccf history reset");
+    _cur = 0;
+    return block::start();
+}
+
+work_return_code_t fir_filter_ccf::work(std::vector<block_work_input>& in, std::vector<block_work_output>& out)
+{
+    const int n_out = std::min(out[0].n_items, in[0].n_items / _decim);
+    if (n_out <= 0) return work_return_code_t::WORK_INSUFFICIENT_INPUT_ITEMS;
+    check(nsh_fir_ccf(_plan, (const float*)in[0].buffer->read_ptr(), (const float*)_hist[_cur], (float*)_hist[_cur ^ 1],
+                      (float*)out[0].buffer->write_ptr(), n_out, current_stream()),
+          "hip::fir_filter_ccf");
+    _cur ^= 1;
+    ++_launches;
+    in[0].n_consumed = n_out * _decim;
+    out[0].n_produced = n_out;
+    return work_return_code_t::WORK_OK;
+}
+
+// ---- FFT ---------------------------------------------------------------------------
+fft_vcc::fft_vcc(size_t fft_size, bool forward) : sync_block(forward ? "fft_vcc (hip)" : "ifft_vcc (hip)"), _forward(forward)
+{
+    if (fft_size != 1024) throw std::invalid_argument("hip::fft_vcc: only 1024-point transforms are implemented");
+}
+
+work_return_code_t fft_vcc::work(std::vector<block_work_input>& in, std::vector<block_work_output>& out)
+{
+    check(nsh_fft1024_c2c((const float*)in[0].buffer->read_ptr(), (float*)out[0].buffer->write_ptr(), out[0].n_items,
+                          _forward ? 0 : 1, current_stream()),
+          "hip::fft_vcc");
+    out[0].n_produced = out[0].n_items;
+    return work_return_code_t::WORK_OK;
+}
+
+channelizer_vcc::channelizer_vcc(const std::vector<gr_complex>& w) : sync_block("channelizer_vcc (hip)"), _w(w)
+{
+    if (w.size() != 1024) throw std::invalid_argument("hip::channelizer_vcc: w must have 1024 bins");
+}
+channelizer_vcc::~channelizer_vcc()
+{
+    if (_wdev) nsh_free(_wdev);
+}
+bool channelizer_vcc::start()
+{
+    if (!_wdev) {
+        check(nsh_malloc(current_device(), _w.size() * sizeof(gr_complex), &_wdev), "hip::channelizer_vcc");
+        check(nsh_memcpy_async(_wdev, _w.data(), _w.size() * sizeof(gr_complex), NSH_H2D, current_stream()),
+              "hip::channelizer_vcc");
+        check(nsh_stream_sync(current_stream()), "hip::channelizer_vcc");
+    }
+    return sync_block::start();
+}
+work_return_code_t channelizer_vcc::work(std::vector<block_work_input>& in, std::vector<block_work_output>& out)
+{
+    check(nsh_channelizer1024((const float*)in[0].buffer->read_ptr(), (float*)out[0].buffer->write_ptr(),
+                              (const float*)_wdev, out[0].n_items, current_stream()),
+          "hip::channelizer_vcc");
+    out[0].n_produced = out[0].n_items;
+    return work_return_code_t::WORK_OK;
+}
+
+// ---- synthetic source ----------------------------------------------------------------
+work_return_code_t synth_source::work(std::vector<block_work_input>&, std::vector<block_work_output>& out)
+{
+    int64_t n = (int64_t)out[0].n_items * (int64_t)_vlen; // samples
+    if (_limit) {
+        const uint64_t left = _first + _limit - _index;
+        if (left == 0) {
+            out[0].n_produced = 0;
+            return work_return_code_t::WORK_DONE;
+        }
+        n = std::min<int64_t>(n, (int64_t)left);
+    }
+    check(nsh_synth_cf32((float*)out[0].buffer->write_ptr(), n, _index, _seed, current_stream()), "hip::synth_source");
+    _index += (uint64_t)n;
+    out[0].n_produced = (int)(n / (int64_t)_vlen);
+    if (_limit && _index >= _first + _limit) return work_return_code_t::WORK_DONE;
+    return work_return_code_t::WORK_OK;
+}
+
+} // namespace hip
+} // namespace gr

@@ -1,0 +1,150 @@
+// flowgraph + flowgraph_monitor (reference runtime/lib/flowgraph.cpp,
+// runtime/lib/flowgraph_monitor.cpp; drain-based completion, see flowgraph_monitor.hpp).
+#include <gnuradio/flowgraph.hpp>
+#include <gnuradio/graph_utils.hpp>
+
+#include <algorithm>
+
+namespace gr {
+
+// ---- flowgraph_monitor ---------------------------------------------------------------
+void flowgraph_monitor::push_message(fg_monitor_message msg)
+{
+    std::lock_guard<std::mutex> g(_m);
+    switch (msg.type()) {
+    case fg_monitor_message_t::DONE: ++_done_blocks; break;
+    case fg_monitor_message_t::FLUSHED: _flushed[msg.schedid()] = true; break;
+    case fg_monitor_message_t::KILL: _killed = true; break;
+    default: break;
+    }
+    _cv.notify_all();
+}
+
+void flowgraph_monitor::start()
+{
+    std::lock_guard<std::mutex> g(_m);
+    _flushed.clear();
+    _killed = false;
+    _done_blocks = 0;
+    _error = nullptr;
+}
+
+bool flowgraph_monitor::run_complete()
+{
+    for (auto& s : d_schedulers)
+        if (!_flushed.count(s->id())) return false;
+    return true;
+}
+
+void flowgraph_monitor::wait()
+{
+    std::unique_lock<std::mutex> l(_m);
+    _cv.wait(l, [this] { return _killed || run_complete(); });
+}
+
+void flowgraph_monitor::report_error(std::exception_ptr e)
+{
+    std::lock_guard<std::mutex> g(_m);
+    if (!_error) _error = e;
+}
+
+std::exception_ptr flowgraph_monitor::error()
+{
+    std::lock_guard<std::mutex> g(_m);
+    return _error;
+}
+
+uint64_t flowgraph_monitor::done_blocks()
+{
+    std::lock_guard<std::mutex> g(_m);
+    return _done_blocks;
+}
+
+bool flowgraph_monitor::replace_scheduler(std::shared_ptr<scheduler> original,
+                                          const std::vector<std::shared_ptr<scheduler>> replacements)
+{
+    std::lock_guard<std::mutex> g(_m);
+    auto it = std::find(d_schedulers.begin(), d_schedulers.end(), original);
+    if (it == d_schedulers.end()) return false;
+    d_schedulers.erase(it);
+    d_schedulers.insert(d_schedulers.end(), replacements.begin(), replacements.end());
+    return true;
+}
+
+// ---- flowgraph -------------------------------------------------------------------------
+flowgraph::~flowgraph()
+{
+    for (auto& s : d_schedulers) {
+        try {
+            s->stop();
+        } catch (...) {
+        }
+    }
+}
+
+void flowgraph::set_scheduler(scheduler_sptr s) { set_schedulers({ std::move(s) }); }
+void flowgraph::set_schedulers(std::vector<scheduler_sptr> s)
+{
+    d_schedulers = std::move(s);
+    int id = 1;
+    for (auto& x : d_schedulers) x->set_id(id++);
+}
+void flowgraph::add_scheduler(scheduler_sptr s)
+{
+    d_schedulers.push_back(std::move(s));
+    int id = 1;
+    for (auto& x : d_schedulers) x->set_id(id++);
+}
+void flowgraph::clear_schedulers() { d_schedulers.clear(); }
+
+void flowgraph::partition(std::vector<domain_conf>& confs)
+{
+    d_fgmon = std::make_shared<flowgraph_monitor>(d_schedulers);
+    auto parts = graph_utils::partition(base(), d_schedulers, confs);
+    d_flat_subgraphs.clear();
+    for (auto& p : parts) {
+        d_flat_subgraphs.push_back(flat_graph::make_flat(p.subgraph));
+        p.scheduler->initialize(d_flat_subgraphs.back(), d_fgmon, p.neighbor_map);
+    }
+}
+
+void flowgraph::validate()
+{
+    if (d_schedulers.empty()) throw std::runtime_error("flowgraph::validate: no scheduler specified");
+    d_fgmon = std::make_shared<flowgraph_monitor>(d_schedulers);
+    d_flat_graph = flat_graph::make_flat(base());
+    for (auto& s : d_schedulers) s->initialize(d_flat_graph, d_fgmon);
+}
+
+void flowgraph::start()
+{
+    if (d_schedulers.empty()) throw std::runtime_error("No Scheduler Specified.");
+    if (!d_fgmon) validate();
+    d_fgmon->start();
+    for (auto& s : d_schedulers) s->start();
+    d_started = true;
+}
+
+void flowgraph::stop()
+{
+    for (auto& s : d_schedulers) s->stop();
+    if (d_fgmon) d_fgmon->stop();
+    d_started = false;
+}
+
+void flowgraph::wait()
+{
+    if (!d_started) return;
+    d_fgmon->wait();
+    for (auto& s : d_schedulers) s->wait();
+    d_started = false;
+    if (auto e = d_fgmon->error()) std::rethrow_exception(e);
+}
+
+void flowgraph::run()
+{
+    start();
+    wait();
+}
+
+} // namespace gr

@@ -1,0 +1,47 @@
+// GPU scheduler domain (see scheduler_hip.hpp).
+#include <gnuradio/hip_context.hpp>
+#include <gnuradio/schedulers/hip/scheduler_hip.hpp>
+
+#include "nsh_hip.h"
+
+namespace gr {
+namespace schedulers {
+
+scheduler_hip::scheduler_hip(const std::string name, int device, size_t fixed_buf_size)
+    : scheduler_mt(name, fixed_buf_size), _device(device)
+{
+    hip::check(nsh_stream_create(device, &_stream), "scheduler_hip: stream");
+    _default_buf_factory = hip_buffer::make;
+    _default_buf_properties = hip_buffer_properties::make(hip_buffer_type::D2D, device);
+}
+
+scheduler_hip::~scheduler_hip()
+{
+    for (auto& t : _threads) t->stop(); // threads use the stream: stop them first
+    _threads.clear();
+    if (_stream) {
+        nsh_stream_sync(_stream);
+        nsh_stream_destroy(_stream);
+    }
+}
+
+std::vector<block_group_properties> scheduler_hip::plan_groups(flat_graph_sptr fg)
+{
+    // The whole partition is one group, producers first.
+    auto order = fg->topological_sort(fg->calc_used_blocks());
+    if (order.empty()) return {};
+    return { block_group_properties(order, name()) };
+}
+
+thread_hooks scheduler_hip::hooks_for_group(const block_group_properties&)
+{
+    thread_hooks h;
+    const int dev = _device;
+    void* s = _stream;
+    h.on_thread_start = [dev, s] { hip::bind_thread(dev, s); };
+    h.on_flush = [s] { hip::check(nsh_stream_sync(s), "scheduler_hip: flush"); };
+    return h;
+}
+
+} // namespace schedulers
+} // namespace gr

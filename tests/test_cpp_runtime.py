@@ -1,0 +1,33 @@
+"""Run the C++ behaviour tests (tests/cpp/*.cpp, built by `make tests`): the reference's
+own scheduler_mt gtests restated against this runtime (CPU), and the GPU flowgraph
+tests through scheduler_hip / hip_buffer / gr::hip blocks (GPU)."""
+import os
+import subprocess
+
+import pytest
+
+from tests.conftest import ROOT
+
+BIN = os.path.join(ROOT, "build", "tests")
+
+
+def run(name, timeout):
+    exe = os.path.join(BIN, name)
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-s", "-C", ROOT, "tests"], check=True)
+    p = subprocess.run([exe], capture_output=True, text=True, timeout=timeout)
+    print(p.stdout)
+    print(p.stderr)
+    assert p.returncode == 0, p.stdout + p.stderr
+    return p.stdout
+
+
+def test_scheduler_mt_behaviour():
+    out = run("qa_scheduler_mt", 600)
+    assert "0 failure(s)" in out
+
+
+@pytest.mark.gpu
+def test_hip_flowgraphs():
+    out = run("qa_hip_flowgraph", 900)
+    assert "0 failure(s)" in out
