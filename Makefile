@@ -16,7 +16,7 @@ CXXFLAGS := -O3 -std=c++17 -fPIC -Wall -Wextra -Wno-unused-parameter -pthread \
 HIP_SRC  := $(wildcard newsched_amd/csrc/*.hip)
 HIP_OBJ  := $(patsubst newsched_amd/csrc/%.hip,$(OBJDIR)/hip/%.o,$(HIP_SRC))
 RT_SRC   := $(wildcard newsched_amd/runtime/lib/*.cpp) $(wildcard newsched_amd/schedulers/lib/*.cpp) \
-            $(wildcard newsched_amd/blocklib/lib/*.cpp)
+            $(wildcard newsched_amd/blocklib/lib/*.cpp) $(wildcard newsched_amd/capi/*.cpp)
 RT_OBJ   := $(patsubst newsched_amd/%.cpp,$(OBJDIR)/rt/%.o,$(RT_SRC))
 RT_HDR   := $(shell find newsched_amd/runtime/include newsched_amd/schedulers/include newsched_amd/blocklib/include -name '*.hpp' 2>/dev/null)
 TEST_SRC := $(wildcard tests/cpp/*.cpp)

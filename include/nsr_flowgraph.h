@@ -1,0 +1,51 @@
+/*
+ * nsr_flowgraph.h -- C-ABI of libnewsched.so's flowgraph runners: the BASELINE
+ * configurations built from the C++ runtime (gr::flowgraph + scheduler_hip / scheduler_mt
+ * + hip_buffer + gr::hip blocks), for bench.py, smoke() and the Python tests. The blocks
+ * and buffers themselves are C++ (newsched_amd/runtime, schedulers, blocklib); this header
+ * only exposes whole-flowgraph entry points with POD arguments.
+ *
+ * Returns 0 on success, nonzero on failure (text in nsr_last_error()); never throws.
+ */
+#ifndef NSR_FLOWGRAPH_H
+#define NSR_FLOWGRAPH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+const char* nsr_last_error(void);
+
+/* C3 measurement flowgraph on GPU `dev` (one scheduler_hip domain):
+ *   nop_source -> nop_head(n) -> [hip_buffer ring of 2n items, PRELOADED with the synthetic
+ *   stream x[first_index .. first_index+n) before any run] -> hip::fir_filter_ccf(taps, algo)
+ *   -> [hip_buffer D2D, 2*out_buf_bytes] -> null_sink
+ * nop_source/nop_head produce items without touching memory (reference blocklib/blocks/
+ * include/gnuradio/blocklib/blocks/nop_source.hpp, nop_head.hpp), so each run streams the
+ * HBM-resident input through the FIR's work() calls exactly once. With first_index > 0 the
+ * FIR starts with the ntaps-1 preceding samples as history (a time shard's halo,
+ * regenerated from the counter-based source). n must be a multiple of 256. */
+int nsr_fir_bench_create(int dev, const float* taps, int ntaps, int algo, int64_t n, uint64_t first_index,
+                         uint64_t seed, size_t out_buf_bytes, int timing, void** handle);
+int nsr_fir_bench_run(void* handle); /* one run (start + wait); rethrown work() errors -> rc */
+/* Over the last run: summed FIR kernel time from HIP events around each launch on the
+ * partition stream, FIR launches, samples, and the algorithm the plan resolved to. */
+int nsr_fir_bench_stats(void* handle, double* kernel_ms, uint64_t* launches, uint64_t* samples, int* algo);
+/* The last `count` FIR outputs of the last run (interleaved re,im fp32) -> host. */
+int nsr_fir_bench_tail(void* handle, int64_t count, float* out_host);
+int nsr_fir_bench_destroy(void* handle);
+
+/* CPU baseline: the reference scheduler_mt CPU path restated -- thread per block,
+ * vmcircbuf edges of 2*fixed_buf_size bytes (reference default 32768):
+ *   vector_source(x[0..nx), repeat) -> head(n) -> blocks::fir_filter_ccf -> null_sink
+ * *seconds = wall time of fg->run() (threads already created). */
+int nsr_cpu_fir_run(const float* taps, int ntaps, const float* x, int64_t nx, int64_t n, size_t fixed_buf_size,
+                    double* seconds);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NSR_FLOWGRAPH_H */

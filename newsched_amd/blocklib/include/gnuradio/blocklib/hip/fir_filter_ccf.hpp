@@ -29,8 +29,24 @@ public:
     int algo() const; // resolved algorithm (after start())
     uint64_t launches() const { return _launches; }
 
+    // History loaded at start() instead of zeros: the ntaps-1 samples that precede this
+    // block's first input (a time shard's halo, regenerated or received by the caller).
+    void set_initial_history(const std::vector<gr_complex>& h) { _init_hist = h; }
+
+    // Per-launch kernel timing with HIP events on the launch stream (bench/profiling).
+    void enable_timing(bool on) { _timing = on; }
+    // Sum of kernel durations (ms) and output samples over the launches of the last run;
+    // synchronises on the recorded events.
+    double kernel_ms();
+    uint64_t timed_samples() const { return _timed_samples; }
+
 private:
     void release();
+    std::vector<gr_complex> _init_hist;
+    bool _timing = false;
+    std::vector<std::pair<void*, void*>> _ev;  // (start, stop) per launch, reused
+    size_t _ev_used = 0;
+    uint64_t _timed_samples = 0;
     std::vector<float> _taps;
     int _decim, _algo;
     int _dev = -1;

@@ -97,6 +97,12 @@ fir_filter_ccf::~fir_filter_ccf() { release(); }
 
 void fir_filter_ccf::release()
 {
+    for (auto& e : _ev) {
+        nsh_event_destroy(e.first);
+        nsh_event_destroy(e.second);
+    }
+    _ev.clear();
+    _ev_used = 0;
     if (_plan) nsh_fir_plan_destroy(_plan);
     for (auto& h : _hist)
         if (h) nsh_free(h);
@@ -120,7 +126,15 @@ bool fir_filter_ccf::start()
     void* s = current_stream();
     check(nsh_memset_async(_hist[0], 0, hbytes, s), "hip::fir_filter_ccf history reset");
     check(nsh_memset_async(_hist[1], 0, hbytes, s), "hip::fir_filter_ccf history reset");
+    if (!_init_hist.empty()) {
+        if (_init_hist.size() != _taps.size() - 1)
+            throw std::invalid_argument("hip::fir_filter_ccf: initial history must have ntaps-1 samples");
+        check(nsh_memcpy_async(_hist[0], _init_hist.data(), hbytes, NSH_H2D, s), "hip::fir_filter_ccf history load");
+        check(nsh_stream_sync(s), "hip::fir_filter_ccf history load"); // host vector must outlive the copy
+    }
     _cur = 0;
+    _ev_used = 0;
+    _timed_samples = 0;
     return block::start();
 }
 
@@ -128,14 +142,42 @@ work_return_code_t fir_filter_ccf::work(std::vector<block_work_input>& in, std::
 {
     const int n_out = std::min(out[0].n_items, in[0].n_items / _decim);
     if (n_out <= 0) return work_return_code_t::WORK_INSUFFICIENT_INPUT_ITEMS;
+    void* s = current_stream();
+    std::pair<void*, void*>* ev = nullptr;
+    if (_timing) {
+        if (_ev_used == _ev.size()) {
+            std::pair<void*, void*> p{ nullptr, nullptr };
+            check(nsh_event_create(&p.first), "hip::fir_filter_ccf timing");
+            check(nsh_event_create(&p.second), "hip::fir_filter_ccf timing");
+            _ev.push_back(p);
+        }
+        ev = &_ev[_ev_used++];
+        check(nsh_event_record(ev->first, s), "hip::fir_filter_ccf timing");
+    }
     check(nsh_fir_ccf(_plan, (const float*)in[0].buffer->read_ptr(), (const float*)_hist[_cur], (float*)_hist[_cur ^ 1],
-                      (float*)out[0].buffer->write_ptr(), n_out, current_stream()),
+                      (float*)out[0].buffer->write_ptr(), n_out, s),
           "hip::fir_filter_ccf");
+    if (ev) {
+        check(nsh_event_record(ev->second, s), "hip::fir_filter_ccf timing");
+        _timed_samples += (uint64_t)n_out;
+    }
     _cur ^= 1;
     ++_launches;
     in[0].n_consumed = n_out * _decim;
     out[0].n_produced = n_out;
     return work_return_code_t::WORK_OK;
+}
+
+double fir_filter_ccf::kernel_ms()
+{
+    double total = 0;
+    for (size_t i = 0; i < _ev_used; ++i) {
+        float ms = 0;
+        check(nsh_event_sync(_ev[i].second), "hip::fir_filter_ccf timing");
+        check(nsh_event_elapsed_ms(_ev[i].first, _ev[i].second, &ms), "hip::fir_filter_ccf timing");
+        total += ms;
+    }
+    return total;
 }
 
 // ---- FFT ---------------------------------------------------------------------------

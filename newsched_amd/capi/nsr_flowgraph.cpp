@@ -1,0 +1,179 @@
+// libnewsched.so flowgraph runners (include/nsr_flowgraph.h).
+#include "nsr_flowgraph.h"
+
+#include <chrono>
+#include <cstring>
+#include <gnuradio/blocklib/blocks/fir_filter_ccf.hpp>
+#include <gnuradio/blocklib/blocks/head.hpp>
+#include <gnuradio/blocklib/blocks/nop.hpp>
+#include <gnuradio/blocklib/blocks/null_sink.hpp>
+#include <gnuradio/blocklib/blocks/vector_source.hpp>
+#include <gnuradio/blocklib/hip/fir_filter_ccf.hpp>
+#include <gnuradio/flowgraph.hpp>
+#include <gnuradio/hip_buffer.hpp>
+#include <gnuradio/hip_context.hpp>
+#include <gnuradio/schedulers/hip/scheduler_hip.hpp>
+#include <gnuradio/schedulers/mt/scheduler_mt.hpp>
+#include <gnuradio/vmcircbuf.hpp>
+#include <string>
+
+#include "nsh_hip.h"
+
+using namespace gr;
+
+namespace {
+thread_local std::string t_err;
+
+template <class F>
+int guarded(F&& f)
+{
+    try {
+        f();
+        t_err.clear();
+        return 0;
+    } catch (const std::exception& e) {
+        t_err = e.what();
+    } catch (...) {
+        t_err = "unknown exception";
+    }
+    return -1;
+}
+
+uint64_t splitmix64(uint64_t x)
+{
+    x += 0x9E3779B97F4A7C15ull;
+    uint64_t z = x;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+gr_complex synth_at(uint64_t i, uint64_t seed)
+{
+    const uint64_t g = 2 * i;
+    return gr_complex((float)(int)(splitmix64(seed ^ g) >> 40) * (1.0f / 8388608.0f) - 1.0f,
+                      (float)(int)(splitmix64(seed ^ (g + 1)) >> 40) * (1.0f / 8388608.0f) - 1.0f);
+}
+
+struct fir_bench {
+    flowgraph::sptr fg;
+    schedulers::scheduler_hip::sptr sched;
+    hip::fir_filter_ccf::sptr fir;
+    std::shared_ptr<hip_buffer> out_ring;
+    int dev = 0;
+};
+} // namespace
+
+extern "C" {
+
+const char* nsr_last_error(void) { return t_err.c_str(); }
+
+int nsr_fir_bench_create(int dev, const float* taps, int ntaps, int algo, int64_t n, uint64_t first_index,
+                         uint64_t seed, size_t out_buf_bytes, int timing, void** handle)
+{
+    return guarded([&] {
+        if (n <= 0 || n % 256) throw std::invalid_argument("nsr_fir_bench_create: n must be a positive multiple of 256");
+        auto b = new fir_bench();
+        b->dev = dev;
+        const size_t isz = sizeof(gr_complex);
+        auto src = blocks::nop_source::make(isz);
+        auto head = blocks::nop_head::make(isz, (size_t)n);
+        b->fir = hip::fir_filter_ccf::make(std::vector<float>(taps, taps + ntaps), 1, algo);
+        b->fir->enable_timing(timing != 0);
+        if (first_index > 0) {
+            std::vector<gr_complex> h((size_t)ntaps - 1);
+            for (size_t j = 0; j < h.size(); ++j) h[j] = synth_at(first_index - h.size() + j, seed);
+            b->fir->set_initial_history(h);
+        }
+        auto snk = blocks::null_sink::make(isz);
+        b->fg = flowgraph::make();
+        // the nop edge is never touched: a host ring costs no memory traffic
+        b->fg->connect(src, 0, head, 0)->set_custom_buffer(VMCIRC_BUFFER_ARGS);
+        // the resident input ring: exactly 2n items so every run starts on a copy of x
+        const int64_t cap = 2 * n;
+        b->fg->connect(head, 0, b->fir, 0)
+            ->set_custom_buffer(
+                [cap, dev](size_t, size_t item, std::shared_ptr<buffer_properties>) -> buffer_sptr {
+                    return std::make_shared<hip_buffer>((size_t)cap, item, hip_buffer_type::D2D, dev);
+                },
+                hip_buffer_properties::make(hip_buffer_type::D2D, dev));
+        b->fg->connect(b->fir, 0, snk, 0); // scheduler default: hip_buffer D2D
+        b->sched = schedulers::scheduler_hip::make("hip" + std::to_string(dev), dev, out_buf_bytes);
+        b->fg->set_scheduler(b->sched);
+        b->fg->validate();
+
+        auto in_ring = std::dynamic_pointer_cast<hip_buffer>(b->sched->buffers()->get_input_buffer(b->fir->input_stream_ports()[0]));
+        b->out_ring = std::dynamic_pointer_cast<hip_buffer>(b->sched->buffers()->get_input_buffer(snk->input_stream_ports()[0]));
+        if (!in_ring || !b->out_ring) throw std::runtime_error("nsr_fir_bench_create: unexpected buffer types");
+        if ((int64_t)in_ring->capacity() != cap) throw std::runtime_error("nsr_fir_bench_create: ring capacity mismatch");
+        void* s = nullptr;
+        hip::check(nsh_stream_create(dev, &s), "nsr: stream");
+        char* base = (char*)in_ring->device_base();
+        hip::check(nsh_synth_cf32((float*)base, n, first_index, seed, s), "nsr: preload");
+        hip::check(nsh_synth_cf32((float*)(base + n * isz), n, first_index, seed, s), "nsr: preload");
+        hip::check(nsh_stream_sync(s), "nsr: preload");
+        nsh_stream_destroy(s);
+        *handle = b;
+    });
+}
+
+int nsr_fir_bench_run(void* handle)
+{
+    return guarded([&] { static_cast<fir_bench*>(handle)->fg->run(); });
+}
+
+int nsr_fir_bench_stats(void* handle, double* kernel_ms, uint64_t* launches, uint64_t* samples, int* algo)
+{
+    return guarded([&] {
+        auto b = static_cast<fir_bench*>(handle);
+        if (kernel_ms) *kernel_ms = b->fir->kernel_ms();
+        if (launches) *launches = b->fir->launches();
+        if (samples) *samples = b->fir->timed_samples();
+        if (algo) *algo = b->fir->algo();
+    });
+}
+
+int nsr_fir_bench_tail(void* handle, int64_t count, float* out_host)
+{
+    return guarded([&] {
+        auto b = static_cast<fir_bench*>(handle);
+        auto r = b->out_ring;
+        if (count <= 0 || (size_t)count > r->capacity() / 2) throw std::invalid_argument("nsr_fir_bench_tail: bad count");
+        const uint64_t end = r->total_written();
+        const uint64_t start = end - (uint64_t)count;
+        const char* src = (const char*)r->device_base() + (start % r->capacity()) * r->item_size();
+        void* s = nullptr;
+        hip::check(nsh_stream_create(b->dev, &s), "nsr: stream");
+        hip::check(nsh_memcpy_async(out_host, src, (size_t)count * r->item_size(), NSH_D2H, s), "nsr: tail copy");
+        hip::check(nsh_stream_sync(s), "nsr: tail copy");
+        nsh_stream_destroy(s);
+    });
+}
+
+int nsr_fir_bench_destroy(void* handle)
+{
+    return guarded([&] { delete static_cast<fir_bench*>(handle); });
+}
+
+int nsr_cpu_fir_run(const float* taps, int ntaps, const float* x, int64_t nx, int64_t n, size_t fixed_buf_size,
+                    double* seconds)
+{
+    return guarded([&] {
+        std::vector<gr_complex> xv((const gr_complex*)x, (const gr_complex*)x + nx);
+        auto src = blocks::vector_source_c::make(xv, true);
+        auto head = blocks::head::make(sizeof(gr_complex), (size_t)n);
+        auto fir = blocks::fir_filter_ccf::make(std::vector<float>(taps, taps + ntaps), 1);
+        auto snk = blocks::null_sink::make(sizeof(gr_complex));
+        auto fg = flowgraph::make();
+        fg->connect(src, 0, head, 0);
+        fg->connect(head, 0, fir, 0);
+        fg->connect(fir, 0, snk, 0);
+        fg->set_scheduler(schedulers::scheduler_mt::make("mt", (unsigned)fixed_buf_size));
+        fg->validate();
+        const auto t0 = std::chrono::steady_clock::now();
+        fg->run();
+        *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (snk->consumed() != (uint64_t)n) throw std::runtime_error("nsr_cpu_fir_run: short run");
+    });
+}
+
+} // extern "C"

@@ -1,0 +1,97 @@
+"""ctypes binding of libnewsched.so's flowgraph runners (include/nsr_flowgraph.h).
+
+The flowgraphs are built and run by the C++ runtime (gr::flowgraph, scheduler_hip,
+hip_buffer, gr::hip blocks); Python only passes POD arguments."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import nsh
+
+RT_LIB = os.path.join(nsh.LIB_DIR, "libnewsched.so")
+_lib = None
+
+_vp, _i, _i64, _u64, _sz, _d = C.c_void_p, C.c_int, C.c_int64, C.c_uint64, C.c_size_t, C.c_double
+SIGNATURES = {
+    "nsr_last_error": (C.c_char_p, []),
+    "nsr_fir_bench_create": (_i, [_i, C.POINTER(C.c_float), _i, _i, _i64, _u64, _u64, _sz, _i, C.POINTER(_vp)]),
+    "nsr_fir_bench_run": (_i, [_vp]),
+    "nsr_fir_bench_stats": (_i, [_vp, C.POINTER(_d), C.POINTER(_u64), C.POINTER(_u64), C.POINTER(_i)]),
+    "nsr_fir_bench_tail": (_i, [_vp, _i64, C.POINTER(C.c_float)]),
+    "nsr_fir_bench_destroy": (_i, [_vp]),
+    "nsr_cpu_fir_run": (_i, [C.POINTER(C.c_float), _i, C.POINTER(C.c_float), _i64, _i64, _sz, C.POINTER(_d)]),
+}
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        nsh.lib()  # libnsh_hip.so first (RTLD_GLOBAL)
+        if not os.path.exists(RT_LIB):
+            raise nsh.NshError(f"{RT_LIB} is missing: run `make runtime` (or __graft_entry__.build())")
+        L = C.CDLL(RT_LIB, mode=C.RTLD_GLOBAL)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc, what):
+    if rc != 0:
+        raise nsh.NshError(f"{what} failed: {lib().nsr_last_error().decode(errors='replace')}")
+
+
+def _f32p(a):
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+class FirBench:
+    """C3 measurement flowgraph (see nsr_fir_bench_create)."""
+
+    def __init__(self, taps, n, device=0, algo=nsh.FIR_AUTO, first_index=0, seed=0x6E736368,
+                 out_buf_bytes=256 << 20, timing=True):
+        t = np.ascontiguousarray(np.asarray(taps, np.float32))
+        self.ntaps, self.n = int(t.size), int(n)
+        h = C.c_void_p()
+        check(lib().nsr_fir_bench_create(device, _f32p(t), self.ntaps, algo, self.n, first_index, seed,
+                                         out_buf_bytes, 1 if timing else 0, C.byref(h)), "nsr_fir_bench_create")
+        self._h = h
+
+    def run(self):
+        check(lib().nsr_fir_bench_run(self._h), "nsr_fir_bench_run")
+
+    def stats(self):
+        ms, la, sa, al = C.c_double(), C.c_uint64(), C.c_uint64(), C.c_int()
+        check(lib().nsr_fir_bench_stats(self._h, C.byref(ms), C.byref(la), C.byref(sa), C.byref(al)),
+              "nsr_fir_bench_stats")
+        return {"kernel_ms": ms.value, "launches": la.value, "samples": sa.value, "algo": al.value}
+
+    def tail(self, count):
+        out = np.empty(count, np.complex64)
+        check(lib().nsr_fir_bench_tail(self._h, count, _f32p(out.view(np.float32))), "nsr_fir_bench_tail")
+        return out
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().nsr_fir_bench_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def cpu_fir_run(taps, x, n, fixed_buf_size=32768) -> float:
+    t = np.ascontiguousarray(np.asarray(taps, np.float32))
+    xv = np.ascontiguousarray(np.asarray(x, np.complex64))
+    s = C.c_double()
+    check(lib().nsr_cpu_fir_run(_f32p(t), t.size, _f32p(xv.view(np.float32)), xv.size, int(n), fixed_buf_size,
+                                C.byref(s)), "nsr_cpu_fir_run")
+    return s.value
