@@ -171,7 +171,7 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": None,
-            "kernel": "k_fir_mfma<5>" if algo_used == "mfma" else "k_fir_direct<1,8>",
+            "kernel": "k_fir_mfma2<5,2>" if algo_used == "mfma" else "k_fir_direct<1,8>",
             "avg_launch_us": round(avg_launch_ms * 1e3, 2),
             "algorithmic_bytes_per_launch": int(BYTES_PER_SAMPLE * per_launch_samples),
             "kernel_gflops": round(FLOP_PER_SAMPLE * per_launch_samples / (avg_launch_ms * 1e-3) / 1e9, 1),

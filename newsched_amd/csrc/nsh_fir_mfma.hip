@@ -7,7 +7,10 @@
 //     B[k][i]   = h[i - r + 32 q]           (zero outside [0, L))           -- the taps
 // One v_mfma_f32_32x32x16_bf16 covers 32 rows (16 blocks x {re, im}) x 32 phases x 16 k;
 // a wave owns a 512-sample tile and runs 2Q k-steps. Q = 5 for L = 127 (K = 160: 26 %
-// zero padding, irrelevant because the kernel is HBM-bound with ~2x matrix-core slack).
+// zero padding). Cost: 3840 bf16 FLOP per output sample, i.e. 51 us of dense MFMA issue
+// per 2^25 samples at 2.4 GHz (60 us at the 2.05 GHz the chip holds under this load), against
+// 91 us for the HBM stream at the measured copy rate: the matrix cores are not free here,
+// and overlapping them with the stream is what the v2 pipeline below is about.
 //
 // Precision: fp32 emulated by a 3-term bf16 split of both operands (x = x1 + x2 + x3 and
 // h = h1 + h2 + h3, each split exact for finite normal fp32) and the six products with
@@ -17,10 +20,12 @@
 // bf16 keeps the fp32 exponent range, so no input scaling is needed. Non-finite inputs
 // are not supported by this form (use NSH_FIR_DIRECT).
 //
-// Data movement: a 256-thread workgroup walks a contiguous range of 2048-output chunks.
-// Each chunk's 2048 + 32(Q-1) input samples are loaded with 16-byte global loads into
-// registers one chunk ahead (overlapping the MFMAs of the current chunk), split, and
-// written as six bf16 planes (re/im x 3 terms) to LDS, with every 32-sample row padded to
+// Data movement (v2, the default; v1 below is kept for A/B runs): a 256-thread workgroup
+// (2 per CU) walks a contiguous range of 2048-output chunks. Each chunk's 2048 samples are
+// loaded with 16-byte nontemporal global loads into registers two chunks ahead, split, and
+// written as six bf16 planes (re/im x 3 terms) to one of two LDS buffers while the MFMAs
+// read the other; the 32(Q-1)-sample halo is the previous chunk's tail, copied LDS -> LDS.
+// Every 32-sample row is padded to
 // 80 B so the per-lane ds_read_b128 A-fragment reads are bank-conflict free (lanes of one
 // 16-lane group read 16 distinct 16-B slots: 5*beta mod 16 is a bijection). The taps'
 // B fragments (3 terms x 2Q k-steps, prepared on the host in lane order) stay in VGPRs for
@@ -28,10 +33,17 @@
 // of a store cover 32 consecutive samples (256 contiguous bytes).
 #include "nsh_common.hpp"
 
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
 #include "nsh_fir_plan.hpp"
+
+// Ablation hooks for tools/probe/fir_ablate.sh only (bit mask; 0 in every product build):
+// 1 = no MFMA, 2 = no global loads, 4 = no bf16 split, 8 = no global stores.
+#ifndef NSH_FIR_ABLATE
+#define NSH_FIR_ABLATE 0
+#endif
 
 namespace {
 
@@ -40,13 +52,15 @@ typedef __attribute__((ext_vector_type(16))) float f32x16;
 typedef float nf4 __attribute__((ext_vector_type(4)));
 typedef float nf2 __attribute__((ext_vector_type(2)));
 
-constexpr int NT = 256;     // threads per workgroup (4 waves)
 constexpr int TILE = 512;   // outputs per wave per chunk
-constexpr int CHUNK = 2048; // outputs per workgroup per chunk
 constexpr int QMAX = 6;     // L <= 161
 
-template <int Q>
+// NW waves per workgroup (one 512-output tile each); DEPTH chunks of input in flight
+// per workgroup (register prefetch).
+template <int Q, int NW = 4>
 struct geom {
+    static constexpr int NT = 64 * NW;                        // threads per workgroup
+    static constexpr int CHUNK = TILE * NW;                   // outputs per chunk
     static constexpr int S = 2 * Q;                           // k-steps of 16
     static constexpr int H = 32 * (Q - 1);                    // halo samples
     static constexpr int NS = CHUNK + H;                      // staged samples per chunk
@@ -78,8 +92,8 @@ __device__ __forceinline__ float2 virt(const float2* __restrict__ in, const floa
     return make_float2(0.f, 0.f);
 }
 
-template <int Q>
-__device__ __forceinline__ void stage_load(float4 (&v)[geom<Q>::VPT],
+template <int Q, int NW, int NV_>
+__device__ __forceinline__ void stage_load(float4 (&v)[NV_],
                                            const float2* __restrict__ in,
                                            const float2* __restrict__ hist,
                                            int64_t chunk,
@@ -87,8 +101,9 @@ __device__ __forceinline__ void stage_load(float4 (&v)[geom<Q>::VPT],
                                            int L,
                                            bool in_aligned)
 {
-    using G = geom<Q>;
-    const int64_t g0 = chunk * CHUNK - G::H;
+    using G = geom<Q, NW>;
+    constexpr int NT = G::NT;
+    const int64_t g0 = chunk * G::CHUNK - G::H;
     const bool interior = in_aligned && g0 >= 0 && g0 + G::NS <= n_in;
     if (interior) {
         const float4* src = reinterpret_cast<const float4*>(in + g0);
@@ -113,10 +128,11 @@ __device__ __forceinline__ void stage_load(float4 (&v)[geom<Q>::VPT],
     }
 }
 
-template <int Q>
-__device__ __forceinline__ void stage_store(const float4 (&v)[geom<Q>::VPT], unsigned char* lds)
+template <int Q, int NW, int NV_>
+__device__ __forceinline__ void stage_store(const float4 (&v)[NV_], unsigned char* lds)
 {
-    using G = geom<Q>;
+    using G = geom<Q, NW>;
+    constexpr int NT = G::NT;
 #pragma unroll
     for (int u = 0; u < G::VPT; ++u) {
         const int vi = threadIdx.x + NT * u;
@@ -138,18 +154,69 @@ __device__ __forceinline__ void stage_store(const float4 (&v)[geom<Q>::VPT], uns
     }
 }
 
-template <int Q>
-__global__ __launch_bounds__(NT, 2) void k_fir_mfma(const float2* __restrict__ in,
-                                                    const float2* __restrict__ hist_in,
-                                                    float2* __restrict__ hist_out,
-                                                    float2* __restrict__ out,
-                                                    const bf16x8* __restrict__ frag, // [3][S][64]
-                                                    int L,
-                                                    int64_t n_out,
-                                                    int in_aligned)
+template <int Q, int NW, int PLANE_ = geom<Q, NW>::PLANE>
+__device__ __forceinline__ void compute_tile(const unsigned char* lds,
+                                             const bf16x8 (&B0)[2 * Q],
+                                             const bf16x8 (&B1)[2 * Q],
+                                             const bf16x8 (&B2)[2 * Q],
+                                             int a_base,
+                                             int64_t n_tile,
+                                             int h,
+                                             int phase,
+                                             int64_t n_out,
+                                             float2* __restrict__ out)
 {
-    using G = geom<Q>;
+    constexpr int S_ = 2 * Q;
+    f32x16 acc_hi = {};
+    f32x16 acc_lo = {};
+#pragma unroll
+    for (int st = 0; st < S_; ++st) {
+        const int q = st >> 1;
+        const int off = a_base - q * 80 + 32 * (st & 1);
+        const bf16x8 A0 = *reinterpret_cast<const bf16x8*>(lds + off);
+        const bf16x8 A1 = *reinterpret_cast<const bf16x8*>(lds + off + PLANE_);
+        const bf16x8 A2 = *reinterpret_cast<const bf16x8*>(lds + off + 2 * PLANE_);
+#if NSH_FIR_ABLATE & 1
+        acc_hi[st & 15] += (float)A0[0] + (float)A1[1] + (float)A2[2] + (float)B0[st][0] + (float)B1[st][1] + (float)B2[st][2];
+        continue;
+#endif
+        acc_hi = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0, B0[st], acc_hi, 0, 0, 0);
+        acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0, B1[st], acc_lo, 0, 0, 0);
+        acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1, B0[st], acc_lo, 0, 0, 0);
+        acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0, B2[st], acc_lo, 0, 0, 0);
+        acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1, B1[st], acc_lo, 0, 0, 0);
+        acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A2, B0[st], acc_lo, 0, 0, 0);
+    }
+#pragma unroll
+    for (int reg = 0; reg < 8; ++reg) {
+        const int blk = (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        const int64_t n = n_tile + 32 * blk + phase;
+        const float re = acc_hi[reg] + acc_lo[reg];
+        const float im = acc_hi[reg + 8] + acc_lo[reg + 8];
+#if NSH_FIR_ABLATE & 8
+        if (re == 1.2345e-30f && n < n_out) {
+#else
+        if (n < n_out) {
+#endif
+            nf2 o = { re, im };
+            __builtin_nontemporal_store(o, reinterpret_cast<nf2*>(out + n));
+        }
+    }
+}
+
+template <int Q, int NW, int DEPTH>
+__global__ __launch_bounds__(64 * NW, (NW >= 8 ? 2 : 2)) void k_fir_mfma(const float2* __restrict__ in,
+                                                                       const float2* __restrict__ hist_in,
+                                                                       float2* __restrict__ hist_out,
+                                                                       float2* __restrict__ out,
+                                                                       const bf16x8* __restrict__ frag, // [3][S][64]
+                                                                       int L,
+                                                                       int64_t n_out,
+                                                                       int in_aligned)
+{
+    using G = geom<Q, NW>;
     constexpr int S = G::S;
+    constexpr int NT = G::NT;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
 
     const int tid = threadIdx.x;
@@ -170,7 +237,7 @@ __global__ __launch_bounds__(NT, 2) void k_fir_mfma(const float2* __restrict__ i
         B2[st] = frag[(2 * S + st) * 64 + lane];
     }
 
-    const int64_t nchunks = (n_out + CHUNK - 1) / CHUNK;
+    const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
     const int64_t per = (nchunks + gridDim.x - 1) / gridDim.x;
     const int64_t c_begin = (int64_t)blockIdx.x * per;
     const int64_t c_end = c_begin + per < nchunks ? c_begin + per : nchunks;
@@ -184,45 +251,350 @@ __global__ __launch_bounds__(NT, 2) void k_fir_mfma(const float2* __restrict__ i
     const int a_base = c * 3 * G::PLANE + ((Q - 1) + 16 * wave + b) * 80 + 16 * h; // bytes, k-step 0
     // Output addressing: C[row][col], col = lane&31 = phase, row = (reg&3) + 8(reg>>2) + 4h.
     const int phase = lane & 31;
+    const bool al = in_aligned != 0;
 
-    float4 v[G::VPT];
-    stage_load<Q>(v, in, hist_in, c_begin, n_in, L, in_aligned != 0);
+    float4 va[G::VPT];
+    float4 vb[G::VPT];
+    stage_load<Q, NW>(va, in, hist_in, c_begin, n_in, L, al);
+    if constexpr (DEPTH > 1) {
+        if (c_begin + 1 < c_end) stage_load<Q, NW>(vb, in, hist_in, c_begin + 1, n_in, L, al);
+    }
 
-    for (int64_t ch = c_begin; ch < c_end; ++ch) {
+    for (int64_t ch = c_begin; ch < c_end; ch += DEPTH) {
+        // chunk ch from va
         if (ch != c_begin) __syncthreads(); // previous chunk's fragment reads are done
-        stage_store<Q>(v, lds);
+        stage_store<Q, NW>(va, lds);
         __syncthreads();
-        if (ch + 1 < c_end) stage_load<Q>(v, in, hist_in, ch + 1, n_in, L, in_aligned != 0);
-
-        f32x16 acc_hi = {};
-        f32x16 acc_lo = {};
-#pragma unroll
-        for (int st = 0; st < S; ++st) {
-            const int q = st >> 1;
-            const int off = a_base - q * 80 + 32 * (st & 1);
-            const bf16x8 A0 = *reinterpret_cast<const bf16x8*>(lds + off);
-            const bf16x8 A1 = *reinterpret_cast<const bf16x8*>(lds + off + G::PLANE);
-            const bf16x8 A2 = *reinterpret_cast<const bf16x8*>(lds + off + 2 * G::PLANE);
-            acc_hi = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0, B0[st], acc_hi, 0, 0, 0);
-            acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0, B1[st], acc_lo, 0, 0, 0);
-            acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1, B0[st], acc_lo, 0, 0, 0);
-            acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0, B2[st], acc_lo, 0, 0, 0);
-            acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1, B1[st], acc_lo, 0, 0, 0);
-            acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A2, B0[st], acc_lo, 0, 0, 0);
-        }
-
-        const int64_t n_tile = ch * CHUNK + (int64_t)wave * TILE;
-#pragma unroll
-        for (int reg = 0; reg < 8; ++reg) {
-            const int blk = (reg & 3) + 8 * (reg >> 2) + 4 * h;
-            const int64_t n = n_tile + 32 * blk + phase;
-            const float re = acc_hi[reg] + acc_lo[reg];
-            const float im = acc_hi[reg + 8] + acc_lo[reg + 8];
-            if (n < n_out) {
-                nf2 o = { re, im };
-                __builtin_nontemporal_store(o, reinterpret_cast<nf2*>(out + n));
+        if (ch + DEPTH < c_end) stage_load<Q, NW>(va, in, hist_in, ch + DEPTH, n_in, L, al);
+        compute_tile<Q, NW>(lds, B0, B1, B2, a_base, ch * G::CHUNK + (int64_t)wave * TILE, h, phase, n_out, out);
+        if constexpr (DEPTH > 1) {
+            if (ch + 1 < c_end) {
+                __syncthreads();
+                stage_store<Q, NW>(vb, lds);
+                __syncthreads();
+                if (ch + 1 + DEPTH < c_end) stage_load<Q, NW>(vb, in, hist_in, ch + 1 + DEPTH, n_in, L, al);
+                compute_tile<Q, NW>(lds, B0, B1, B2, a_base, (ch + 1) * G::CHUNK + (int64_t)wave * TILE, h, phase, n_out,
+                                    out);
             }
         }
+    }
+}
+
+// ---- v2: software-pipelined form --------------------------------------------------------
+// * split by truncation: x1 = x & 0xffff0000, x2 = (x - x1) & 0xffff0000, x3 = x - x1 - x2;
+//   both subtractions are exact and x3 has <= 8 significant bits, so x = x1 + x2 + x3 holds
+//   exactly (as for the rounding split); bf16 pairs are packed with one v_perm_b32.
+// * two LDS plane buffers: chunk c+1 is split into buffer (i+1)&1 in the same basic block
+//   as chunk c's MFMAs from buffer i&1, so the VALU split co-issues with the matrix pipe;
+//   one barrier per chunk.
+// * the 32(Q-1)-sample halo of chunk c+1 is the tail of chunk c: copied LDS -> LDS, so
+//   HBM reads each input sample once (only a workgroup's first chunk loads its halo).
+template <int Q>
+struct geom2 {
+    static constexpr int NT = 256;
+    static constexpr int CHUNK = 2048;
+    static constexpr int S = 2 * Q;
+    static constexpr int H = 32 * (Q - 1);
+    static constexpr int HR = Q - 1;                          // halo rows (32 samples each)
+    static constexpr int NB = (CHUNK + H) / 32;               // rows per buffer
+    static constexpr int PLANE = (NB * 80 + 255) / 256 * 256;
+    static constexpr int BUF = 6 * PLANE;
+    static constexpr int LDS = 2 * BUF;
+    static constexpr int VPT = CHUNK / 2 / NT;                // 4 float4 per thread (main part)
+};
+
+__device__ __forceinline__ unsigned hi16pair(float a, float b)
+{
+    // upper halves of a (low 16 bits of result) and b (high 16 bits): one v_perm_b32
+    return __builtin_amdgcn_perm(__float_as_uint(b), __float_as_uint(a), 0x07060302u);
+}
+__device__ __forceinline__ float trunc_bf(float x) { return __uint_as_float(__float_as_uint(x) & 0xffff0000u); }
+
+// Split two consecutive samples (a, b) of one component into three packed bf16 pairs.
+__device__ __forceinline__ void split_pair(float a, float b, unsigned& p1, unsigned& p2, unsigned& p3)
+{
+    const float a1 = trunc_bf(a), b1 = trunc_bf(b);
+    const float ar = a - a1, br = b - b1;
+    const float a2 = trunc_bf(ar), b2 = trunc_bf(br);
+    const float a3 = ar - a2, b3 = br - b2;
+    p1 = hi16pair(a1, b1);
+    p2 = hi16pair(a2, b2);
+    p3 = hi16pair(a3, b3);
+}
+
+// Global -> registers: the 2048 non-halo samples of chunk ch (local samples H .. H+2047).
+template <int Q>
+__device__ __forceinline__ void load_main(float4 (&v)[geom2<Q>::VPT], const float2* __restrict__ in,
+                                          const float2* __restrict__ hist, int64_t ch, int64_t n_in, int L,
+                                          bool in_aligned)
+{
+    using G = geom2<Q>;
+    const int64_t g0 = ch * G::CHUNK;
+#if NSH_FIR_ABLATE & 2
+    for (int u = 0; u < G::VPT; ++u) v[u] = make_float4((float)g0, (float)u, (float)threadIdx.x, 1.f);
+    return;
+#endif
+    if (in_aligned && g0 + G::CHUNK <= n_in) {
+        const nf4* src = reinterpret_cast<const nf4*>(in + g0);
+#pragma unroll
+        for (int u = 0; u < G::VPT; ++u) {
+            const nf4 t = __builtin_nontemporal_load(src + threadIdx.x + G::NT * u);
+            v[u] = make_float4(t.x, t.y, t.z, t.w);
+        }
+    } else {
+#pragma unroll
+        for (int u = 0; u < G::VPT; ++u) {
+            const int vi = threadIdx.x + G::NT * u;
+            const float2 a = virt(in, hist, g0 + 2 * vi, n_in, L);
+            const float2 b = virt(in, hist, g0 + 2 * vi + 1, n_in, L);
+            v[u] = make_float4(a.x, a.y, b.x, b.y);
+        }
+    }
+}
+
+// Registers -> six bf16 planes of one buffer (rows HR.. of the buffer).
+template <int Q>
+__device__ __forceinline__ void store_main(const float4 (&v)[geom2<Q>::VPT], unsigned char* buf)
+{
+    using G = geom2<Q>;
+#pragma unroll
+    for (int u = 0; u < G::VPT; ++u) {
+        const int s = G::H + 2 * (threadIdx.x + G::NT * u); // even local sample
+        const int off = (s >> 5) * 80 + (s & 31) * 2;
+        unsigned r1, r2, r3, i1, i2, i3;
+#if NSH_FIR_ABLATE & 4
+        r1 = r2 = r3 = __float_as_uint(v[u].x);
+        i1 = i2 = i3 = __float_as_uint(v[u].y);
+#else
+        split_pair(v[u].x, v[u].z, r1, r2, r3);
+        split_pair(v[u].y, v[u].w, i1, i2, i3);
+#endif
+        *reinterpret_cast<unsigned*>(buf + 0 * G::PLANE + off) = r1;
+        *reinterpret_cast<unsigned*>(buf + 1 * G::PLANE + off) = r2;
+        *reinterpret_cast<unsigned*>(buf + 2 * G::PLANE + off) = r3;
+        *reinterpret_cast<unsigned*>(buf + 3 * G::PLANE + off) = i1;
+        *reinterpret_cast<unsigned*>(buf + 4 * G::PLANE + off) = i2;
+        *reinterpret_cast<unsigned*>(buf + 5 * G::PLANE + off) = i3;
+    }
+}
+
+// Halo rows of the next buffer = last HR rows of the current one (6 planes x HR x 64 B).
+template <int Q>
+__device__ __forceinline__ void copy_halo(const unsigned char* cur, unsigned char* nxt)
+{
+    using G = geom2<Q>;
+    constexpr int PIECES = 6 * G::HR * 4; // 16-B pieces (64 data bytes per row)
+    if constexpr (PIECES > 0) {
+        for (int t = threadIdx.x; t < PIECES; t += G::NT) {
+            const int plane = t / (G::HR * 4);
+            const int rem = t % (G::HR * 4);
+            const int row = rem >> 2, q16 = rem & 3;
+            const uint4 d = *reinterpret_cast<const uint4*>(cur + plane * G::PLANE + (G::NB - G::HR + row) * 80 + q16 * 16);
+            *reinterpret_cast<uint4*>(nxt + plane * G::PLANE + row * 80 + q16 * 16) = d;
+        }
+    }
+}
+
+// First chunk of a workgroup: its halo comes from global memory / history.
+template <int Q>
+__device__ __forceinline__ void load_store_halo(unsigned char* buf, const float2* __restrict__ in,
+                                                const float2* __restrict__ hist, int64_t ch, int64_t n_in, int L)
+{
+    using G = geom2<Q>;
+    if constexpr (G::H > 0) {
+        const int64_t g0 = ch * G::CHUNK - G::H;
+        for (int p = threadIdx.x; p < G::H / 2; p += G::NT) {
+            const float2 a = virt(in, hist, g0 + 2 * p, n_in, L);
+            const float2 b = virt(in, hist, g0 + 2 * p + 1, n_in, L);
+            const int s = 2 * p;
+            const int off = (s >> 5) * 80 + (s & 31) * 2;
+            unsigned r1, r2, r3, i1, i2, i3;
+            split_pair(a.x, b.x, r1, r2, r3);
+            split_pair(a.y, b.y, i1, i2, i3);
+            *reinterpret_cast<unsigned*>(buf + 0 * G::PLANE + off) = r1;
+            *reinterpret_cast<unsigned*>(buf + 1 * G::PLANE + off) = r2;
+            *reinterpret_cast<unsigned*>(buf + 2 * G::PLANE + off) = r3;
+            *reinterpret_cast<unsigned*>(buf + 3 * G::PLANE + off) = i1;
+            *reinterpret_cast<unsigned*>(buf + 4 * G::PLANE + off) = i2;
+            *reinterpret_cast<unsigned*>(buf + 5 * G::PLANE + off) = i3;
+        }
+    }
+}
+
+// One split unit (float4 = two samples) of store_main.
+template <int Q>
+__device__ __forceinline__ void store_unit(const float4& v, unsigned char* buf, int u)
+{
+    using G = geom2<Q>;
+    const int s = G::H + 2 * (threadIdx.x + G::NT * u);
+    const int off = (s >> 5) * 80 + (s & 31) * 2;
+    unsigned r1, r2, r3, i1, i2, i3;
+#if NSH_FIR_ABLATE & 4
+    r1 = r2 = r3 = __float_as_uint(v.x);
+    i1 = i2 = i3 = __float_as_uint(v.y);
+#else
+    split_pair(v.x, v.z, r1, r2, r3);
+    split_pair(v.y, v.w, i1, i2, i3);
+#endif
+    *reinterpret_cast<unsigned*>(buf + 0 * G::PLANE + off) = r1;
+    *reinterpret_cast<unsigned*>(buf + 1 * G::PLANE + off) = r2;
+    *reinterpret_cast<unsigned*>(buf + 2 * G::PLANE + off) = r3;
+    *reinterpret_cast<unsigned*>(buf + 3 * G::PLANE + off) = i1;
+    *reinterpret_cast<unsigned*>(buf + 4 * G::PLANE + off) = i2;
+    *reinterpret_cast<unsigned*>(buf + 5 * G::PLANE + off) = i3;
+}
+
+// compute_tile of the current buffer with the split of the next chunk (registers `nxt`)
+// woven into the k-steps, so each wave's own VALU/DS-write work fills MFMA issue gaps
+// instead of running as a serial block before the MFMA chain.
+template <int Q>
+__device__ __forceinline__ void compute_tile_fused(const unsigned char* lds,
+                                                   const bf16x8 (&B0)[2 * Q],
+                                                   const bf16x8 (&B1)[2 * Q],
+                                                   const bf16x8 (&B2)[2 * Q],
+                                                   int a_base,
+                                                   int64_t n_tile,
+                                                   int h,
+                                                   int phase,
+                                                   int64_t n_out,
+                                                   float2* __restrict__ out,
+                                                   const float4 (&nxt)[geom2<Q>::VPT],
+                                                   unsigned char* nbuf)
+{
+    using G = geom2<Q>;
+    constexpr int S_ = 2 * Q;
+    constexpr int PLANE_ = G::PLANE;
+    if constexpr (S_ < G::VPT) store_main<Q>(nxt, nbuf); // short filters: no room to weave
+    f32x16 acc_hi = {};
+    f32x16 acc_lo = {};
+#pragma unroll
+    for (int st = 0; st < S_; ++st) {
+        const int q = st >> 1;
+        const int off = a_base - q * 80 + 32 * (st & 1);
+        const bf16x8 A0 = *reinterpret_cast<const bf16x8*>(lds + off);
+        const bf16x8 A1 = *reinterpret_cast<const bf16x8*>(lds + off + PLANE_);
+        const bf16x8 A2 = *reinterpret_cast<const bf16x8*>(lds + off + 2 * PLANE_);
+#if NSH_FIR_ABLATE & 1
+        acc_hi[st & 15] += (float)A0[0] + (float)A1[1] + (float)A2[2] + (float)B0[st][0] + (float)B1[st][1] + (float)B2[st][2];
+#else
+        acc_hi = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0, B0[st], acc_hi, 0, 0, 0);
+        acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0, B1[st], acc_lo, 0, 0, 0);
+        acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1, B0[st], acc_lo, 0, 0, 0);
+        acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0, B2[st], acc_lo, 0, 0, 0);
+        acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1, B1[st], acc_lo, 0, 0, 0);
+        acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A2, B0[st], acc_lo, 0, 0, 0);
+#endif
+        // split units at k-steps 1, 3, 5, 7 (S_ = 10 for Q = 5)
+        if constexpr (S_ >= G::VPT) {
+            constexpr int STRIDE = S_ / G::VPT;
+            if (st % STRIDE == STRIDE - 1 && st / STRIDE < G::VPT) store_unit<Q>(nxt[st / STRIDE], nbuf, st / STRIDE);
+        }
+    }
+#pragma unroll
+    for (int reg = 0; reg < 8; ++reg) {
+        const int blk = (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        const int64_t n = n_tile + 32 * blk + phase;
+        const float re = acc_hi[reg] + acc_lo[reg];
+        const float im = acc_hi[reg + 8] + acc_lo[reg + 8];
+#if NSH_FIR_ABLATE & 8
+        if (re == 1.2345e-30f && n < n_out) {
+#else
+        if (n < n_out) {
+#endif
+            nf2 o = { re, im };
+            __builtin_nontemporal_store(o, reinterpret_cast<nf2*>(out + n));
+        }
+    }
+}
+
+template <int Q, int DEPTH, bool FUSED = false>
+__global__ __launch_bounds__(256, 2) void k_fir_mfma2(const float2* __restrict__ in,
+                                                     const float2* __restrict__ hist_in,
+                                                     float2* __restrict__ hist_out,
+                                                     float2* __restrict__ out,
+                                                     const bf16x8* __restrict__ frag, // [3][S][64]
+                                                     int L,
+                                                     int64_t n_out,
+                                                     int in_aligned)
+{
+    using G = geom2<Q>;
+    constexpr int S = G::S;
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int64_t n_in = n_out;
+
+    if (blockIdx.x == 0) {
+        for (int j = tid; j < L - 1; j += G::NT) hist_out[j] = virt(in, hist_in, n_in - (L - 1) + j, n_in, L);
+    }
+
+    bf16x8 B0[S], B1[S], B2[S];
+#pragma unroll
+    for (int st = 0; st < S; ++st) {
+        B0[st] = frag[(0 * S + st) * 64 + lane];
+        B1[st] = frag[(1 * S + st) * 64 + lane];
+        B2[st] = frag[(2 * S + st) * 64 + lane];
+    }
+
+    const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
+    const int64_t per = (nchunks + gridDim.x - 1) / gridDim.x;
+    const int64_t c_begin = (int64_t)blockIdx.x * per;
+    const int64_t c_end = c_begin + per < nchunks ? c_begin + per : nchunks;
+    if (c_begin >= c_end) return;
+    const int64_t c_last = c_end - 1;
+
+    const int rho = lane & 31;
+    const int b = rho & 15;
+    const int c = rho >> 4;
+    const int h = lane >> 5;
+    const int a_base = c * 3 * G::PLANE + ((Q - 1) + 16 * wave + b) * 80 + 16 * h;
+    const int phase = lane & 31;
+    const bool al = in_aligned != 0;
+
+    auto clamp = [&](int64_t x) { return x <= c_last ? x : c_last; };
+    // prologue: chunk c_begin -> buffer 0 (halo from global); chunks up to c_begin+DEPTH in flight
+    float4 va[G::VPT], vb[G::VPT], vc[G::VPT];
+    load_store_halo<Q>(lds, in, hist_in, c_begin, n_in, L);
+    load_main<Q>(va, in, hist_in, c_begin, n_in, L, al);
+    store_main<Q>(va, lds);
+    load_main<Q>(va, in, hist_in, clamp(c_begin + 1), n_in, L, al);
+    if constexpr (DEPTH > 1) load_main<Q>(vb, in, hist_in, clamp(c_begin + 2), n_in, L, al);
+    __syncthreads();
+
+    // step ch: `nxt` holds chunk ch+1 (split into the other buffer now), `ld` receives
+    // chunk ch+1+DEPTH (clamped: the tail re-reads its last chunk from L2).
+    auto step = [&](float4 (&nxt)[G::VPT], float4 (&ld)[G::VPT], int64_t ch) {
+        unsigned char* cur = lds + ((ch - c_begin) & 1) * G::BUF;
+        unsigned char* nbuf = lds + (((ch - c_begin) & 1) ^ 1) * G::BUF;
+        load_main<Q>(ld, in, hist_in, clamp(ch + 1 + DEPTH), n_in, L, al);
+        copy_halo<Q>(cur, nbuf);
+        if constexpr (FUSED) {
+            compute_tile_fused<Q>(cur, B0, B1, B2, a_base, ch * G::CHUNK + (int64_t)wave * TILE, h, phase, n_out, out,
+                                  nxt, nbuf);
+        } else {
+            store_main<Q>(nxt, nbuf); // split chunk ch+1 while chunk ch runs on the matrix cores
+            compute_tile<Q, 4, G::PLANE>(cur, B0, B1, B2, a_base, ch * G::CHUNK + (int64_t)wave * TILE, h, phase, n_out,
+                                         out);
+        }
+        __syncthreads();
+    };
+    int64_t ch = c_begin;
+    if constexpr (DEPTH == 1) {
+        for (; ch + 1 <= c_last; ch += 2) {
+            step(va, vb, ch);
+            step(vb, va, ch + 1);
+        }
+        if (ch <= c_last) step(va, vb, ch);
+    } else {
+        for (; ch + 2 <= c_last; ch += 3) {
+            step(va, vc, ch);
+            step(vb, va, ch + 1);
+            step(vc, vb, ch + 2);
+        }
+        if (ch <= c_last) step(va, vc, ch++);
+        if (ch <= c_last) step(vb, va, ch);
     }
 }
 
@@ -242,25 +614,66 @@ float bf16_to_f(unsigned short b)
     return f;
 }
 
-template <int Q>
-int launch_q(const nsh_fir_plan* p, const float2* in, const float2* hin, float2* hout, float2* out, int64_t n_out, hipStream_t s)
+template <int Q, int NW, int DEPTH>
+int launch_v(const nsh_fir_plan* p, const float2* in, const float2* hin, float2* hout, float2* out, int64_t n_out,
+             hipStream_t s, int wg_per_cu)
 {
-    using G = geom<Q>;
+    using G = geom<Q, NW>;
     static bool attr_set = false;
     if (!attr_set) {
-        NSH_CK(hipFuncSetAttribute((const void*)k_fir_mfma<Q>, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
+        NSH_CK(hipFuncSetAttribute((const void*)k_fir_mfma<Q, NW, DEPTH>, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
         attr_set = true;
     }
-    const int64_t nchunks = (n_out + CHUNK - 1) / CHUNK;
+    const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
     int n_cu = 256;
     (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, p->dev);
-    const int64_t max_grid = (int64_t)n_cu * 2;
+    const int64_t max_grid = (int64_t)n_cu * wg_per_cu;
     const unsigned grid = (unsigned)(nchunks < max_grid ? nchunks : max_grid);
     const int aligned = ((uintptr_t)in % 16 == 0) ? 1 : 0;
-    hipLaunchKernelGGL(k_fir_mfma<Q>, dim3(grid), dim3(NT), G::LDS, s, in, hin, hout, out,
+    hipLaunchKernelGGL((k_fir_mfma<Q, NW, DEPTH>), dim3(grid), dim3(G::NT), G::LDS, s, in, hin, hout, out,
                        (const bf16x8*)p->frag_dev, p->L, n_out, aligned);
     NSH_CK_LAUNCH("nsh_fir_ccf(mfma)");
     return 0;
+}
+
+template <int Q, int DEPTH, bool FUSED = false>
+int launch_v2(const nsh_fir_plan* p, const float2* in, const float2* hin, float2* hout, float2* out, int64_t n_out,
+              hipStream_t s, int wg_per_cu)
+{
+    using G = geom2<Q>;
+    static bool attr_set = false;
+    if (!attr_set) {
+        NSH_CK(hipFuncSetAttribute((const void*)k_fir_mfma2<Q, DEPTH, FUSED>, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
+        attr_set = true;
+    }
+    const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
+    int n_cu = 256;
+    (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, p->dev);
+    const int64_t max_grid = (int64_t)n_cu * wg_per_cu;
+    const unsigned grid = (unsigned)(nchunks < max_grid ? nchunks : max_grid);
+    const int aligned = ((uintptr_t)in % 16 == 0) ? 1 : 0;
+    hipLaunchKernelGGL((k_fir_mfma2<Q, DEPTH, FUSED>), dim3(grid), dim3(G::NT), G::LDS, s, in, hin, hout, out,
+                       (const bf16x8*)p->frag_dev, p->L, n_out, aligned);
+    NSH_CK_LAUNCH("nsh_fir_ccf(mfma2)");
+    return 0;
+}
+
+// Tuning variants (selected by NSH_FIR_MFMA_VARIANT for A/B runs; default = measured best).
+template <int Q>
+int launch_q(const nsh_fir_plan* p, const float2* in, const float2* hin, float2* hout, float2* out, int64_t n_out, hipStream_t s)
+{
+    switch (p->variant) {
+    case 1: return launch_v<Q, 4, 1>(p, in, hin, hout, out, n_out, s, 2);
+    case 2: return launch_v<Q, 4, 2>(p, in, hin, hout, out, n_out, s, 2);
+    case 3: return launch_v<Q, 8, 1>(p, in, hin, hout, out, n_out, s, 2);
+    case 4: return launch_v<Q, 8, 2>(p, in, hin, hout, out, n_out, s, 2);
+    case 5: return launch_v<Q, 8, 2>(p, in, hin, hout, out, n_out, s, 1);
+    case 6: return launch_v2<Q, 1>(p, in, hin, hout, out, n_out, s, 2);
+    case 7: return launch_v2<Q, 2>(p, in, hin, hout, out, n_out, s, 2);
+    case 12: return launch_v2<Q, 1, true>(p, in, hin, hout, out, n_out, s, 2);
+    case 13: return launch_v2<Q, 2, true>(p, in, hin, hout, out, n_out, s, 2);
+    default: return launch_v2<Q, 2>(p, in, hin, hout, out, n_out, s, 2);
+    }
 }
 
 } // namespace
@@ -276,6 +689,7 @@ bool nsh_fir_mfma_supported(const nsh_fir_plan* p)
 
 int nsh_fir_mfma_prepare(nsh_fir_plan* p)
 {
+    if (const char* v = std::getenv("NSH_FIR_MFMA_VARIANT")) p->variant = std::atoi(v);
     const int Q = (p->L + 30) / 32 + 1;
     const int S = 2 * Q;
     p->Q = Q;

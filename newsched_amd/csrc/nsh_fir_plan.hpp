@@ -16,6 +16,7 @@ struct nsh_fir_plan {
     int Q = 0;
     int S = 0;
     void* frag_dev = nullptr;
+    int variant = 0;      // MFMA kernel tuning variant (0 = default)
 };
 
 bool nsh_fir_mfma_supported(const nsh_fir_plan* p);

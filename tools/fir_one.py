@@ -1,0 +1,32 @@
+"""Run one FIR configuration (and a calibration copy) repeatedly -- the workload for the
+rocprofv3 --pmc passes in tools/pmc_fir.sh."""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np
+import scipy.signal as ss
+import torch
+
+from newsched_amd import nsh
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--algo", default="mfma", choices=["mfma", "direct"])
+ap.add_argument("--log2n", type=int, default=25)
+ap.add_argument("--reps", type=int, default=10)
+a = ap.parse_args()
+n = 1 << a.log2n
+h = ss.firwin(127, 0.2).astype(np.float32)
+x = torch.empty(n, dtype=torch.complex64, device="cuda")
+nsh.synth(x, n, 0)
+y = torch.empty_like(x)
+hin = torch.zeros(126, dtype=torch.complex64, device="cuda")
+hout = torch.zeros_like(hin)
+p = nsh.FirPlan(h, 1, nsh.FIR_MFMA if a.algo == "mfma" else nsh.FIR_DIRECT)
+for _ in range(a.reps):
+    p(x, hin, hout, y, n)
+for _ in range(a.reps):
+    nsh.copy(x, y, 8 * n)  # calibration: exactly 8n B read + 8n B written per launch
+torch.cuda.synchronize()
+print("done", n, a.algo)
