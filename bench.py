@@ -52,16 +52,16 @@ def cpu_model():
     return "unknown"
 
 
-def load_pmc_traffic(samples_per_launch):
+def load_pmc_traffic(kernel, samples_per_launch):
     """HBM bytes per launch from the committed PMC summary (profiles/pmc_fir.json, produced
     by tools/pmc_summary.py from separate rocprofv3 --pmc passes, gfx950 FETCH_SIZE x2
-    correction applied there), scaled to this launch size."""
+    correction applied there), scaled to this launch size. kernel: "fir_mfma" | "fir_direct"."""
     p = os.path.join(ROOT, "profiles", "pmc_fir.json")
     try:
         with open(p) as f:
             d = json.load(f)
-        return float(d["hbm_bytes_per_sample"]) * samples_per_launch
-    except (OSError, KeyError, ValueError):
+        return float(d[kernel]["hbm_bytes_per_sample"]) * samples_per_launch
+    except (OSError, KeyError, ValueError, TypeError):
         return None
 
 
@@ -72,7 +72,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--log2n", type=int, default=28)
     ap.add_argument("--algo", default="auto", choices=["auto", "mfma", "direct"])
-    ap.add_argument("--out-buf-mib", type=int, default=256)
+    ap.add_argument("--out-buf-mib", type=int, default=2048, help="FIR output hip_buffer (default: one launch per 2^28-sample step)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-log2n", type=int, default=28, help="CPU baseline sample (default: the full stream)")
     a = ap.parse_args()
@@ -179,7 +179,7 @@ def main():
         "parity": {"check": "last 4096 outputs of the last step vs oracle (double accumulation)",
                    "max_abs_err": err, "scale": scale, "ok": bool(ok)},
     }
-    tr = load_pmc_traffic(per_launch_samples)
+    tr = load_pmc_traffic("fir_" + algo_used, per_launch_samples)
     if tr is not None:
         out["roofline"]["traffic"] = int(tr)
 

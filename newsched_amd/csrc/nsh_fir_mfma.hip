@@ -180,6 +180,30 @@ __device__ __forceinline__ void compute_tile(const unsigned char* lds,
         acc_hi[st & 15] += (float)A0[0] + (float)A1[1] + (float)A2[2] + (float)B0[st][0] + (float)B1[st][1] + (float)B2[st][2];
         continue;
 #endif
+#if NSH_FIR_ABLATE & 16 // timing only: half the matrix work
+        acc_hi = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0, B0[st], acc_hi, 0, 0, 0);
+        acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1, B0[st], acc_lo, 0, 0, 0);
+        acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A2, B2[st], acc_lo, 0, 0, 0);
+        continue;
+#endif
+#if NSH_FIR_ABLATE & 32 // timing only: the int8 instruction count (6 x i32_32x32x32_i8 per 2 k-steps)
+        if (st & 1) {
+            typedef int i32x4 __attribute__((ext_vector_type(4)));
+            typedef int i32x16 __attribute__((ext_vector_type(16)));
+            const i32x4 a0 = __builtin_bit_cast(i32x4, A0), a1 = __builtin_bit_cast(i32x4, A1), a2 = __builtin_bit_cast(i32x4, A2);
+            const i32x4 b0 = __builtin_bit_cast(i32x4, B0[st]), b1 = __builtin_bit_cast(i32x4, B1[st]), b2 = __builtin_bit_cast(i32x4, B2[st]);
+            i32x16 ih = __builtin_bit_cast(i32x16, acc_hi), il = __builtin_bit_cast(i32x16, acc_lo);
+            ih = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, b0, ih, 0, 0, 0);
+            il = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, b1, il, 0, 0, 0);
+            il = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, b0, il, 0, 0, 0);
+            ih = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, b2, ih, 0, 0, 0);
+            il = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, b1, il, 0, 0, 0);
+            ih = __builtin_amdgcn_mfma_i32_32x32x32_i8(a2, b0, ih, 0, 0, 0);
+            acc_hi = __builtin_bit_cast(f32x16, ih);
+            acc_lo = __builtin_bit_cast(f32x16, il);
+        }
+        continue;
+#endif
         acc_hi = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0, B0[st], acc_hi, 0, 0, 0);
         acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0, B1[st], acc_lo, 0, 0, 0);
         acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1, B0[st], acc_lo, 0, 0, 0);
@@ -421,93 +445,7 @@ __device__ __forceinline__ void load_store_halo(unsigned char* buf, const float2
     }
 }
 
-// One split unit (float4 = two samples) of store_main.
-template <int Q>
-__device__ __forceinline__ void store_unit(const float4& v, unsigned char* buf, int u)
-{
-    using G = geom2<Q>;
-    const int s = G::H + 2 * (threadIdx.x + G::NT * u);
-    const int off = (s >> 5) * 80 + (s & 31) * 2;
-    unsigned r1, r2, r3, i1, i2, i3;
-#if NSH_FIR_ABLATE & 4
-    r1 = r2 = r3 = __float_as_uint(v.x);
-    i1 = i2 = i3 = __float_as_uint(v.y);
-#else
-    split_pair(v.x, v.z, r1, r2, r3);
-    split_pair(v.y, v.w, i1, i2, i3);
-#endif
-    *reinterpret_cast<unsigned*>(buf + 0 * G::PLANE + off) = r1;
-    *reinterpret_cast<unsigned*>(buf + 1 * G::PLANE + off) = r2;
-    *reinterpret_cast<unsigned*>(buf + 2 * G::PLANE + off) = r3;
-    *reinterpret_cast<unsigned*>(buf + 3 * G::PLANE + off) = i1;
-    *reinterpret_cast<unsigned*>(buf + 4 * G::PLANE + off) = i2;
-    *reinterpret_cast<unsigned*>(buf + 5 * G::PLANE + off) = i3;
-}
-
-// compute_tile of the current buffer with the split of the next chunk (registers `nxt`)
-// woven into the k-steps, so each wave's own VALU/DS-write work fills MFMA issue gaps
-// instead of running as a serial block before the MFMA chain.
-template <int Q>
-__device__ __forceinline__ void compute_tile_fused(const unsigned char* lds,
-                                                   const bf16x8 (&B0)[2 * Q],
-                                                   const bf16x8 (&B1)[2 * Q],
-                                                   const bf16x8 (&B2)[2 * Q],
-                                                   int a_base,
-                                                   int64_t n_tile,
-                                                   int h,
-                                                   int phase,
-                                                   int64_t n_out,
-                                                   float2* __restrict__ out,
-                                                   const float4 (&nxt)[geom2<Q>::VPT],
-                                                   unsigned char* nbuf)
-{
-    using G = geom2<Q>;
-    constexpr int S_ = 2 * Q;
-    constexpr int PLANE_ = G::PLANE;
-    if constexpr (S_ < G::VPT) store_main<Q>(nxt, nbuf); // short filters: no room to weave
-    f32x16 acc_hi = {};
-    f32x16 acc_lo = {};
-#pragma unroll
-    for (int st = 0; st < S_; ++st) {
-        const int q = st >> 1;
-        const int off = a_base - q * 80 + 32 * (st & 1);
-        const bf16x8 A0 = *reinterpret_cast<const bf16x8*>(lds + off);
-        const bf16x8 A1 = *reinterpret_cast<const bf16x8*>(lds + off + PLANE_);
-        const bf16x8 A2 = *reinterpret_cast<const bf16x8*>(lds + off + 2 * PLANE_);
-#if NSH_FIR_ABLATE & 1
-        acc_hi[st & 15] += (float)A0[0] + (float)A1[1] + (float)A2[2] + (float)B0[st][0] + (float)B1[st][1] + (float)B2[st][2];
-#else
-        acc_hi = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0, B0[st], acc_hi, 0, 0, 0);
-        acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0, B1[st], acc_lo, 0, 0, 0);
-        acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1, B0[st], acc_lo, 0, 0, 0);
-        acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0, B2[st], acc_lo, 0, 0, 0);
-        acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1, B1[st], acc_lo, 0, 0, 0);
-        acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A2, B0[st], acc_lo, 0, 0, 0);
-#endif
-        // split units at k-steps 1, 3, 5, 7 (S_ = 10 for Q = 5)
-        if constexpr (S_ >= G::VPT) {
-            constexpr int STRIDE = S_ / G::VPT;
-            if (st % STRIDE == STRIDE - 1 && st / STRIDE < G::VPT) store_unit<Q>(nxt[st / STRIDE], nbuf, st / STRIDE);
-        }
-    }
-#pragma unroll
-    for (int reg = 0; reg < 8; ++reg) {
-        const int blk = (reg & 3) + 8 * (reg >> 2) + 4 * h;
-        const int64_t n = n_tile + 32 * blk + phase;
-        const float re = acc_hi[reg] + acc_lo[reg];
-        const float im = acc_hi[reg + 8] + acc_lo[reg + 8];
-#if NSH_FIR_ABLATE & 8
-        if (re == 1.2345e-30f && n < n_out) {
-#else
-        if (n < n_out) {
-#endif
-            nf2 o = { re, im };
-            __builtin_nontemporal_store(o, reinterpret_cast<nf2*>(out + n));
-        }
-    }
-}
-
-template <int Q, int DEPTH, bool FUSED = false>
+template <int Q, int DEPTH>
 __global__ __launch_bounds__(256, 2) void k_fir_mfma2(const float2* __restrict__ in,
                                                      const float2* __restrict__ hist_in,
                                                      float2* __restrict__ hist_out,
@@ -570,14 +508,8 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma2(const float2* __restrict__
         unsigned char* nbuf = lds + (((ch - c_begin) & 1) ^ 1) * G::BUF;
         load_main<Q>(ld, in, hist_in, clamp(ch + 1 + DEPTH), n_in, L, al);
         copy_halo<Q>(cur, nbuf);
-        if constexpr (FUSED) {
-            compute_tile_fused<Q>(cur, B0, B1, B2, a_base, ch * G::CHUNK + (int64_t)wave * TILE, h, phase, n_out, out,
-                                  nxt, nbuf);
-        } else {
-            store_main<Q>(nxt, nbuf); // split chunk ch+1 while chunk ch runs on the matrix cores
-            compute_tile<Q, 4, G::PLANE>(cur, B0, B1, B2, a_base, ch * G::CHUNK + (int64_t)wave * TILE, h, phase, n_out,
-                                         out);
-        }
+        store_main<Q>(nxt, nbuf); // split chunk ch+1 while chunk ch runs on the matrix cores
+        compute_tile<Q, 4, G::PLANE>(cur, B0, B1, B2, a_base, ch * G::CHUNK + (int64_t)wave * TILE, h, phase, n_out, out);
         __syncthreads();
     };
     int64_t ch = c_begin;
@@ -636,14 +568,14 @@ int launch_v(const nsh_fir_plan* p, const float2* in, const float2* hin, float2*
     return 0;
 }
 
-template <int Q, int DEPTH, bool FUSED = false>
+template <int Q, int DEPTH>
 int launch_v2(const nsh_fir_plan* p, const float2* in, const float2* hin, float2* hout, float2* out, int64_t n_out,
               hipStream_t s, int wg_per_cu)
 {
     using G = geom2<Q>;
     static bool attr_set = false;
     if (!attr_set) {
-        NSH_CK(hipFuncSetAttribute((const void*)k_fir_mfma2<Q, DEPTH, FUSED>, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
+        NSH_CK(hipFuncSetAttribute((const void*)k_fir_mfma2<Q, DEPTH>, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
         attr_set = true;
     }
     const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
@@ -652,7 +584,7 @@ int launch_v2(const nsh_fir_plan* p, const float2* in, const float2* hin, float2
     const int64_t max_grid = (int64_t)n_cu * wg_per_cu;
     const unsigned grid = (unsigned)(nchunks < max_grid ? nchunks : max_grid);
     const int aligned = ((uintptr_t)in % 16 == 0) ? 1 : 0;
-    hipLaunchKernelGGL((k_fir_mfma2<Q, DEPTH, FUSED>), dim3(grid), dim3(G::NT), G::LDS, s, in, hin, hout, out,
+    hipLaunchKernelGGL((k_fir_mfma2<Q, DEPTH>), dim3(grid), dim3(G::NT), G::LDS, s, in, hin, hout, out,
                        (const bf16x8*)p->frag_dev, p->L, n_out, aligned);
     NSH_CK_LAUNCH("nsh_fir_ccf(mfma2)");
     return 0;
@@ -670,8 +602,6 @@ int launch_q(const nsh_fir_plan* p, const float2* in, const float2* hin, float2*
     case 5: return launch_v<Q, 8, 2>(p, in, hin, hout, out, n_out, s, 1);
     case 6: return launch_v2<Q, 1>(p, in, hin, hout, out, n_out, s, 2);
     case 7: return launch_v2<Q, 2>(p, in, hin, hout, out, n_out, s, 2);
-    case 12: return launch_v2<Q, 1, true>(p, in, hin, hout, out, n_out, s, 2);
-    case 13: return launch_v2<Q, 2, true>(p, in, hin, hout, out, n_out, s, 2);
     default: return launch_v2<Q, 2>(p, in, hin, hout, out, n_out, s, 2);
     }
 }
