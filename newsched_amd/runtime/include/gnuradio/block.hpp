@@ -58,12 +58,14 @@ public:
         return work(work_input, work_output);
     }
 
-    void set_scheduler(std::shared_ptr<scheduler> s) { p_scheduler = std::move(s); }
+    // weak: the scheduler owns its blocks (a strong back-reference would leak both)
+    void set_scheduler(std::shared_ptr<scheduler> s) { p_scheduler = s; }
+    std::shared_ptr<scheduler> get_scheduler() const { return p_scheduler.lock(); }
 
     gpdict attributes;
 
 protected:
-    std::shared_ptr<scheduler> p_scheduler = nullptr;
+    std::weak_ptr<scheduler> p_scheduler;
 
 private:
     bool d_running = false;

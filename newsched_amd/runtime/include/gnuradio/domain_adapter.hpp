@@ -21,6 +21,8 @@ public:
     buffer_sptr buffer() { return _buffer; }
     buffer_location_t buffer_location() const { return _buffer_loc; }
     void set_buffer_location(buffer_location_t l) { _buffer_loc = l; }
+    // Called by the buffer manager once a LOCAL adapter's edge buffer exists.
+    virtual void buffer_ready() {}
 
 protected:
     domain_adapter(buffer_location_t loc, const std::string& name = "domain_adapter") : node(name), _buffer_loc(loc) {}
@@ -41,6 +43,13 @@ public:
     make_domain_adapter_pair(port_sptr upstream_port, port_sptr downstream_port, const std::string& name = "")
     {
         throw std::runtime_error("Cannot create domain adapter pair from base class");
+    }
+    // One half of a crossing whose other end lives in another process
+    // (domain_adapter_remote.hpp). local_port: the local block's port at the crossing.
+    virtual std::shared_ptr<domain_adapter>
+    make_remote_adapter(port_sptr local_port, bool local_is_upstream, int crossing, const std::string& name = "")
+    {
+        throw std::runtime_error("this domain_adapter_conf cannot cross process boundaries");
     }
 
 protected:

@@ -120,6 +120,7 @@ private:
 public:
     // LOCAL side publishes its buffer to the REMOTE side when the buffer manager sets it.
     void publish() { _sync->set(_buffer); }
+    void buffer_ready() override { publish(); }
 };
 
 class domain_adapter_direct_conf : public domain_adapter_conf

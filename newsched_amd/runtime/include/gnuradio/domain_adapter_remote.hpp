@@ -1,0 +1,160 @@
+// Cross-process domain adapters: one flowgraph partitioned over several processes (one
+// per GPU), with every edge between domains of different processes carried by a
+// point-to-point channel.
+//
+// The reference partitions a flowgraph only within one process
+// (runtime/lib/graph_utils.cpp:11-205 + domain_adapter_direct.hpp:10-258; its
+// domain_adapter.hpp:13-97 already names LOCAL/REMOTE buffer locations and a request
+// protocol for the purpose). Here each process builds the SAME flowgraph and the SAME
+// domain_conf list (SPMD), marks the domains that live elsewhere with remote_domain, and
+// calls flowgraph::partition: graph_utils then instantiates only the local half of every
+// crossing edge whose other end is remote:
+//
+//   process A:  blk_a -> [da_remote SEND] ~~~~ control: TCP (counts, done flags)
+//   process B:                        ~~~~~> [da_remote RECV] -> blk_b
+//                                     data:  RCCL ncclSend/ncclRecv on the partition
+//                                            streams (device buffers, different GPUs), or
+//                                            the TCP socket (host buffers; device buffers
+//                                            staged through pinned memory)
+//
+// Crossing i uses TCP port base_port + i on `host` (the receiving process listens).
+// Sender: every post_write of the upstream block is forwarded immediately (chunks of at
+// most the receiver's free ring space), stream-ordered after the producing kernel, and
+// the span is released at once (the next kernel that reuses it is stream-ordered after the
+// send). Receiver: a thread per adapter posts the matching receive into its ring, then
+// post_write + NOTIFY_INPUT wake the downstream block. Per-run DONE / READER_DONE
+// messages make drain-based termination and restarted flowgraphs work across processes.
+#pragma once
+#include <gnuradio/domain_adapter.hpp>
+#include <gnuradio/scheduler.hpp>
+
+#include <atomic>
+#include <condition_variable>
+#include <exception>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+
+namespace gr {
+
+namespace remote {
+class channel;   // TCP control (and host data) socket
+class transport; // data path: "rccl" | "socket"
+} // namespace remote
+
+// Placeholder scheduler for a domain that another process runs. Never initialised or
+// started here; `rank` is informational (the process that owns the domain).
+class remote_domain : public scheduler
+{
+public:
+    using sptr = std::shared_ptr<remote_domain>;
+    static sptr make(int rank, const std::string& name = "remote") { return std::make_shared<remote_domain>(rank, name); }
+    remote_domain(int rank, const std::string& name) : scheduler(name), _rank(rank) {}
+    int rank() const { return _rank; }
+    void initialize(flat_graph_sptr, flowgraph_monitor_sptr, neighbor_interface_map) override {}
+    void push_message(scheduler_message_sptr) override {}
+    void start() override {}
+    void stop() override {}
+    void wait() override {}
+
+private:
+    int _rank;
+};
+
+enum class remote_role { SEND, RECV };
+
+struct remote_edge_options {
+    std::string host = "127.0.0.1"; // address of the receiving process
+    int base_port = 29650;          // crossing i listens on base_port + i
+    std::string transport = "auto"; // "auto" | "rccl" | "socket"
+    int device = -1;                // GPU of this process (-1: the current thread's device)
+    double timeout_s = 120.0;       // connect / accept / handshake limit
+};
+
+class domain_adapter_remote : public domain_adapter
+{
+public:
+    using sptr = std::shared_ptr<domain_adapter_remote>;
+    // other_port: the local block port this adapter faces (SEND faces an output port).
+    static sptr make(remote_role role, port_sptr other_port, int crossing, const remote_edge_options& opt);
+    ~domain_adapter_remote() override;
+
+    // buffer interface: RECV serves the downstream block's reads, SEND the upstream
+    // block's writes; both forward to the LOCAL ring created by the buffer manager.
+    void* read_ptr() override;
+    void* write_ptr() override;
+    bool read_info(buffer_info_t& info) override;
+    bool write_info(buffer_info_t& info) override;
+    void post_read(int n) override;
+    void post_write(int n) override;
+    void copy_items(buffer_sptr from, int n) override;
+    void set_writer_done() override;
+    void set_reader_done() override;
+    bool writer_done() const override;
+    bool reader_done() const override;
+    void reset_flags() override;
+
+    void buffer_ready() override; // connect, handshake, start the receive thread
+
+    remote_role role() const { return _role; }
+    int crossing() const { return _crossing; }
+    std::string transport_kind() const;
+    uint64_t items_moved() const { return _moved.load(); }
+
+private:
+    domain_adapter_remote(remote_role role, int crossing, const remote_edge_options& opt);
+    void pump();           // SEND: forward everything readable in the local ring
+    void poll_reverse();   // SEND: consume READER_DONE messages
+    void recv_loop();      // RECV thread body
+    void check_failed() const;
+    void notify_downstream();
+    bool local_is_device_side() const; // the side of the ring this adapter touches
+
+    remote_role _role;
+    int _crossing;
+    remote_edge_options _opt;
+    std::shared_ptr<remote::channel> _ch;
+    std::shared_ptr<remote::transport> _tr;
+    int _max_chunk = 0; // items per message (receiver's empty-ring writable count)
+    size_t _isz = 0;
+    int _device = -1;
+
+    std::atomic<uint64_t> _runs{ 0 };          // local runs started (reset_flags calls)
+    std::atomic<uint64_t> _remote_done{ 0 };   // DONE (RECV) / READER_DONE (SEND) messages
+    std::atomic<uint64_t> _moved{ 0 };
+    std::atomic<uint64_t> _reader_finished{ 0 }; // RECV: runs whose local reader finished
+    std::atomic<bool> _ready{ false };            // setup complete (_ch, _tr valid)
+    std::atomic<bool> _closing{ false };
+    std::atomic<bool> _thread_done{ false };      // RECV thread finished
+    std::thread _thr;
+    std::mutex _m;
+    std::condition_variable _cv; // RECV: space freed by the downstream block
+    std::exception_ptr _err;
+    std::atomic<bool> _failed{ false };
+    void* _stream = nullptr; // RECV thread's stream (device rings)
+    void* _scratch = nullptr; // RECV: discard area after the reader finished
+    size_t _scratch_bytes = 0;
+};
+
+class domain_adapter_remote_conf : public domain_adapter_conf
+{
+public:
+    using sptr = std::shared_ptr<domain_adapter_remote_conf>;
+    static sptr make(const remote_edge_options& opt = remote_edge_options())
+    {
+        return std::make_shared<domain_adapter_remote_conf>(opt);
+    }
+    explicit domain_adapter_remote_conf(const remote_edge_options& opt)
+        : domain_adapter_conf(buffer_preference_t::DOWNSTREAM), _opt(opt)
+    {
+    }
+    domain_adapter_sptr make_remote_adapter(port_sptr local_port, bool local_is_upstream, int crossing,
+                                            const std::string& name) override;
+    const remote_edge_options& options() const { return _opt; }
+
+private:
+    remote_edge_options _opt;
+};
+
+} // namespace gr

@@ -44,6 +44,12 @@ class flowgraph_monitor
 {
 public:
     explicit flowgraph_monitor(std::vector<std::shared_ptr<scheduler>>& scheds) : d_schedulers(scheds) {}
+    // drop the scheduler references (schedulers hold the monitor: break the cycle)
+    void release()
+    {
+        std::lock_guard<std::mutex> g(_m);
+        d_schedulers.clear();
+    }
     virtual ~flowgraph_monitor() = default;
 
     virtual void push_message(fg_monitor_message msg);

@@ -81,6 +81,11 @@ public:
         if (std::find(_connected_ports.begin(), _connected_ports.end(), other) == _connected_ports.end())
             _connected_ports.push_back(std::move(other));
     }
+    void disconnect(const sptr& other)
+    {
+        _connected_ports.erase(std::remove(_connected_ports.begin(), _connected_ports.end(), other),
+                               _connected_ports.end());
+    }
     const std::vector<sptr>& connected_ports() const { return _connected_ports; }
 
 protected:

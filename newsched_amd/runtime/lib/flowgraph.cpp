@@ -1,5 +1,6 @@
 // flowgraph + flowgraph_monitor (reference runtime/lib/flowgraph.cpp,
 // runtime/lib/flowgraph_monitor.cpp; drain-based completion, see flowgraph_monitor.hpp).
+#include <gnuradio/domain_adapter_remote.hpp>
 #include <gnuradio/flowgraph.hpp>
 #include <gnuradio/graph_utils.hpp>
 
@@ -80,6 +81,23 @@ flowgraph::~flowgraph()
         } catch (...) {
         }
     }
+    // Ownership cycles of a finished flowgraph: block ports point at their thread
+    // (neighbor interface) which owns the blocks; the monitor and the schedulers point at
+    // each other. Break them so threads, buffers and domain adapters (whose destructors
+    // close cross-process edges gracefully) are released with the flowgraph.
+    auto unhook = [](graph& g) {
+        for (auto& e : g.edges())
+            for (auto* n : { e->src().node().get(), e->dst().node().get() })
+                if (n)
+                    for (auto& p : n->all_ports()) p->set_parent_intf(nullptr);
+        for (auto& n : g.orphan_nodes())
+            for (auto& p : n->all_ports()) p->set_parent_intf(nullptr);
+    };
+    for (auto& fgs : d_flat_subgraphs)
+        if (fgs) unhook(*fgs);
+    if (d_flat_graph) unhook(*d_flat_graph);
+    unhook(*this);
+    if (d_fgmon) d_fgmon->release();
 }
 
 void flowgraph::set_scheduler(scheduler_sptr s) { set_schedulers({ std::move(s) }); }
@@ -99,10 +117,18 @@ void flowgraph::clear_schedulers() { d_schedulers.clear(); }
 
 void flowgraph::partition(std::vector<domain_conf>& confs)
 {
+    // Domains run by another process (remote_domain) are neither monitored nor started
+    // here; this process runs the local ones and its halves of the crossings.
+    d_schedulers.erase(std::remove_if(d_schedulers.begin(), d_schedulers.end(),
+                                      [](const scheduler_sptr& s) {
+                                          return std::dynamic_pointer_cast<remote_domain>(s) != nullptr;
+                                      }),
+                       d_schedulers.end());
     d_fgmon = std::make_shared<flowgraph_monitor>(d_schedulers);
     auto parts = graph_utils::partition(base(), d_schedulers, confs);
     d_flat_subgraphs.clear();
     for (auto& p : parts) {
+        if (std::dynamic_pointer_cast<remote_domain>(p.scheduler)) continue;
         d_flat_subgraphs.push_back(flat_graph::make_flat(p.subgraph));
         p.scheduler->initialize(d_flat_subgraphs.back(), d_fgmon, p.neighbor_map);
     }

@@ -2,6 +2,7 @@
 // domain_conf, replace every crossing edge with an adapter pair, and record the
 // neighbouring schedulers of the blocks at each crossing.
 #include <gnuradio/block.hpp>
+#include <gnuradio/domain_adapter_remote.hpp>
 #include <gnuradio/graph_utils.hpp>
 
 #include <algorithm>
@@ -56,7 +57,12 @@ graph_partition_info_vec graph_utils::partition(graph_sptr input_graph, std::vec
         }
     }
 
+    // Crossings are numbered in the order found above: identical in every process that
+    // builds the same flowgraph and domain_conf list, so crossing i names the same edge
+    // (and TCP port) on both sides of a process boundary.
+    int crossing_index = 0;
     for (auto& c : crossings) {
+        const int xi = crossing_index++;
         auto src_node = c.e->src().node();
         auto dst_node = c.e->dst().node();
         if (!blk_part.count(src_node->id()) || !blk_part.count(dst_node->id()))
@@ -68,8 +74,31 @@ graph_partition_info_vec graph_utils::partition(graph_sptr input_graph, std::vec
         if (!da_conf) da_conf = conf.da_conf();
         if (!da_conf) throw std::runtime_error("domain crossing without a domain_adapter_conf");
 
-        auto pair = da_conf->make_domain_adapter_pair(c.e->src().port(), c.e->dst().port(),
-                                                      "da_" + src_node->alias() + "->" + dst_node->alias());
+        const bool src_remote = std::dynamic_pointer_cast<remote_domain>(blk_sched[src_node->id()]) != nullptr;
+        const bool dst_remote = std::dynamic_pointer_cast<remote_domain>(blk_sched[dst_node->id()]) != nullptr;
+        const std::string name = "da_" + src_node->alias() + "->" + dst_node->alias();
+        if (src_remote && dst_remote) continue; // neither end runs here
+        if (src_remote || dst_remote) {
+            // the far block does not run in this process: notifications must stop at the
+            // adapter instead of reaching its (scheduler-less) port
+            c.e->src().port()->disconnect(c.e->dst().port());
+            c.e->dst().port()->disconnect(c.e->src().port());
+            // one half only; the other process builds the matching half for crossing xi
+            if (!src_remote) {
+                auto up = da_conf->make_remote_adapter(c.e->src().port(), true, xi, name);
+                ret[blk_part[src_node->id()]]
+                    .subgraph->connect(c.e->src(), node_endpoint(up, up->all_ports()[0]))
+                    ->set_custom_buffer(c.e->buffer_factory(), c.e->buf_properties());
+            } else {
+                auto down = da_conf->make_remote_adapter(c.e->dst().port(), false, xi, name);
+                ret[blk_part[dst_node->id()]]
+                    .subgraph->connect(node_endpoint(down, down->all_ports()[0]), c.e->dst())
+                    ->set_custom_buffer(c.e->buffer_factory(), c.e->buf_properties());
+            }
+            continue;
+        }
+
+        auto pair = da_conf->make_domain_adapter_pair(c.e->src().port(), c.e->dst().port(), name);
         auto up = pair.first;    // takes the upstream block's output
         auto down = pair.second; // feeds the downstream block's input
         ret[blk_part[src_node->id()]]

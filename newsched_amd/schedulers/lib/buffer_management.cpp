@@ -24,7 +24,7 @@ void buffer_manager::initialize_buffers(flat_graph_sptr fg, buffer_factory_funct
         if (da) {
             if (da->buffer_location() == buffer_location_t::LOCAL) {
                 da->set_buffer(make_buf(e));
-                if (auto dd = std::dynamic_pointer_cast<domain_adapter_direct>(da)) dd->publish();
+                da->buffer_ready(); // direct: publish to the peer; remote: connect + handshake
             }
             d_edge_buffers[e.get()] = std::dynamic_pointer_cast<buffer>(da);
         } else {

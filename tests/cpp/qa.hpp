@@ -3,7 +3,10 @@
 // command line (or all) and returns nonzero on any failure.
 #pragma once
 #include <chrono>
+#include <csignal>
 #include <cstdio>
+#include <cstdlib>
+#include <unistd.h>
 #include <cstring>
 #include <functional>
 #include <sstream>
@@ -56,9 +59,29 @@ inline void fail(const char* file, int line, const std::string& what)
         }                                                       \
     } while (0)
 
+namespace qa {
+inline const char*& current_name()
+{
+    static const char* n = "";
+    return n;
+}
+// Watchdog: a case that hangs fails with its name instead of stalling the whole suite.
+inline void on_alarm(int)
+{
+    const char* a = "\n  TIMEOUT in ";
+    (void)!write(2, a, std::strlen(a));
+    (void)!write(2, current_name(), std::strlen(current_name()));
+    (void)!write(2, "\n", 1);
+    _exit(3);
+}
+} // namespace qa
+
 int main(int argc, char** argv)
 {
     int run = 0;
+    const char* tmo = std::getenv("QA_CASE_TIMEOUT");
+    const unsigned case_timeout = tmo ? (unsigned)std::atoi(tmo) : 240u;
+    std::signal(SIGALRM, qa::on_alarm);
     for (auto& t : qa::registry()) {
         bool sel = argc < 2;
         for (int i = 1; i < argc; ++i)
@@ -66,11 +89,14 @@ int main(int argc, char** argv)
         if (!sel) continue;
         const int before = qa::failures();
         const auto t0 = std::chrono::steady_clock::now();
+        qa::current_name() = t.name.c_str();
+        alarm(case_timeout);
         try {
             t.fn();
         } catch (const std::exception& e) {
             qa::fail(__FILE__, __LINE__, std::string("exception: ") + e.what());
         }
+        alarm(0);
         const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         std::printf("[%s] %s (%.3f s)\n", qa::failures() == before ? " OK " : "FAIL", t.name.c_str(), s);
         ++run;
