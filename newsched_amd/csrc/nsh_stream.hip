@@ -39,6 +39,60 @@ __device__ __forceinline__ void st_nt(float4* p, float4 v)
     __builtin_nontemporal_store(w, reinterpret_cast<nf4*>(p));
 }
 
+// Blocked grid-stride: each workgroup step covers kUnroll x kBlock float4s, all loads issued
+// before the first store (4 x 16 B in flight per lane); the grid is sized to ~64 Ki
+// workgroups so every CU has many waves in flight (tools/probe/copy_variants.hip:
+// nontemporal, unroll 4, large grid = the measured copy ceiling).
+constexpr int kUnroll = 4;
+inline unsigned tile_grid(int64_t n_vec)
+{
+    int64_t g = (n_vec + (int64_t)kBlock * kUnroll - 1) / ((int64_t)kBlock * kUnroll);
+    const int64_t cap = 65536;
+    if (g > cap) g = cap;
+    if (g < 1) g = 1;
+    return (unsigned)g;
+}
+template <class F>
+__device__ __forceinline__ void tiles_unary(const float4* __restrict__ in, float4* __restrict__ out, int64_t nv, F f)
+{
+    const int64_t step = (int64_t)gridDim.x * kBlock * kUnroll;
+    for (int64_t base = (int64_t)blockIdx.x * kBlock * kUnroll + threadIdx.x; base < nv; base += step) {
+        float4 v[kUnroll];
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            const int64_t i = base + (int64_t)u * kBlock;
+            if (i < nv) v[u] = ld_nt(in + i);
+        }
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            const int64_t i = base + (int64_t)u * kBlock;
+            if (i < nv) st_nt(out + i, f(v[u]));
+        }
+    }
+}
+template <class F>
+__device__ __forceinline__ void tiles_binary(const float4* __restrict__ a, const float4* __restrict__ b,
+                                             float4* __restrict__ out, int64_t nv, F f)
+{
+    const int64_t step = (int64_t)gridDim.x * kBlock * kUnroll;
+    for (int64_t base = (int64_t)blockIdx.x * kBlock * kUnroll + threadIdx.x; base < nv; base += step) {
+        float4 x[kUnroll], y[kUnroll];
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            const int64_t i = base + (int64_t)u * kBlock;
+            if (i < nv) {
+                x[u] = ld_nt(a + i);
+                y[u] = ld_nt(b + i);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            const int64_t i = base + (int64_t)u * kBlock;
+            if (i < nv) st_nt(out + i, f(x[u], y[u]));
+        }
+    }
+}
+
 __device__ __forceinline__ float2 cmul(float2 a, float2 k)
 {
     return make_float2(__fsub_rn(__fmul_rn(a.x, k.x), __fmul_rn(a.y, k.y)),
@@ -76,13 +130,11 @@ __global__ __launch_bounds__(kBlock) void k_map_c_v4(const float4* __restrict__ 
                                                      int64_t n_vec,
                                                      Op op)
 {
-    const int64_t stride = (int64_t)gridDim.x * kBlock;
-    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n_vec; i += stride) {
-        float4 v = ld_nt(in + i);
-        float2 a = op(make_float2(v.x, v.y));
-        float2 b = op(make_float2(v.z, v.w));
-        st_nt(out + i, make_float4(a.x, a.y, b.x, b.y));
-    }
+    tiles_unary(in, out, n_vec, [&](float4 v) {
+        const float2 a = op(make_float2(v.x, v.y));
+        const float2 b = op(make_float2(v.z, v.w));
+        return make_float4(a.x, a.y, b.x, b.y);
+    });
 }
 template <class Op>
 __global__ __launch_bounds__(kBlock) void k_map_c_v2(const float2* __restrict__ in,
@@ -103,7 +155,7 @@ int launch_map_c(const float* in, float* out, int64_t n, Op op, hipStream_t s, c
     if (a16) {
         const int64_t nv = n / 2;
         if (nv > 0) {
-            hipLaunchKernelGGL(k_map_c_v4<Op>, dim3(nsh::stream_grid(nv, kBlock)), dim3(kBlock), 0, s,
+            hipLaunchKernelGGL(k_map_c_v4<Op>, dim3(tile_grid(nv)), dim3(kBlock), 0, s,
                                (const float4*)in, (float4*)out, nv, op);
             NSH_CK_LAUNCH(what);
         }
@@ -135,14 +187,11 @@ __global__ __launch_bounds__(kBlock) void k_bin_v4(const float4* __restrict__ a,
                                                    float4* __restrict__ out,
                                                    int64_t n_vec)
 {
-    const int64_t stride = (int64_t)gridDim.x * kBlock;
-    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n_vec; i += stride) {
-        float4 x = ld_nt(a + i);
-        float4 y = ld_nt(b + i);
-        float2 p = bin<OP>(make_float2(x.x, x.y), make_float2(y.x, y.y));
-        float2 q = bin<OP>(make_float2(x.z, x.w), make_float2(y.z, y.w));
-        st_nt(out + i, make_float4(p.x, p.y, q.x, q.y));
-    }
+    tiles_binary(a, b, out, n_vec, [](float4 x, float4 y) {
+        const float2 p = bin<OP>(make_float2(x.x, x.y), make_float2(y.x, y.y));
+        const float2 q = bin<OP>(make_float2(x.z, x.w), make_float2(y.z, y.w));
+        return make_float4(p.x, p.y, q.x, q.y);
+    });
 }
 template <int OP>
 __global__ __launch_bounds__(kBlock) void k_bin_v2(const float2* __restrict__ a,
@@ -162,7 +211,7 @@ int launch_bin(const float* a, const float* b, float* out, int64_t n, hipStream_
     if (a16) {
         const int64_t nv = n / 2;
         if (nv > 0) {
-            hipLaunchKernelGGL(k_bin_v4<OP>, dim3(nsh::stream_grid(nv, kBlock)), dim3(kBlock), 0, s,
+            hipLaunchKernelGGL(k_bin_v4<OP>, dim3(tile_grid(nv)), dim3(kBlock), 0, s,
                                (const float4*)a, (const float4*)b, (float4*)out, nv);
             NSH_CK_LAUNCH(what);
         }
@@ -180,21 +229,17 @@ int launch_bin(const float* a, const float* b, float* out, int64_t n, hipStream_
 }
 
 // Byte copy, 16 B per lane (copy.cu:6-17 restated once per work() instead of per vector).
-__global__ __launch_bounds__(kBlock) void k_copy_v4(const nu4* __restrict__ in, nu4* __restrict__ out, int64_t nv)
+__global__ __launch_bounds__(kBlock) void k_copy_v4(const float4* __restrict__ in, float4* __restrict__ out, int64_t nv)
 {
-    const int64_t stride = (int64_t)gridDim.x * kBlock;
-    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nv; i += stride)
-        __builtin_nontemporal_store(__builtin_nontemporal_load(in + i), out + i);
+    tiles_unary(in, out, nv, [](float4 v) { return v; }); // bits moved as-is (no arithmetic)
 }
 
 // f32 scalar map (multiply_const_ff), 4 floats per lane.
 __global__ __launch_bounds__(kBlock) void k_mulc_f_v4(const float4* __restrict__ in, float4* __restrict__ out, int64_t nv, float k)
 {
-    const int64_t stride = (int64_t)gridDim.x * kBlock;
-    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nv; i += stride) {
-        float4 v = ld_nt(in + i);
-        st_nt(out + i, make_float4(__fmul_rn(v.x, k), __fmul_rn(v.y, k), __fmul_rn(v.z, k), __fmul_rn(v.w, k)));
-    }
+    tiles_unary(in, out, nv, [k](float4 v) {
+        return make_float4(__fmul_rn(v.x, k), __fmul_rn(v.y, k), __fmul_rn(v.z, k), __fmul_rn(v.w, k));
+    });
 }
 __global__ __launch_bounds__(kBlock) void k_mulc_f_v1(const float* __restrict__ in, float* __restrict__ out, int64_t n, float k)
 {
@@ -235,8 +280,7 @@ int nsh_copy(const void* in, void* out, size_t bytes, void* stream)
     hipStream_t s = nsh::S(stream);
     if ((uintptr_t)in % 16 == 0 && (uintptr_t)out % 16 == 0 && bytes >= 16) {
         const int64_t nv = (int64_t)(bytes / 16);
-        hipLaunchKernelGGL(k_copy_v4, dim3(nsh::stream_grid(nv, kBlock)), dim3(kBlock), 0, s,
-                           (const nu4*)in, (nu4*)out, nv);
+        hipLaunchKernelGGL(k_copy_v4, dim3(tile_grid(nv)), dim3(kBlock), 0, s, (const float4*)in, (float4*)out, nv);
         NSH_CK_LAUNCH("nsh_copy");
         const size_t done = (size_t)nv * 16;
         if (done < bytes)
@@ -259,7 +303,7 @@ int nsh_mul_const_ff(const float* in, float* out, int64_t n, float k, void* stre
     if ((uintptr_t)in % 16 == 0 && (uintptr_t)out % 16 == 0) {
         const int64_t nv = n / 4;
         if (nv) {
-            hipLaunchKernelGGL(k_mulc_f_v4, dim3(nsh::stream_grid(nv, kBlock)), dim3(kBlock), 0, s,
+            hipLaunchKernelGGL(k_mulc_f_v4, dim3(tile_grid(nv)), dim3(kBlock), 0, s,
                                (const float4*)in, (float4*)out, nv, k);
             NSH_CK_LAUNCH("nsh_mul_const_ff");
         }

@@ -48,6 +48,9 @@ def main():
     res["copy"] = {"ms": ms, "GB/s": 16 * n / ms / 1e6}
     ms = timeit(lambda: nsh.mul_const_chain_cc(x, y, n, [np.exp(0.1j), np.exp(0.2j), np.exp(0.3j), np.exp(0.4j)], stream=s), a.reps, s)
     res["mulchain4"] = {"ms": ms, "GS/s": n / ms / 1e6, "GB/s": 16 * n / ms / 1e6}
+    z = torch.empty_like(x)
+    ms = timeit(lambda: nsh.add_cc(x, y, z, n, stream=s), a.reps, s)
+    res["add_cc"] = {"ms": ms, "GS/s": n / ms / 1e6, "GB/s": 24 * n / ms / 1e6}
     ms = timeit(lambda: nsh.fft1024(x, y, n // 1024, stream=s), a.reps, s)
     res["fft1024"] = {"ms": ms, "GS/s": n / ms / 1e6, "GB/s": 16 * n / ms / 1e6}
     w = torch.ones(1024, dtype=torch.complex64, device="cuda")
