@@ -14,7 +14,8 @@
 //    staged samples; taps come from the scalar cache (s_load, uniform index). LDS rows
 //    are padded by one sample every R*D samples so the per-lane ds_read_b64 of the window
 //    is bank-conflict-free. Exact fp32 products, fp32 accumulation in tap order.
-//  * MFMA -- bf16x3 split-precision Toeplitz MFMA (nsh_fir_mfma.hip), decim 1.
+//  * MFMA / MFMA16 -- bf16x3 split-precision Toeplitz MFMA on 32- / 16-sample blocks
+//    (nsh_fir_mfma.hip), decim 1.
 #include "nsh_common.hpp"
 
 #include <algorithm>
@@ -159,13 +160,23 @@ int nsh_fir_plan_create(int dev, const float* taps_host, int ntaps, int decim, i
         delete p;
         return nsh::fail(e, "nsh_fir_plan_create: taps upload");
     }
+    if (algo < NSH_FIR_AUTO || algo > NSH_FIR_MFMA16) {
+        (void)hipFree(p->taps_dev);
+        delete p;
+        return nsh::fail_msg("nsh_fir_plan_create: unknown algorithm");
+    }
     int resolved = algo;
     if (algo == NSH_FIR_AUTO) resolved = nsh_fir_mfma_supported(p) ? NSH_FIR_MFMA : NSH_FIR_DIRECT;
-    if (resolved == NSH_FIR_MFMA) {
-        if (!nsh_fir_mfma_supported(p)) {
+    if (resolved == NSH_FIR_MFMA16 && !nsh_fir_mfma16_supported(p)) {
+        (void)hipFree(p->taps_dev);
+        delete p;
+        return nsh::fail_msg("nsh_fir_plan_create: MFMA16 form needs decim 1, finite taps and ntaps <= 145");
+    }
+    if (resolved == NSH_FIR_MFMA || resolved == NSH_FIR_MFMA16) {
+        if (resolved == NSH_FIR_MFMA && !nsh_fir_mfma_supported(p)) {
             (void)hipFree(p->taps_dev);
             delete p;
-            return nsh::fail_msg("nsh_fir_plan_create: MFMA form needs decim 1 and ntaps <= 513");
+            return nsh::fail_msg("nsh_fir_plan_create: MFMA form needs decim 1, finite taps and ntaps <= 161");
         }
         const int rc = nsh_fir_mfma_prepare(p);
         if (rc) {
@@ -185,6 +196,7 @@ int nsh_fir_plan_destroy(void* plan)
     if (!p) return 0;
     if (p->taps_dev) (void)hipFree(p->taps_dev);
     if (p->frag_dev) (void)hipFree(p->frag_dev);
+    if (p->frag16_dev) (void)hipFree(p->frag16_dev);
     delete p;
     return 0;
 }
@@ -200,6 +212,8 @@ int nsh_fir_ccf(void* plan, const float* in, const float* hist_in, float* hist_o
     hipStream_t s = nsh::S(stream);
     if (p->algo == NSH_FIR_MFMA)
         return nsh_fir_mfma_run(p, (const float2*)in, (const float2*)hist_in, (float2*)hist_out, (float2*)out, n_out, s);
+    if (p->algo == NSH_FIR_MFMA16)
+        return nsh_fir_mfma16_run(p, (const float2*)in, (const float2*)hist_in, (float2*)hist_out, (float2*)out, n_out, s);
     return run_direct(p, (const float2*)in, (const float2*)hist_in, (float2*)hist_out, (float2*)out, n_out, s);
 }
 

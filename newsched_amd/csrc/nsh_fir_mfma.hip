@@ -48,6 +48,7 @@
 namespace {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
 typedef float nf4 __attribute__((ext_vector_type(4)));
 typedef float nf2 __attribute__((ext_vector_type(2)));
@@ -184,6 +185,27 @@ __device__ __forceinline__ void compute_tile(const unsigned char* lds,
         acc_hi = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0, B0[st], acc_hi, 0, 0, 0);
         acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1, B0[st], acc_lo, 0, 0, 0);
         acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A2, B2[st], acc_lo, 0, 0, 0);
+        continue;
+#endif
+#if NSH_FIR_ABLATE & 64 // timing only: the same FLOPs as 2 x v_mfma_f32_16x16x32_bf16 per product
+        {
+            typedef float f32x4 __attribute__((ext_vector_type(4)));
+            typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+            f32x4 c0 = { acc_hi[0], acc_hi[1], acc_hi[2], acc_hi[3] }, c1 = { acc_lo[0], acc_lo[1], acc_lo[2], acc_lo[3] };
+#pragma unroll
+            for (int rep = 0; rep < 2; ++rep) {
+                c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A0, B0[st], c0, 0, 0, 0);
+                c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A0, B1[st], c1, 0, 0, 0);
+                c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A1, B0[st], c1, 0, 0, 0);
+                c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A0, B2[st], c1, 0, 0, 0);
+                c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A1, B1[st], c1, 0, 0, 0);
+                c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A2, B0[st], c1, 0, 0, 0);
+            }
+            for (int t = 0; t < 4; ++t) {
+                acc_hi[t] = c0[t];
+                acc_lo[t] = c1[t];
+            }
+        }
         continue;
 #endif
 #if NSH_FIR_ABLATE & 32 // timing only: the int8 instruction count (6 x i32_32x32x32_i8 per 2 k-steps)
@@ -530,6 +552,322 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma2(const float2* __restrict__
     }
 }
 
+// ---- v5: 16-phase blocks on v_mfma_f32_16x16x32_bf16 -------------------------------------
+// Same Toeplitz GEMM with 16-sample blocks: y[16b + i] = sum_q sum_{r<16} h[i - r + 16q] x[16(b-q) + r],
+// q < QH = ceil((L + 15) / 16) (9 for L = 127), K = 16 QH padded to the 32 of one k-step.
+// Under this kernel's power-limited clock the 16x16x32 form issues the same FLOPs faster
+// (ablation mask 64: -5 % min, -10 % median vs 32x32x16), the tap fragments need half the
+// VGPRs (3 x KS x 4) and the LDS rows need no padding:
+//   * rows of 16 samples = 32 B per bf16 plane, packed; A-fragment row rho = l & 15 is
+//     (component c = rho & 1, block b = rho >> 1), k-group g = l >> 4 reads 16 B of row
+//     (b - q), q = 2s + (g >> 1); with the im planes at an offset = 128 mod 256 B every
+//     16-lane ds_read_b128 group covers 16 distinct 16-B slots (searched exhaustively);
+//   * C row 4g + reg = (c = reg & 1, b = 2g + (reg >> 1)): re and im of a block land in
+//     the same lane (regs 0/1 and 2/3), stored as float2 without lane exchanges.
+// A wave owns 512 outputs = 4 row-tiles of 8 blocks; tap fragments are shared by the tiles.
+template <int QH>
+struct geom5 {
+    static constexpr int NT = 256;
+    static constexpr int CHUNK = 2048;
+    static constexpr int KS = QH / 2;                          // full k-steps of 32 (16x16x32)
+    static constexpr int TAIL = QH % 2;                        // one k-step of 16 (16x16x16)
+    static constexpr int H = 16 * (QH - 1);                    // halo samples
+    static constexpr int HR = QH - 1;                          // halo rows
+    static constexpr int NB = (CHUNK + H) / 16;                // rows per buffer
+    static constexpr int PLANE = NB * 32;
+    static constexpr int IM_OFF = (3 * PLANE + 255) / 256 * 256 + 128;
+    static constexpr int BUF = (IM_OFF + 3 * PLANE + 255) / 256 * 256;
+    static constexpr int LDS = 2 * BUF;
+    static constexpr int VPT = CHUNK / 2 / NT;                 // 4 float4 per thread
+    static constexpr int TILES = 4;                            // row-tiles per wave
+};
+
+template <int QH>
+__device__ __forceinline__ void v5_store_pair(unsigned char* buf, int s, float a_re, float b_re, float a_im,
+                                              float b_im)
+{
+    using G = geom5<QH>;
+    const int off = (s >> 4) * 32 + (s & 15) * 2;
+    unsigned r1, r2, r3, i1, i2, i3;
+#if NSH_FIR_ABLATE & 4
+    r1 = r2 = r3 = __float_as_uint(a_re);
+    i1 = i2 = i3 = __float_as_uint(a_im);
+#else
+    split_pair(a_re, b_re, r1, r2, r3);
+    split_pair(a_im, b_im, i1, i2, i3);
+#endif
+    *reinterpret_cast<unsigned*>(buf + 0 * G::PLANE + off) = r1;
+    *reinterpret_cast<unsigned*>(buf + 1 * G::PLANE + off) = r2;
+    *reinterpret_cast<unsigned*>(buf + 2 * G::PLANE + off) = r3;
+    *reinterpret_cast<unsigned*>(buf + G::IM_OFF + 0 * G::PLANE + off) = i1;
+    *reinterpret_cast<unsigned*>(buf + G::IM_OFF + 1 * G::PLANE + off) = i2;
+    *reinterpret_cast<unsigned*>(buf + G::IM_OFF + 2 * G::PLANE + off) = i3;
+}
+
+template <int QH>
+__device__ __forceinline__ void v5_load_main(float4 (&v)[geom5<QH>::VPT], const float2* __restrict__ in,
+                                             const float2* __restrict__ hist, int64_t ch, int64_t n_in, int L,
+                                             bool in_aligned)
+{
+    using G = geom5<QH>;
+    const int64_t g0 = ch * G::CHUNK;
+#if NSH_FIR_ABLATE & 2
+    for (int u = 0; u < G::VPT; ++u) v[u] = make_float4((float)g0, (float)u, (float)threadIdx.x, 1.f);
+    return;
+#endif
+    if (in_aligned && g0 + G::CHUNK <= n_in) {
+        const nf4* src = reinterpret_cast<const nf4*>(in + g0);
+#pragma unroll
+        for (int u = 0; u < G::VPT; ++u) {
+            const nf4 t = __builtin_nontemporal_load(src + threadIdx.x + G::NT * u);
+            v[u] = make_float4(t.x, t.y, t.z, t.w);
+        }
+    } else {
+#pragma unroll
+        for (int u = 0; u < G::VPT; ++u) {
+            const int vi = threadIdx.x + G::NT * u;
+            const float2 a = virt(in, hist, g0 + 2 * vi, n_in, L);
+            const float2 b = virt(in, hist, g0 + 2 * vi + 1, n_in, L);
+            v[u] = make_float4(a.x, a.y, b.x, b.y);
+        }
+    }
+}
+
+template <int QH>
+__device__ __forceinline__ void v5_store_main(const float4 (&v)[geom5<QH>::VPT], unsigned char* buf)
+{
+    using G = geom5<QH>;
+#pragma unroll
+    for (int u = 0; u < G::VPT; ++u)
+        v5_store_pair<QH>(buf, G::H + 2 * (threadIdx.x + G::NT * u), v[u].x, v[u].z, v[u].y, v[u].w);
+}
+
+template <int QH>
+__device__ __forceinline__ void v5_copy_halo(const unsigned char* cur, unsigned char* nxt)
+{
+    using G = geom5<QH>;
+    constexpr int PIECES = 6 * G::HR * 2; // 16-B pieces (32 B per row)
+    if constexpr (PIECES > 0) {
+        for (int t = threadIdx.x; t < PIECES; t += G::NT) {
+            const int plane = t / (G::HR * 2);
+            const int rem = t % (G::HR * 2);
+            const int pbase = (plane < 3 ? 0 : G::IM_OFF) + (plane % 3) * G::PLANE;
+            const uint4 d = *reinterpret_cast<const uint4*>(cur + pbase + (G::NB - G::HR) * 32 + rem * 16);
+            *reinterpret_cast<uint4*>(nxt + pbase + rem * 16) = d;
+        }
+    }
+}
+
+template <int QH>
+__device__ __forceinline__ void v5_load_store_halo(unsigned char* buf, const float2* __restrict__ in,
+                                                   const float2* __restrict__ hist, int64_t ch, int64_t n_in, int L)
+{
+    using G = geom5<QH>;
+    if constexpr (G::H > 0) {
+        const int64_t g0 = ch * G::CHUNK - G::H;
+        for (int p = threadIdx.x; p < G::H / 2; p += G::NT) {
+            const float2 a = virt(in, hist, g0 + 2 * p, n_in, L);
+            const float2 b = virt(in, hist, g0 + 2 * p + 1, n_in, L);
+            v5_store_pair<QH>(buf, 2 * p, a.x, b.x, a.y, b.y);
+        }
+    }
+}
+
+// The wave's 4 row-tiles x (KS k-steps of 32 + an optional tail of 16).
+template <int QH>
+__device__ __forceinline__ void v5_compute(const unsigned char* lds, const bf16x8 (&B0)[geom5<QH>::KS + 1],
+                                           const bf16x8 (&B1)[geom5<QH>::KS + 1], const bf16x8 (&B2)[geom5<QH>::KS + 1],
+                                           const bf16x4 (&T)[3], int64_t n_tile, int64_t n_out,
+                                           float2* __restrict__ out)
+{
+    using G = geom5<QH>;
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int rho = lane & 15;
+    const int c = rho & 1, b = rho >> 1;
+    const int g = lane >> 4;
+    const int phase = lane & 15;
+    const int row_base = c * G::IM_OFF + (G::HR + wave * 32 + b) * 32; // this lane's block row, q = 0
+    f32x4 hi[G::TILES], lo[G::TILES];
+#pragma unroll
+    for (int t = 0; t < G::TILES; ++t) {
+        hi[t] = f32x4{ 0.f, 0.f, 0.f, 0.f };
+        lo[t] = f32x4{ 0.f, 0.f, 0.f, 0.f };
+    }
+#pragma unroll
+    for (int st = 0; st < G::KS; ++st) {
+        const int q = 2 * st + (g >> 1);
+#pragma unroll
+        for (int t = 0; t < G::TILES; ++t) {
+            const int off = row_base + t * 8 * 32 - q * 32 + (g & 1) * 16;
+            const bf16x8 A0 = *reinterpret_cast<const bf16x8*>(lds + off);
+            const bf16x8 A1 = *reinterpret_cast<const bf16x8*>(lds + off + G::PLANE);
+            const bf16x8 A2 = *reinterpret_cast<const bf16x8*>(lds + off + 2 * G::PLANE);
+#if NSH_FIR_ABLATE & 1
+            hi[t][0] += (float)A0[0] + (float)A1[1] + (float)A2[2] + (float)B0[st][0] + (float)B1[st][1] + (float)B2[st][2];
+            continue;
+#endif
+            hi[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A0, B0[st], hi[t], 0, 0, 0);
+            lo[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A0, B1[st], lo[t], 0, 0, 0);
+            lo[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A1, B0[st], lo[t], 0, 0, 0);
+            lo[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A0, B2[st], lo[t], 0, 0, 0);
+            lo[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A1, B1[st], lo[t], 0, 0, 0);
+            lo[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A2, B0[st], lo[t], 0, 0, 0);
+        }
+    }
+    if constexpr (G::TAIL) {
+        // q = QH - 1 alone: v_mfma_f32_16x16x16_bf16, lane l holds A[l & 15][k = 4(l >> 4) + j]
+#pragma unroll
+        for (int t = 0; t < G::TILES; ++t) {
+            const int off = row_base + t * 8 * 32 - (QH - 1) * 32 + g * 8;
+            const bf16x4 A0 = *reinterpret_cast<const bf16x4*>(lds + off);
+            const bf16x4 A1 = *reinterpret_cast<const bf16x4*>(lds + off + G::PLANE);
+            const bf16x4 A2 = *reinterpret_cast<const bf16x4*>(lds + off + 2 * G::PLANE);
+#if NSH_FIR_ABLATE & 1
+            hi[t][1] += (float)A0[0] + (float)A1[1] + (float)A2[2] + (float)T[0][0] + (float)T[1][1] + (float)T[2][2];
+            continue;
+#endif
+            hi[t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(A0, T[0], hi[t], 0, 0, 0);
+            lo[t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(A0, T[1], lo[t], 0, 0, 0);
+            lo[t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(A1, T[0], lo[t], 0, 0, 0);
+            lo[t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(A0, T[2], lo[t], 0, 0, 0);
+            lo[t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(A1, T[1], lo[t], 0, 0, 0);
+            lo[t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(A2, T[0], lo[t], 0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < G::TILES; ++t) {
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+            const int blk = t * 8 + 2 * g + half;
+            const int64_t n = n_tile + (int64_t)wave * TILE + blk * 16 + phase;
+            const float re = hi[t][2 * half] + lo[t][2 * half];
+            const float im = hi[t][2 * half + 1] + lo[t][2 * half + 1];
+#if NSH_FIR_ABLATE & 8
+            if (re == 1.2345e-30f && n < n_out) {
+#else
+            if (n < n_out) {
+#endif
+                nf2 o = { re, im };
+                __builtin_nontemporal_store(o, reinterpret_cast<nf2*>(out + n));
+            }
+        }
+    }
+}
+
+template <int QH, int DEPTH>
+__global__ __launch_bounds__(256, 2) void k_fir_mfma5(const float2* __restrict__ in,
+                                                     const float2* __restrict__ hist_in,
+                                                     float2* __restrict__ hist_out,
+                                                     float2* __restrict__ out,
+                                                     const bf16x8* __restrict__ frag, // [3][KS][64] + tail [3][64] x4
+                                                     int L,
+                                                     int64_t n_out,
+                                                     int in_aligned)
+{
+    using G = geom5<QH>;
+    constexpr int KS = G::KS;
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int64_t n_in = n_out;
+
+    if (blockIdx.x == 0) {
+        for (int j = tid; j < L - 1; j += G::NT) hist_out[j] = virt(in, hist_in, n_in - (L - 1) + j, n_in, L);
+    }
+
+    bf16x8 B0[KS + 1], B1[KS + 1], B2[KS + 1]; // +1: keeps the arrays non-empty for QH = 1
+#pragma unroll
+    for (int st = 0; st < KS; ++st) {
+        B0[st] = frag[(0 * KS + st) * 64 + lane];
+        B1[st] = frag[(1 * KS + st) * 64 + lane];
+        B2[st] = frag[(2 * KS + st) * 64 + lane];
+    }
+    bf16x4 T[3] = {};
+    if constexpr (G::TAIL) {
+        const bf16x4* tf = reinterpret_cast<const bf16x4*>(frag + 3 * KS * 64);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) T[k] = tf[k * 64 + lane];
+    }
+
+    const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
+    const int64_t per = (nchunks + gridDim.x - 1) / gridDim.x;
+    const int64_t c_begin = (int64_t)blockIdx.x * per;
+    const int64_t c_end = c_begin + per < nchunks ? c_begin + per : nchunks;
+    if (c_begin >= c_end) return;
+    const int64_t c_last = c_end - 1;
+    const bool al = in_aligned != 0;
+    auto clamp = [&](int64_t x) { return x <= c_last ? x : c_last; };
+
+    float4 va[G::VPT], vb[G::VPT], vc[G::VPT];
+    v5_load_store_halo<QH>(lds, in, hist_in, c_begin, n_in, L);
+    v5_load_main<QH>(va, in, hist_in, c_begin, n_in, L, al);
+    v5_store_main<QH>(va, lds);
+    v5_load_main<QH>(va, in, hist_in, clamp(c_begin + 1), n_in, L, al);
+    if constexpr (DEPTH > 1) v5_load_main<QH>(vb, in, hist_in, clamp(c_begin + 2), n_in, L, al);
+    __syncthreads();
+
+    auto step = [&](float4 (&nxt)[G::VPT], float4 (&ld)[G::VPT], int64_t ch) {
+        unsigned char* cur = lds + ((ch - c_begin) & 1) * G::BUF;
+        unsigned char* nbuf = lds + (((ch - c_begin) & 1) ^ 1) * G::BUF;
+        v5_load_main<QH>(ld, in, hist_in, clamp(ch + 1 + DEPTH), n_in, L, al);
+        v5_copy_halo<QH>(cur, nbuf);
+        v5_store_main<QH>(nxt, nbuf);
+        v5_compute<QH>(cur, B0, B1, B2, T, ch * G::CHUNK, n_out, out);
+        __syncthreads();
+    };
+    int64_t ch = c_begin;
+    if constexpr (DEPTH == 1) {
+        for (; ch + 1 <= c_last; ch += 2) {
+            step(va, vb, ch);
+            step(vb, va, ch + 1);
+        }
+        if (ch <= c_last) step(va, vb, ch);
+    } else {
+        for (; ch + 2 <= c_last; ch += 3) {
+            step(va, vc, ch);
+            step(vb, va, ch + 1);
+            step(vc, vb, ch + 2);
+        }
+        if (ch <= c_last) step(va, vc, ch++);
+        if (ch <= c_last) step(vb, va, ch);
+    }
+}
+
+template <int QH, int DEPTH>
+int launch_v5(const nsh_fir_plan* p, const float2* in, const float2* hin, float2* hout, float2* out, int64_t n_out,
+              hipStream_t s, int wg_per_cu)
+{
+    using G = geom5<QH>;
+    static bool attr_set = false;
+    if (!attr_set) {
+        NSH_CK(hipFuncSetAttribute((const void*)k_fir_mfma5<QH, DEPTH>, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
+        attr_set = true;
+    }
+    const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
+    int n_cu = 256;
+    (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, p->dev);
+    const int64_t max_grid = (int64_t)n_cu * wg_per_cu;
+    const unsigned grid = (unsigned)(nchunks < max_grid ? nchunks : max_grid);
+    const int aligned = ((uintptr_t)in % 16 == 0) ? 1 : 0;
+    hipLaunchKernelGGL((k_fir_mfma5<QH, DEPTH>), dim3(grid), dim3(G::NT), G::LDS, s, in, hin, hout, out,
+                       (const bf16x8*)p->frag16_dev, p->L, n_out, aligned);
+    NSH_CK_LAUNCH("nsh_fir_ccf(mfma5)");
+    return 0;
+}
+
+template <int QH>
+int launch_qh(const nsh_fir_plan* p, const float2* in, const float2* hin, float2* hout, float2* out, int64_t n_out,
+              hipStream_t s)
+{
+    switch (p->variant) {
+    case 20: return launch_v5<QH, 2>(p, in, hin, hout, out, n_out, s, 2);
+    case 22: return launch_v5<QH, 1>(p, in, hin, hout, out, n_out, s, 2);
+    default: return launch_v5<QH, 1>(p, in, hin, hout, out, n_out, s, 3); // 163 VGPRs: 3 waves/SIMD
+    }
+}
+
 // Host-side bf16 round-to-nearest-even (taps are finite).
 unsigned short bf16_rne(float f)
 {
@@ -644,11 +982,82 @@ int nsh_fir_mfma_prepare(nsh_fir_plan* p)
             }
     NSH_CK(hipMalloc(&p->frag_dev, frag.size() * sizeof(unsigned short)));
     NSH_CK(hipMemcpy(p->frag_dev, frag.data(), frag.size() * sizeof(unsigned short), hipMemcpyHostToDevice));
+
+    // v5: QH/2 k-steps of 32 for v_mfma_f32_16x16x32_bf16 (lane l holds B[k = 8(l >> 4) + j]
+    // [col = l & 15], k = 32 st + kk -> q = 2 st + (kk >> 4), r = kk & 15), then for odd QH a
+    // tail for v_mfma_f32_16x16x16_bf16 (q = QH - 1, lane l holds B[r = 4(l >> 4) + j][l & 15]).
+    // Tap index i - r + 16 q; each tap split into three bf16 terms (RNE).
+    p->QH = (p->L + 15 + 15) / 16;
+    if (p->QH <= 10) {
+        const int KS = p->QH / 2;
+        const bool tail = p->QH % 2;
+        std::vector<unsigned short> f16((size_t)3 * KS * 64 * 8 + (tail ? (size_t)3 * 64 * 4 : 0), 0);
+        auto put3 = [&](float hv, size_t i0, size_t i1, size_t i2) {
+            const unsigned short h1 = bf16_rne(hv);
+            const float r1 = hv - bf16_to_f(h1);
+            const unsigned short h2 = bf16_rne(r1);
+            const float r2 = r1 - bf16_to_f(h2);
+            f16[i0] = h1;
+            f16[i1] = h2;
+            f16[i2] = bf16_rne(r2);
+        };
+        auto tap = [&](int t) { return (t >= 0 && t < p->L) ? p->taps_host[t] : 0.f; };
+        for (int st = 0; st < KS; ++st)
+            for (int lane = 0; lane < 64; ++lane)
+                for (int j = 0; j < 8; ++j) {
+                    const int kk = 8 * (lane >> 4) + j;
+                    const float hv = tap((lane & 15) - (kk & 15) + 16 * (2 * st + (kk >> 4)));
+                    put3(hv, (((size_t)0 * KS + st) * 64 + lane) * 8 + j, (((size_t)1 * KS + st) * 64 + lane) * 8 + j,
+                         (((size_t)2 * KS + st) * 64 + lane) * 8 + j);
+                }
+        if (tail) {
+            const size_t t0 = (size_t)3 * KS * 64 * 8;
+            for (int lane = 0; lane < 64; ++lane)
+                for (int j = 0; j < 4; ++j) {
+                    const int r = 4 * (lane >> 4) + j;
+                    const float hv = tap((lane & 15) - r + 16 * (p->QH - 1));
+                    put3(hv, t0 + ((size_t)0 * 64 + lane) * 4 + j, t0 + ((size_t)1 * 64 + lane) * 4 + j,
+                         t0 + ((size_t)2 * 64 + lane) * 4 + j);
+                }
+        }
+        NSH_CK(hipMalloc(&p->frag16_dev, f16.size() * sizeof(unsigned short)));
+        NSH_CK(hipMemcpy(p->frag16_dev, f16.data(), f16.size() * sizeof(unsigned short), hipMemcpyHostToDevice));
+    }
     return 0;
+}
+
+bool nsh_fir_mfma16_supported(const nsh_fir_plan* p)
+{
+    if (p->D != 1) return false;
+    for (float t : p->taps_host)
+        if (!(t == t) || t - t != 0.f) return false;
+    return (p->L + 30) / 16 <= 10;
+}
+
+int nsh_fir_mfma16_run(const nsh_fir_plan* p, const float2* in, const float2* hist_in, float2* hist_out, float2* out,
+                       int64_t n_out, hipStream_t s)
+{
+    if (p->frag16_dev) {
+        switch (p->QH) {
+        case 1: return launch_qh<1>(p, in, hist_in, hist_out, out, n_out, s);
+        case 2: return launch_qh<2>(p, in, hist_in, hist_out, out, n_out, s);
+        case 3: return launch_qh<3>(p, in, hist_in, hist_out, out, n_out, s);
+        case 4: return launch_qh<4>(p, in, hist_in, hist_out, out, n_out, s);
+        case 5: return launch_qh<5>(p, in, hist_in, hist_out, out, n_out, s);
+        case 6: return launch_qh<6>(p, in, hist_in, hist_out, out, n_out, s);
+        case 7: return launch_qh<7>(p, in, hist_in, hist_out, out, n_out, s);
+        case 8: return launch_qh<8>(p, in, hist_in, hist_out, out, n_out, s);
+        case 9: return launch_qh<9>(p, in, hist_in, hist_out, out, n_out, s);
+        case 10: return launch_qh<10>(p, in, hist_in, hist_out, out, n_out, s);
+        default: break;
+        }
+    }
+    return nsh::fail_msg("nsh_fir_ccf(mfma16): unsupported tap count");
 }
 
 int nsh_fir_mfma_run(const nsh_fir_plan* p, const float2* in, const float2* hist_in, float2* hist_out, float2* out, int64_t n_out, hipStream_t s)
 {
+    if (p->variant >= 20) return nsh_fir_mfma16_run(p, in, hist_in, hist_out, out, n_out, s); // A/B tuning
     switch (p->Q) {
     case 1: return launch_q<1>(p, in, hist_in, hist_out, out, n_out, s);
     case 2: return launch_q<2>(p, in, hist_in, hist_out, out, n_out, s);

@@ -16,10 +16,17 @@ struct nsh_fir_plan {
     int Q = 0;
     int S = 0;
     void* frag_dev = nullptr;
+    // 16-phase form (v_mfma_f32_16x16x32_bf16): QH tap blocks of 16, (QH+1)/2 k-steps of
+    // 32; [part(3)][kstep][lane(64)][8] bf16.
+    int QH = 0;
+    void* frag16_dev = nullptr;
     int variant = 0;      // MFMA kernel tuning variant (0 = default)
 };
 
 bool nsh_fir_mfma_supported(const nsh_fir_plan* p);
+bool nsh_fir_mfma16_supported(const nsh_fir_plan* p);
 int nsh_fir_mfma_prepare(nsh_fir_plan* p);
 int nsh_fir_mfma_run(const nsh_fir_plan* p, const float2* in, const float2* hist_in, float2* hist_out,
                      float2* out, int64_t n_out, hipStream_t s);
+int nsh_fir_mfma16_run(const nsh_fir_plan* p, const float2* in, const float2* hist_in, float2* hist_out,
+                       float2* out, int64_t n_out, hipStream_t s);

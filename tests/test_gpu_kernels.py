@@ -114,7 +114,8 @@ def test_add_mul_cc_bit_exact(torch_cuda, n):
     np.testing.assert_array_equal(host(dy), orc.mul_cc(a, b))
 
 
-ALGOS = [("direct", nsh.FIR_DIRECT), ("mfma", nsh.FIR_MFMA)]
+ALGOS = [("direct", nsh.FIR_DIRECT), ("mfma", nsh.FIR_MFMA), ("mfma16", nsh.FIR_MFMA16)]
+MAX_TAPS = {"direct": 4096, "mfma": 161, "mfma16": 145}
 
 
 def run_fir(torch, plan, x, n_out, hist=None):
@@ -143,9 +144,11 @@ def test_fir127_golden(torch_cuda, golden, name, algo):
 
 
 @pytest.mark.parametrize("name,algo", ALGOS)
-@pytest.mark.parametrize("ntaps", [1, 2, 31, 32, 33, 64, 127, 128, 161])
+@pytest.mark.parametrize("ntaps", [1, 2, 16, 17, 31, 32, 33, 64, 127, 128, 145, 161])
 @pytest.mark.parametrize("n", [1, 100, 2047, 2048, 2049, 70001])
 def test_fir_vs_oracle_shapes(torch_cuda, name, algo, ntaps, n):
+    if ntaps > MAX_TAPS[name]:
+        pytest.skip(f"{name} supports ntaps <= {MAX_TAPS[name]}")
     torch = torch_cuda
     rng = np.random.default_rng(ntaps * 1000 + n)
     h = rng.standard_normal(ntaps).astype(np.float32) * 0.1
