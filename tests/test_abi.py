@@ -39,11 +39,12 @@ def test_hip_shim_loads_and_reports():
     assert L.nsh_last_error() == b""
 
 
-def test_hip_shim_is_gfx950_code_object():
+def test_hip_shim_is_gfx950_code_object(tmp_path):
     from newsched_amd import nsh
 
-    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", nsh.HIP_LIB],
-                         capture_output=True, text=True)
+    # --offloading extracts the bundled code objects into the working directory
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", os.path.abspath(nsh.HIP_LIB)],
+                         capture_output=True, text=True, cwd=tmp_path)
     if out.returncode != 0:
         pytest.skip("llvm-objdump --offloading unavailable")
     assert "gfx950" in out.stdout + out.stderr
