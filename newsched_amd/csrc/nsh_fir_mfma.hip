@@ -552,6 +552,205 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma2(const float2* __restrict__
     }
 }
 
+// ---- v6: ping-pong workgroup (two 4-wave groups, one wave of each per SIMD) ----------------
+// v2's two 256-thread workgroups per CU do identical work in lockstep, so both waves of a SIMD
+// split (VALU + ds_write) at the same time and the matrix pipe idles meanwhile: with no HBM
+// traffic at all the MFMA (~55 us) and LDS (~45 us) parts of a 2^25-sample launch simply add
+// up (ablation masks 14/15). Here one 512-thread workgroup per CU runs two groups in
+// alternating roles: in phase p group (p & 1) computes chunk p from LDS buffer p & 1 while the
+// other group copies that buffer's tail (the next halo) and splits chunk p + 1 into the other
+// buffer, then loads chunk p + 3 for its next split; one barrier per phase. Every SIMD always
+// hosts one computing wave, and the splitting wave fills the MFMA issue gaps.
+template <int Q>
+__device__ __forceinline__ void g_load_main(float4 (&v)[geom2<Q>::VPT], const float2* __restrict__ in,
+                                           const float2* __restrict__ hist, int64_t ch, int64_t n_in, int L,
+                                           bool in_aligned, int gt)
+{
+    using G = geom2<Q>;
+    const int64_t g0 = ch * G::CHUNK;
+#if NSH_FIR_ABLATE & 2
+    for (int u = 0; u < G::VPT; ++u) v[u] = make_float4((float)g0, (float)u, (float)gt, 1.f);
+    return;
+#endif
+    if (in_aligned && g0 + G::CHUNK <= n_in) {
+        const nf4* src = reinterpret_cast<const nf4*>(in + g0);
+#pragma unroll
+        for (int u = 0; u < G::VPT; ++u) {
+            const nf4 t = __builtin_nontemporal_load(src + gt + G::NT * u);
+            v[u] = make_float4(t.x, t.y, t.z, t.w);
+        }
+    } else {
+#pragma unroll
+        for (int u = 0; u < G::VPT; ++u) {
+            const int vi = gt + G::NT * u;
+            const float2 a = virt(in, hist, g0 + 2 * vi, n_in, L);
+            const float2 b = virt(in, hist, g0 + 2 * vi + 1, n_in, L);
+            v[u] = make_float4(a.x, a.y, b.x, b.y);
+        }
+    }
+}
+
+template <int Q>
+__device__ __forceinline__ void g_store_pair(unsigned char* buf, int s, float a_re, float b_re, float a_im, float b_im)
+{
+    using G = geom2<Q>;
+    const int off = (s >> 5) * 80 + (s & 31) * 2;
+    unsigned r1, r2, r3, i1, i2, i3;
+#if NSH_FIR_ABLATE & 4
+    r1 = r2 = r3 = __float_as_uint(a_re);
+    i1 = i2 = i3 = __float_as_uint(a_im);
+#else
+    split_pair(a_re, b_re, r1, r2, r3);
+    split_pair(a_im, b_im, i1, i2, i3);
+#endif
+    *reinterpret_cast<unsigned*>(buf + 0 * G::PLANE + off) = r1;
+    *reinterpret_cast<unsigned*>(buf + 1 * G::PLANE + off) = r2;
+    *reinterpret_cast<unsigned*>(buf + 2 * G::PLANE + off) = r3;
+    *reinterpret_cast<unsigned*>(buf + 3 * G::PLANE + off) = i1;
+    *reinterpret_cast<unsigned*>(buf + 4 * G::PLANE + off) = i2;
+    *reinterpret_cast<unsigned*>(buf + 5 * G::PLANE + off) = i3;
+}
+
+template <int Q>
+__device__ __forceinline__ void g_store_main(const float4 (&v)[geom2<Q>::VPT], unsigned char* buf, int gt)
+{
+    using G = geom2<Q>;
+#pragma unroll
+    for (int u = 0; u < G::VPT; ++u)
+        g_store_pair<Q>(buf, G::H + 2 * (gt + G::NT * u), v[u].x, v[u].z, v[u].y, v[u].w);
+}
+
+template <int Q>
+__device__ __forceinline__ void g_copy_halo(const unsigned char* cur, unsigned char* nxt, int gt)
+{
+    using G = geom2<Q>;
+    constexpr int PIECES = 6 * G::HR * 4;
+    if constexpr (PIECES > 0) {
+        for (int t = gt; t < PIECES; t += G::NT) {
+            const int plane = t / (G::HR * 4);
+            const int rem = t % (G::HR * 4);
+            const int row = rem >> 2, q16 = rem & 3;
+            const uint4 d = *reinterpret_cast<const uint4*>(cur + plane * G::PLANE + (G::NB - G::HR + row) * 80 + q16 * 16);
+            *reinterpret_cast<uint4*>(nxt + plane * G::PLANE + row * 80 + q16 * 16) = d;
+        }
+    }
+}
+
+template <int Q>
+__device__ __forceinline__ void g_load_store_halo(unsigned char* buf, const float2* __restrict__ in,
+                                                  const float2* __restrict__ hist, int64_t ch, int64_t n_in, int L, int gt)
+{
+    using G = geom2<Q>;
+    if constexpr (G::H > 0) {
+        const int64_t g0 = ch * G::CHUNK - G::H;
+        for (int p = gt; p < G::H / 2; p += G::NT) {
+            const float2 a = virt(in, hist, g0 + 2 * p, n_in, L);
+            const float2 b = virt(in, hist, g0 + 2 * p + 1, n_in, L);
+            g_store_pair<Q>(buf, 2 * p, a.x, b.x, a.y, b.y);
+        }
+    }
+}
+
+template <int Q>
+__global__ __launch_bounds__(512, 1) void k_fir_mfma6(const float2* __restrict__ in,
+                                                     const float2* __restrict__ hist_in,
+                                                     float2* __restrict__ hist_out,
+                                                     float2* __restrict__ out,
+                                                     const bf16x8* __restrict__ frag, // [3][S][64]
+                                                     int L,
+                                                     int64_t n_out,
+                                                     int in_aligned,
+                                                     int prio)
+{
+    using G = geom2<Q>;
+    constexpr int S = G::S;
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const int tid = threadIdx.x;
+    const int grp = tid >> 8;                    // wave-uniform: waves 0-3 / 4-7
+    const int gt = tid & 255;
+    const int lane = tid & 63;
+    const int gwave = (tid >> 6) & 3;
+    const int64_t n_in = n_out;
+
+    if (blockIdx.x == 0) {
+        for (int j = tid; j < L - 1; j += 512) hist_out[j] = virt(in, hist_in, n_in - (L - 1) + j, n_in, L);
+    }
+
+    bf16x8 B0[S], B1[S], B2[S];
+#pragma unroll
+    for (int st = 0; st < S; ++st) {
+        B0[st] = frag[(0 * S + st) * 64 + lane];
+        B1[st] = frag[(1 * S + st) * 64 + lane];
+        B2[st] = frag[(2 * S + st) * 64 + lane];
+    }
+
+    const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
+    const int64_t per = (nchunks + gridDim.x - 1) / gridDim.x;
+    const int64_t c_begin = (int64_t)blockIdx.x * per;
+    const int64_t c_end = c_begin + per < nchunks ? c_begin + per : nchunks;
+    if (c_begin >= c_end) return;
+    const int64_t n = c_end - c_begin; // chunks of this workgroup, offsets 0 .. n-1
+    const bool al = in_aligned != 0;
+    auto chunk = [&](int64_t k) { return c_begin + (k < n ? k : n - 1); };
+
+    const int rho = lane & 31;
+    const int b = rho & 15;
+    const int c = rho >> 4;
+    const int h = lane >> 5;
+    const int a_base = c * 3 * G::PLANE + ((Q - 1) + 16 * gwave + b) * 80 + 16 * h;
+    const int phase = lane & 31;
+
+    // Group g splits offsets g, g+2, ... and computes the same offsets one phase later.
+    // Registers `v` always hold this group's next chunk to split.
+    float4 v[G::VPT];
+    if (grp == 0) {
+        g_load_store_halo<Q>(lds, in, hist_in, chunk(0), n_in, L, gt);
+        g_load_main<Q>(v, in, hist_in, chunk(0), n_in, L, al, gt);
+        g_store_main<Q>(v, lds, gt);
+        g_load_main<Q>(v, in, hist_in, chunk(2), n_in, L, al, gt);
+    } else {
+        g_load_main<Q>(v, in, hist_in, chunk(1), n_in, L, al, gt);
+    }
+    __syncthreads();
+
+    for (int64_t p = 0; p < n; ++p) {
+        unsigned char* cur = lds + (p & 1) * G::BUF;
+        unsigned char* nxt = lds + ((p & 1) ^ 1) * G::BUF;
+        if (grp == (int)(p & 1)) {
+            if (prio) __builtin_amdgcn_s_setprio(1);
+            compute_tile<Q, 4, G::PLANE>(cur, B0, B1, B2, a_base, (c_begin + p) * G::CHUNK + (int64_t)gwave * TILE, h,
+                                         phase, n_out, out);
+            if (prio) __builtin_amdgcn_s_setprio(0);
+        } else if (p + 1 < n) {
+            g_copy_halo<Q>(cur, nxt, gt);
+            g_store_main<Q>(v, nxt, gt);
+            g_load_main<Q>(v, in, hist_in, chunk(p + 3), n_in, L, al, gt);
+        }
+        __syncthreads();
+    }
+}
+
+template <int Q>
+int launch_v6(const nsh_fir_plan* p, const float2* in, const float2* hin, float2* hout, float2* out, int64_t n_out,
+              hipStream_t s, int prio)
+{
+    using G = geom2<Q>;
+    static bool attr_set = false;
+    if (!attr_set) {
+        NSH_CK(hipFuncSetAttribute((const void*)k_fir_mfma6<Q>, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
+        attr_set = true;
+    }
+    const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
+    int n_cu = 256;
+    (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, p->dev);
+    const unsigned grid = (unsigned)(nchunks < n_cu ? nchunks : n_cu);
+    const int aligned = ((uintptr_t)in % 16 == 0) ? 1 : 0;
+    hipLaunchKernelGGL(k_fir_mfma6<Q>, dim3(grid), dim3(512), G::LDS, s, in, hin, hout, out,
+                       (const bf16x8*)p->frag_dev, p->L, n_out, aligned, prio);
+    NSH_CK_LAUNCH("nsh_fir_ccf(mfma6)");
+    return 0;
+}
+
 // ---- v5: 16-phase blocks on v_mfma_f32_16x16x32_bf16 -------------------------------------
 // Same Toeplitz GEMM with 16-sample blocks: y[16b + i] = sum_q sum_{r<16} h[i - r + 16q] x[16(b-q) + r],
 // q < QH = ceil((L + 15) / 16) (9 for L = 127), K = 16 QH padded to the 32 of one k-step.
@@ -940,6 +1139,8 @@ int launch_q(const nsh_fir_plan* p, const float2* in, const float2* hin, float2*
     case 5: return launch_v<Q, 8, 2>(p, in, hin, hout, out, n_out, s, 1);
     case 6: return launch_v2<Q, 1>(p, in, hin, hout, out, n_out, s, 2);
     case 7: return launch_v2<Q, 2>(p, in, hin, hout, out, n_out, s, 2);
+    case 8: return launch_v6<Q>(p, in, hin, hout, out, n_out, s, 0);
+    case 9: return launch_v6<Q>(p, in, hin, hout, out, n_out, s, 1);
     default: return launch_v2<Q, 2>(p, in, hin, hout, out, n_out, s, 2);
     }
 }
