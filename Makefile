@@ -21,11 +21,14 @@ RT_OBJ   := $(patsubst newsched_amd/%.cpp,$(OBJDIR)/rt/%.o,$(RT_SRC))
 RT_HDR   := $(shell find newsched_amd/runtime/include newsched_amd/schedulers/include newsched_amd/blocklib/include -name '*.hpp' 2>/dev/null)
 TEST_SRC := $(wildcard tests/cpp/*.cpp)
 TEST_BIN := $(patsubst tests/cpp/%.cpp,build/tests/%,$(TEST_SRC))
+TOOL_SRC := $(wildcard tools/*.cpp)
+TOOL_BIN := $(patsubst tools/%.cpp,build/tools/%,$(TOOL_SRC))
 
-all: hip runtime tests oracle
+all: hip runtime tests tools oracle
 hip: $(LIBDIR)/libnsh_hip.so
 runtime: $(LIBDIR)/libnewsched.so
 tests: $(TEST_BIN)
+tools: $(TOOL_BIN)
 oracle:
 	$(MAKE) -C oracle
 
@@ -44,12 +47,16 @@ $(OBJDIR)/rt/%.o: newsched_amd/%.cpp $(RT_HDR) include/nsh_hip.h
 $(LIBDIR)/libnewsched.so: $(RT_OBJ) $(LIBDIR)/libnsh_hip.so
 	$(CXX) -shared -fPIC -pthread -o $@ $(RT_OBJ) -L$(LIBDIR) -lnsh_hip -Wl,-rpath,'$$ORIGIN'
 
-build/tests/%: tests/cpp/%.cpp $(LIBDIR)/libnewsched.so tests/cpp/qa.hpp
+build/tests/%: tests/cpp/%.cpp $(LIBDIR)/libnewsched.so $(wildcard tests/cpp/*.hpp)
 	@mkdir -p build/tests
 	$(CXX) $(CXXFLAGS) -Itests/cpp -o $@ $< -L$(LIBDIR) -lnewsched -lnsh_hip -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)'
+
+build/tools/%: tools/%.cpp $(LIBDIR)/libnewsched.so
+	@mkdir -p build/tools
+	$(CXX) $(CXXFLAGS) -o $@ $< -L$(LIBDIR) -lnewsched -lnsh_hip -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)'
 
 clean:
 	rm -rf build $(LIBDIR)
 	$(MAKE) -C oracle clean
 
-.PHONY: all hip runtime tests oracle clean
+.PHONY: all hip runtime tests tools oracle clean

@@ -170,13 +170,25 @@ __device__ __forceinline__ void compute_tile(const unsigned char* lds,
     constexpr int S_ = 2 * Q;
     f32x16 acc_hi = {};
     f32x16 acc_lo = {};
+#if NSH_FIR_ABLATE & 128 // timing only: A fragments read for q = 0 and reused for every q
+    bf16x8 Ar[2][3];
+#endif
 #pragma unroll
     for (int st = 0; st < S_; ++st) {
         const int q = st >> 1;
         const int off = a_base - q * 80 + 32 * (st & 1);
+#if NSH_FIR_ABLATE & 128
+        if (q == 0) {
+            Ar[st & 1][0] = *reinterpret_cast<const bf16x8*>(lds + off);
+            Ar[st & 1][1] = *reinterpret_cast<const bf16x8*>(lds + off + PLANE_);
+            Ar[st & 1][2] = *reinterpret_cast<const bf16x8*>(lds + off + 2 * PLANE_);
+        }
+        const bf16x8 A0 = Ar[st & 1][0], A1 = Ar[st & 1][1], A2 = Ar[st & 1][2];
+#else
         const bf16x8 A0 = *reinterpret_cast<const bf16x8*>(lds + off);
         const bf16x8 A1 = *reinterpret_cast<const bf16x8*>(lds + off + PLANE_);
         const bf16x8 A2 = *reinterpret_cast<const bf16x8*>(lds + off + 2 * PLANE_);
+#endif
 #if NSH_FIR_ABLATE & 1
         acc_hi[st & 15] += (float)A0[0] + (float)A1[1] + (float)A2[2] + (float)B0[st][0] + (float)B1[st][1] + (float)B2[st][2];
         continue;

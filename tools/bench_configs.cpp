@@ -1,0 +1,316 @@
+// Secondary BASELINE configs (BASELINE.json configs[0,1,3,4]; configs[2] = C3 is bench.py),
+// measured through the same runtime as the headline: flowgraphs in one scheduler_hip domain
+// with an HBM-resident input ring (nop_source -> nop_head(n) -> [2n-item hip_buffer,
+// preloaded with the counter-based stream] -> blocks -> null_sink), wall time of whole
+// fg->run() calls (median of K after one warm-up), tail parity against an in-tool CPU
+// reference, and the CPU scheduler_mt path of the same config where the CPU blocks exist.
+//   build/tools/bench_configs [log2n=28] [steps=5]     -> one JSON line per config
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <complex>
+#include <cstdio>
+#include <cstdlib>
+#include <gnuradio/blocklib/blocks/copy.hpp>
+#include <gnuradio/blocklib/blocks/fir_filter_ccf.hpp>
+#include <gnuradio/blocklib/blocks/head.hpp>
+#include <gnuradio/blocklib/blocks/multiply_const.hpp>
+#include <gnuradio/blocklib/blocks/nop.hpp>
+#include <gnuradio/blocklib/blocks/null_sink.hpp>
+#include <gnuradio/blocklib/blocks/null_source.hpp>
+#include <gnuradio/blocklib/blocks/vector_source.hpp>
+#include <gnuradio/blocklib/hip/fft.hpp>
+#include <gnuradio/blocklib/hip/fir_filter_ccf.hpp>
+#include <gnuradio/blocklib/hip/multiply_const.hpp>
+#include <gnuradio/flowgraph.hpp>
+#include <gnuradio/hip_buffer.hpp>
+#include <gnuradio/hip_context.hpp>
+#include <gnuradio/schedulers/hip/scheduler_hip.hpp>
+#include <gnuradio/schedulers/mt/scheduler_mt.hpp>
+#include <gnuradio/vmcircbuf.hpp>
+#include <string>
+#include <vector>
+
+#include "nsh_hip.h"
+
+using namespace gr;
+using clk = std::chrono::steady_clock;
+
+static uint64_t splitmix64(uint64_t x)
+{
+    x += 0x9E3779B97F4A7C15ull;
+    uint64_t z = x;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+static std::vector<gr_complex> synth(size_t n, uint64_t first = 0, uint64_t seed = 0x6E736368)
+{
+    std::vector<gr_complex> v(n);
+    for (size_t i = 0; i < n; ++i) {
+        const uint64_t g = 2 * (first + i);
+        v[i] = gr_complex((float)(int)(splitmix64(seed ^ g) >> 40) * (1.0f / 8388608.0f) - 1.0f,
+                          (float)(int)(splitmix64(seed ^ (g + 1)) >> 40) * (1.0f / 8388608.0f) - 1.0f);
+    }
+    return v;
+}
+static gr_complex cmul(gr_complex a, gr_complex k)
+{
+    volatile float p0 = a.real() * k.real(), p1 = a.imag() * k.imag(), p2 = a.real() * k.imag(), p3 = a.imag() * k.real();
+    return gr_complex(p0 - p1, p2 + p3);
+}
+static std::vector<float> lowpass(int L, double fc) // firwin(L, 2 fc) with a Hamming window, unit DC gain
+{
+    std::vector<float> h(L);
+    double s = 0;
+    for (int k = 0; k < L; ++k) {
+        const double t = k - (L - 1) / 2.0;
+        const double sinc = t == 0 ? 2 * fc : std::sin(2 * M_PI * fc * t) / (M_PI * t);
+        h[k] = (float)(sinc * (0.54 - 0.46 * std::cos(2 * M_PI * k / (L - 1))));
+        s += h[k];
+    }
+    for (auto& v : h) v = (float)(v / s);
+    return h;
+}
+static std::vector<gr_complex> fir_ref(const std::vector<gr_complex>& x, const std::vector<float>& h, int D)
+{
+    std::vector<gr_complex> y(x.size() / D);
+    for (size_t m = 0; m < y.size(); ++m) {
+        std::complex<double> acc = 0;
+        for (size_t k = 0; k < h.size(); ++k) {
+            const long g = (long)(m * D) - (long)k;
+            if (g >= 0) acc += (double)h[k] * std::complex<double>(x[g]);
+        }
+        y[m] = gr_complex(acc);
+    }
+    return y;
+}
+static double rel_err(const std::vector<gr_complex>& y, const std::vector<gr_complex>& r, size_t skip = 0)
+{
+    double e = 0, s = 0;
+    for (size_t i = skip; i < y.size(); ++i) {
+        e = std::max(e, (double)std::abs(y[i] - r[i]));
+        s = std::max(s, (double)std::abs(r[i]));
+    }
+    return s > 0 ? e / s : e;
+}
+static double median(std::vector<double> v)
+{
+    std::sort(v.begin(), v.end());
+    return v[v.size() / 2];
+}
+
+// GPU flowgraph with a resident input ring in front of `first` and a hip_buffer in front of
+// the null_sink after `last`.
+struct gpu_fg {
+    flowgraph::sptr fg;
+    schedulers::scheduler_hip::sptr sched;
+    block_sptr snk;
+    int64_t n_items;
+    size_t isz;
+    int dev = 0;
+
+    gpu_fg(std::vector<block_sptr> chain, int64_t n_items_, size_t isz_, size_t out_buf_bytes)
+        : n_items(n_items_), isz(isz_)
+    {
+        auto src = blocks::nop_source::make(isz);
+        auto head = blocks::nop_head::make(isz, (size_t)n_items);
+        snk = blocks::null_sink::make(isz);
+        fg = flowgraph::make();
+        fg->connect(src, 0, head, 0)->set_custom_buffer(VMCIRC_BUFFER_ARGS);
+        const int64_t cap = 2 * n_items;
+        const int d = dev;
+        fg->connect(head, 0, chain[0], 0)
+            ->set_custom_buffer(
+                [cap, d](size_t, size_t item, std::shared_ptr<buffer_properties>) -> buffer_sptr {
+                    return std::make_shared<hip_buffer>((size_t)cap, item, hip_buffer_type::D2D, d);
+                },
+                hip_buffer_properties::make(hip_buffer_type::D2D, d));
+        for (size_t i = 1; i < chain.size(); ++i) fg->connect(chain[i - 1], 0, chain[i], 0);
+        fg->connect(chain.back(), 0, snk, 0);
+        sched = schedulers::scheduler_hip::make("hip", dev, out_buf_bytes);
+        fg->set_scheduler(sched);
+        fg->validate();
+        auto ring = std::dynamic_pointer_cast<hip_buffer>(sched->buffers()->get_input_buffer(chain[0]->input_stream_ports()[0]));
+        void* s = nullptr;
+        hip::check(nsh_stream_create(dev, &s), "stream");
+        const int64_t n_samples = n_items * (int64_t)(isz / sizeof(gr_complex));
+        char* base = (char*)ring->device_base();
+        hip::check(nsh_synth_cf32((float*)base, n_samples, 0, 0x6E736368, s), "preload");
+        hip::check(nsh_synth_cf32((float*)(base + n_items * isz), n_samples, 0, 0x6E736368, s), "preload");
+        hip::check(nsh_stream_sync(s), "preload");
+        nsh_stream_destroy(s);
+    }
+    double run(int steps)
+    {
+        fg->run(); // warm-up
+        std::vector<double> t;
+        for (int i = 0; i < steps; ++i) {
+            const auto t0 = clk::now();
+            fg->run();
+            t.push_back(std::chrono::duration<double>(clk::now() - t0).count());
+        }
+        return median(t);
+    }
+    // last `count` samples written into the sink's input ring
+    std::vector<gr_complex> tail(int64_t count)
+    {
+        auto r = std::dynamic_pointer_cast<hip_buffer>(sched->buffers()->get_input_buffer(snk->input_stream_ports()[0]));
+        const size_t per = isz / sizeof(gr_complex);
+        const uint64_t end = r->total_written() * per;
+        const uint64_t cap = r->capacity() * per;
+        std::vector<gr_complex> out((size_t)count);
+        const uint64_t start = end - (uint64_t)count;
+        const char* src = (const char*)r->device_base() + (start % cap) * sizeof(gr_complex);
+        void* s = nullptr;
+        hip::check(nsh_stream_create(dev, &s), "stream");
+        hip::check(nsh_memcpy_async(out.data(), src, (size_t)count * sizeof(gr_complex), NSH_D2H, s), "tail");
+        hip::check(nsh_stream_sync(s), "tail");
+        nsh_stream_destroy(s);
+        return out;
+    }
+};
+
+// CPU scheduler_mt path: vector_source(repeat) -> head(n) -> chain -> null_sink
+static double cpu_run(std::vector<block_sptr> chain, int64_t n, size_t fixed = 32768)
+{
+    auto src = blocks::vector_source_c::make(synth(1 << 16), true);
+    auto head = blocks::head::make(sizeof(gr_complex), (size_t)n);
+    auto snk = blocks::null_sink::make(sizeof(gr_complex));
+    auto fg = flowgraph::make();
+    fg->connect(src, 0, head, 0);
+    fg->connect(head, 0, chain[0], 0);
+    for (size_t i = 1; i < chain.size(); ++i) fg->connect(chain[i - 1], 0, chain[i], 0);
+    fg->connect(chain.back(), 0, snk, 0);
+    fg->set_scheduler(schedulers::scheduler_mt::make("mt", (unsigned)fixed));
+    fg->validate();
+    const auto t0 = clk::now();
+    fg->run();
+    return std::chrono::duration<double>(clk::now() - t0).count();
+}
+
+static void emit(const std::string& s) { std::printf("%s\n", s.c_str()), std::fflush(stdout); }
+static std::string num(double v, int prec = 1)
+{
+    char b[64];
+    std::snprintf(b, sizeof b, "%.*f", prec, v);
+    return b;
+}
+
+int main(int argc, char** argv)
+{
+    const int log2n = argc > 1 ? std::atoi(argv[1]) : 28;
+    const int steps = argc > 2 ? std::atoi(argv[2]) : 5;
+    const int64_t n = 1ll << log2n;
+    const double hbm = 8000.0; // GB/s spec
+    const std::vector<gr_complex> ks = { std::polar(1.0f, 0.1f), std::polar(1.0f, 0.2f), std::polar(1.0f, 0.3f),
+                                         std::polar(1.0f, 0.4f) };
+
+    // ---- C1: null_source -> head(2^20) -> copy -> null_sink, CPU only ----------------------
+    {
+        std::vector<double> t;
+        for (int r = 0; r < 7; ++r) {
+            auto src = blocks::null_source::make(sizeof(gr_complex));
+            auto head = blocks::head::make(sizeof(gr_complex), 1u << 20);
+            auto cp = blocks::copy::make(sizeof(gr_complex));
+            auto snk = blocks::null_sink::make(sizeof(gr_complex));
+            auto fg = flowgraph::make();
+            fg->connect(src, 0, head, 0);
+            fg->connect(head, 0, cp, 0);
+            fg->connect(cp, 0, snk, 0);
+            fg->set_scheduler(schedulers::scheduler_mt::make("mt", 32768));
+            fg->validate();
+            const auto t0 = clk::now();
+            fg->run();
+            t.push_back(std::chrono::duration<double>(clk::now() - t0).count());
+        }
+        const double s = median(t);
+        emit("{\"config\": \"C1\", \"workload\": \"null_source->head(2^20)->copy->null_sink, scheduler_mt 4 threads, 32 KiB buffers\", "
+             "\"value\": " + num((1 << 20) / s / 1e6, 2) + ", \"unit\": \"MSamples/s\", \"median_of\": 7, "
+             "\"note\": \"drain-based termination; the reference adds a fixed 100 ms sleep per run (flowgraph_monitor.cpp:27)\"}");
+    }
+
+    // ---- C2: 4 x multiply_const_cc ----------------------------------------------------------
+    for (int fused = 1; fused >= 0; --fused) {
+        std::vector<block_sptr> chain;
+        if (fused)
+            chain.push_back(hip::multiply_const_chain_cc::make(ks));
+        else
+            for (auto k : ks) chain.push_back(hip::multiply_const_cc::make(k));
+        gpu_fg g(chain, n, sizeof(gr_complex), (size_t)n * sizeof(gr_complex));
+        const double s = g.run(steps);
+        auto y = g.tail(4096);
+        auto x = synth(4096, n - 4096);
+        for (auto& v : x)
+            for (auto k : ks) v = cmul(v, k);
+        const bool exact = y == x;
+        const double gbs = (fused ? 16.0 : 64.0) * n / s / 1e9;
+        std::string line = "{\"config\": \"C2\", \"variant\": \"" + std::string(fused ? "fused multiply_const_chain_cc" : "4 blocks, every edge in HBM") +
+                           "\", \"value\": " + num(n / s / 1e6) + ", \"unit\": \"MSamples/s\", \"ms_per_run\": " + num(s * 1e3, 3) +
+                           ", \"hbm_bytes_per_sample\": " + (fused ? "16" : "64") + ", \"achieved_GBs\": " + num(gbs) +
+                           ", \"hbm_frac\": " + num(gbs / hbm, 4) + ", \"parity_tail_bitexact\": " + (exact ? "true" : "false");
+        if (fused) {
+            const int64_t nc = 1 << 25;
+            std::vector<block_sptr> cc;
+            for (auto k : ks) cc.push_back(blocks::multiply_const_cc::make(k));
+            const double cs = cpu_run(cc, nc);
+            line += ", \"cpu_baseline\": {\"value\": " + num(nc / cs / 1e6, 2) +
+                    ", \"unit\": \"MSamples/s\", \"sample\": \"2^25 samples, vector_source->head->4x blocks::multiply_const_cc->null_sink, scheduler_mt thread per block\"}";
+        }
+        emit(line + "}");
+    }
+
+    // ---- C4: fft1024 -> x W -> ifft1024, fused channelizer ----------------------------------
+    {
+        std::vector<gr_complex> w(1024);
+        for (int b = 0; b < 1024; ++b) w[b] = gr_complex((float)((1.0 + 0.5 * std::cos(2 * M_PI * b / 1024.0)) / 1024.0), 0.f);
+        const int64_t frames = n / 1024;
+        gpu_fg g({ hip::channelizer_vcc::make(w) }, frames, 1024 * sizeof(gr_complex), (size_t)n * sizeof(gr_complex));
+        const double s = g.run(steps);
+        // parity: the last frame, direct DFT in double
+        auto y = g.tail(1024);
+        auto x = synth(1024, n - 1024);
+        std::vector<std::complex<double>> X(1024), Z(1024);
+        for (int k = 0; k < 1024; ++k) {
+            std::complex<double> acc = 0;
+            for (int t = 0; t < 1024; ++t) acc += std::complex<double>(x[t]) * std::polar(1.0, -2 * M_PI * k * t / 1024.0);
+            X[k] = acc * std::complex<double>(w[k]);
+        }
+        std::vector<gr_complex> r(1024);
+        for (int t = 0; t < 1024; ++t) {
+            std::complex<double> acc = 0;
+            for (int k = 0; k < 1024; ++k) acc += X[k] * std::polar(1.0, 2 * M_PI * k * t / 1024.0);
+            r[t] = gr_complex(acc);
+        }
+        const double gbs = 16.0 * n / s / 1e9;
+        emit("{\"config\": \"C4\", \"variant\": \"fused channelizer_vcc (fft1024 * W ifft1024 in LDS)\", \"value\": " + num(n / s / 1e6) +
+             ", \"unit\": \"MSamples/s\", \"ms_per_run\": " + num(s * 1e3, 3) + ", \"hbm_bytes_per_sample\": 16, \"achieved_GBs\": " +
+             num(gbs) + ", \"hbm_frac\": " + num(gbs / hbm, 4) + ", \"parity_last_frame_rel_err\": " + num(rel_err(y, r), 9) + "}");
+    }
+
+    // ---- C5 at G = 1: 4 x (127-tap, D = 2) ----------------------------------------------------
+    {
+        const auto h = lowpass(127, 0.225); // firwin(127, 0.45)
+        std::vector<block_sptr> chain;
+        for (int i = 0; i < 4; ++i) chain.push_back(hip::fir_filter_ccf::make(h, 2));
+        gpu_fg g(chain, n, sizeof(gr_complex), (size_t)n * sizeof(gr_complex) / 2);
+        const double s = g.run(steps);
+        // parity: last 4096 outputs from the last 4096*16 + 4 stage halos of input
+        const int64_t m = 4096, win = m * 16 + 2048;
+        auto x = synth(win, n - win);
+        for (int i = 0; i < 4; ++i) x = fir_ref(x, h, 2);
+        std::vector<gr_complex> r(x.end() - m, x.end());
+        auto y = g.tail(m);
+        const double gbs = 8.5 * n / s / 1e9;
+        const int64_t nc = 1 << 24;
+        std::vector<block_sptr> cc;
+        for (int i = 0; i < 4; ++i) cc.push_back(blocks::fir_filter_ccf::make(h, 2));
+        const double cs = cpu_run(cc, nc);
+        emit("{\"config\": \"C5\", \"variant\": \"G=1: 4 x fir_filter_ccf(127 taps, decim 2) in one scheduler_hip domain\", \"value\": " +
+             num(n / s / 1e6) + ", \"unit\": \"MSamples/s (input)\", \"ms_per_run\": " + num(s * 1e3, 3) +
+             ", \"hbm_bytes_per_input_sample\": 8.5, \"achieved_GBs\": " + num(gbs) + ", \"hbm_frac\": " + num(gbs / hbm, 4) +
+             ", \"parity_tail_rel_err\": " + num(rel_err(y, r), 9) + ", \"cpu_baseline\": {\"value\": " + num(nc / cs / 1e6, 2) +
+             ", \"unit\": \"MSamples/s (input)\", \"sample\": \"2^24 samples, vector_source->head->4x blocks::fir_filter_ccf(decim 2)->null_sink, scheduler_mt thread per block\"}}");
+    }
+    return 0;
+}
