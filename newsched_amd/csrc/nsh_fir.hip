@@ -176,7 +176,8 @@ int nsh_fir_plan_create(int dev, const float* taps_host, int ntaps, int decim, i
         if (resolved == NSH_FIR_MFMA && !nsh_fir_mfma_supported(p)) {
             (void)hipFree(p->taps_dev);
             delete p;
-            return nsh::fail_msg("nsh_fir_plan_create: MFMA form needs decim 1, finite taps and ntaps <= 161");
+            return nsh::fail_msg("nsh_fir_plan_create: MFMA form needs finite taps and decim 1 with ntaps <= 161, "
+                                 "decim 2 with ntaps <= 160 or decim 4 with ntaps <= 320");
         }
         const int rc = nsh_fir_mfma_prepare(p);
         if (rc) {
@@ -197,6 +198,7 @@ int nsh_fir_plan_destroy(void* plan)
     if (p->taps_dev) (void)hipFree(p->taps_dev);
     if (p->frag_dev) (void)hipFree(p->frag_dev);
     if (p->frag16_dev) (void)hipFree(p->frag16_dev);
+    if (p->fragd_dev) (void)hipFree(p->fragd_dev);
     delete p;
     return 0;
 }

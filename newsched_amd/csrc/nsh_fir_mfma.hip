@@ -927,6 +927,16 @@ __device__ __forceinline__ void v5_compute(const unsigned char* lds, const bf16x
             lo[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A2, B0[st], lo[t], 0, 0, 0);
         }
     }
+    // The K tail accumulates into its own registers: an accumulator handed directly from a
+    // 16x16x32 MFMA to a dependent 16x16x16 one is read before its upper rows are written
+    // when nothing is scheduled in between (measured: regs 2-3 stale, ~1e-6 errors), so the
+    // two opcodes never share an accumulation chain.
+    f32x4 hi_t[G::TILES], lo_t[G::TILES];
+#pragma unroll
+    for (int t = 0; t < G::TILES; ++t) {
+        hi_t[t] = f32x4{ 0.f, 0.f, 0.f, 0.f };
+        lo_t[t] = f32x4{ 0.f, 0.f, 0.f, 0.f };
+    }
     if constexpr (G::TAIL) {
         // q = QH - 1 alone: v_mfma_f32_16x16x16_bf16, lane l holds A[l & 15][k = 4(l >> 4) + j]
 #pragma unroll
@@ -939,12 +949,12 @@ __device__ __forceinline__ void v5_compute(const unsigned char* lds, const bf16x
             hi[t][1] += (float)A0[0] + (float)A1[1] + (float)A2[2] + (float)T[0][0] + (float)T[1][1] + (float)T[2][2];
             continue;
 #endif
-            hi[t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(A0, T[0], hi[t], 0, 0, 0);
-            lo[t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(A0, T[1], lo[t], 0, 0, 0);
-            lo[t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(A1, T[0], lo[t], 0, 0, 0);
-            lo[t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(A0, T[2], lo[t], 0, 0, 0);
-            lo[t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(A1, T[1], lo[t], 0, 0, 0);
-            lo[t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(A2, T[0], lo[t], 0, 0, 0);
+            hi_t[t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(A0, T[0], hi_t[t], 0, 0, 0);
+            lo_t[t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(A0, T[1], lo_t[t], 0, 0, 0);
+            lo_t[t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(A1, T[0], lo_t[t], 0, 0, 0);
+            lo_t[t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(A0, T[2], lo_t[t], 0, 0, 0);
+            lo_t[t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(A1, T[1], lo_t[t], 0, 0, 0);
+            lo_t[t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(A2, T[0], lo_t[t], 0, 0, 0);
         }
     }
 #pragma unroll
@@ -953,8 +963,8 @@ __device__ __forceinline__ void v5_compute(const unsigned char* lds, const bf16x
         for (int half = 0; half < 2; ++half) {
             const int blk = t * 8 + 2 * g + half;
             const int64_t n = n_tile + (int64_t)wave * TILE + blk * 16 + phase;
-            const float re = hi[t][2 * half] + lo[t][2 * half];
-            const float im = hi[t][2 * half + 1] + lo[t][2 * half + 1];
+            const float re = (hi[t][2 * half] + hi_t[t][2 * half]) + (lo[t][2 * half] + lo_t[t][2 * half]);
+            const float im = (hi[t][2 * half + 1] + hi_t[t][2 * half + 1]) + (lo[t][2 * half + 1] + lo_t[t][2 * half + 1]);
 #if NSH_FIR_ABLATE & 8
             if (re == 1.2345e-30f && n < n_out) {
 #else
@@ -1079,6 +1089,332 @@ int launch_qh(const nsh_fir_plan* p, const float2* in, const float2* hin, float2
     }
 }
 
+// ---- v7: decimating FIR (D = 2, 4) as a polyphase Toeplitz GEMM -------------------------------
+// y[m] = sum_k h[k] x[D m - k]; with k = D j + r and the phase streams
+//     z_0[i] = x[D i],   z_r[i] = x[D i + D - r]  (r >= 1),
+//     h'_0[j] = h[D j],  h'_r[j] = h[D (j - 1) + r]  (j >= 1; h'_r[0] = 0),
+// y[m] = sum_r sum_j h'_r[j] z_r[m - j]: D ordinary FIRs at the output rate on the
+// deinterleaved input, summed in the same accumulators. Each phase is laid out and
+// multiplied exactly as the 16-sample form above (v5). A chunk = 2048 input samples =
+// 2048/D outputs; a thread's 2D consecutive samples give one aligned bf16 pair per phase, so
+// the split still writes packed 32-bit words. Per output the matrix work is about the
+// decim-1 form's (K = 16 QH per phase, QH = ceil((ceil(L/D) + 16) / 16)), per input sample 1/D.
+template <int D, int QH>
+struct geom7 {
+    static constexpr int NT = 256;
+    static constexpr int CHUNK_IN = 2048;
+    static constexpr int CHUNK = CHUNK_IN / D;                 // outputs per chunk
+    static constexpr int TILES = 4 / D;                        // row-tiles (8 blocks of 16) per wave
+    static constexpr int WAVE_OUT = TILES * 128;
+    static constexpr int KS = QH / 2;
+    static constexpr int TAIL = QH % 2;
+    static constexpr int H = 16 * (QH - 1);                    // halo samples per phase
+    static constexpr int HR = QH - 1;
+    static constexpr int NB = (CHUNK + H) / 16;                // rows per phase
+    static constexpr int PLANE = NB * 32;
+    static constexpr int IM_OFF = (3 * PLANE + 255) / 256 * 256 + 128;
+    static constexpr int PH = (IM_OFF + 3 * PLANE + 255) / 256 * 256; // one phase's planes
+    static constexpr int BUF = D * PH;
+    static constexpr int LDS = 2 * BUF;
+    static constexpr int VPT = CHUNK_IN / 2 / NT;              // 4 float4 per thread
+    static constexpr int UNITS = VPT * 2 / (2 * D);            // groups of 2D samples per thread
+    static_assert(D == 2 || D == 4, "D");
+    static_assert(VPT == 4, "register arrays below are declared [4]");
+};
+
+template <int D, int QH>
+__device__ __forceinline__ void v7_store_pair(unsigned char* buf, int r, int s, float a_re, float b_re, float a_im,
+                                              float b_im)
+{
+    using G = geom7<D, QH>;
+    unsigned char* ph = buf + r * G::PH;
+    const int off = (s >> 4) * 32 + (s & 15) * 2;
+    unsigned r1, r2, r3, i1, i2, i3;
+    split_pair(a_re, b_re, r1, r2, r3);
+    split_pair(a_im, b_im, i1, i2, i3);
+    *reinterpret_cast<unsigned*>(ph + 0 * G::PLANE + off) = r1;
+    *reinterpret_cast<unsigned*>(ph + 1 * G::PLANE + off) = r2;
+    *reinterpret_cast<unsigned*>(ph + 2 * G::PLANE + off) = r3;
+    *reinterpret_cast<unsigned*>(ph + G::IM_OFF + 0 * G::PLANE + off) = i1;
+    *reinterpret_cast<unsigned*>(ph + G::IM_OFF + 1 * G::PLANE + off) = i2;
+    *reinterpret_cast<unsigned*>(ph + G::IM_OFF + 2 * G::PLANE + off) = i3;
+}
+
+// Registers: thread t holds input samples [2D (t + 256 u'), 2D (t + 256 u') + 2D) of the
+// chunk, u' < UNITS, as D float4 each (2 samples per float4).
+template <int D, int QH>
+__device__ __forceinline__ void v7_load_main(float4 (&v)[4], const float2* __restrict__ in,
+                                             const float2* __restrict__ hist, int64_t ch, int64_t n_in, int L,
+                                             bool in_aligned)
+{
+    using G = geom7<D, QH>;
+    const int64_t g0 = ch * G::CHUNK_IN;
+    if (in_aligned && g0 + G::CHUNK_IN <= n_in) {
+        const nf4* src = reinterpret_cast<const nf4*>(in + g0);
+#pragma unroll
+        for (int u = 0; u < G::UNITS; ++u)
+#pragma unroll
+            for (int f = 0; f < D; ++f) {
+                const nf4 t = __builtin_nontemporal_load(src + (threadIdx.x + G::NT * u) * D + f);
+                v[u * D + f] = make_float4(t.x, t.y, t.z, t.w);
+            }
+    } else {
+#pragma unroll
+        for (int u = 0; u < G::UNITS; ++u)
+#pragma unroll
+            for (int f = 0; f < D; ++f) {
+                const int64_t l = (int64_t)((threadIdx.x + G::NT * u) * D + f) * 2;
+                const float2 a = virt(in, hist, g0 + l, n_in, L);
+                const float2 b = virt(in, hist, g0 + l + 1, n_in, L);
+                v[u * D + f] = make_float4(a.x, a.y, b.x, b.y);
+            }
+    }
+}
+
+__device__ __forceinline__ float2 f4_sample(const float4& v, int which)
+{
+    return which ? make_float2(v.z, v.w) : make_float2(v.x, v.y);
+}
+
+// Split + deinterleave into the phase planes (rows HR.. of each phase).
+template <int D, int QH>
+__device__ __forceinline__ void v7_store_main(const float4 (&v)[4], unsigned char* buf)
+{
+    using G = geom7<D, QH>;
+#pragma unroll
+    for (int u = 0; u < G::UNITS; ++u) {
+        const int i0 = 2 * (threadIdx.x + G::NT * u); // phase-stream index of this unit's first pair
+#pragma unroll
+        for (int r = 0; r < D; ++r) {
+            // z_r[i] = x[D i + s_r]: local samples D i0 + s_r and D (i0 + 1) + s_r
+            const int sr = r == 0 ? 0 : D - r;
+            const int la = sr, lb = D + sr; // within the unit's 2D samples
+            const float2 a = f4_sample(v[u * D + la / 2], la & 1);
+            const float2 b = f4_sample(v[u * D + lb / 2], lb & 1);
+            v7_store_pair<D, QH>(buf, r, G::H + i0, a.x, b.x, a.y, b.y);
+        }
+    }
+}
+
+template <int D, int QH>
+__device__ __forceinline__ void v7_copy_halo(const unsigned char* cur, unsigned char* nxt)
+{
+    using G = geom7<D, QH>;
+    constexpr int PER_PHASE = 6 * G::HR * 2;
+    constexpr int PIECES = D * PER_PHASE;
+    if constexpr (G::HR > 0) {
+        for (int t = threadIdx.x; t < PIECES; t += G::NT) {
+            const int r = t / PER_PHASE;
+            const int tt = t % PER_PHASE;
+            const int plane = tt / (G::HR * 2);
+            const int rem = tt % (G::HR * 2);
+            const int pbase = r * G::PH + (plane < 3 ? 0 : G::IM_OFF) + (plane % 3) * G::PLANE;
+            const uint4 d = *reinterpret_cast<const uint4*>(cur + pbase + (G::NB - G::HR) * 32 + rem * 16);
+            *reinterpret_cast<uint4*>(nxt + pbase + rem * 16) = d;
+        }
+    }
+}
+
+// Halo rows of the first chunk from global memory / history: z_r[i], i in [-H, 0) relative
+// to the chunk's first output.
+template <int D, int QH>
+__device__ __forceinline__ void v7_load_store_halo(unsigned char* buf, const float2* __restrict__ in,
+                                                   const float2* __restrict__ hist, int64_t ch, int64_t n_in, int L)
+{
+    using G = geom7<D, QH>;
+    if constexpr (G::H > 0) {
+        const int64_t m0 = ch * G::CHUNK; // first output of the chunk
+        for (int t = threadIdx.x; t < D * (G::H / 2); t += G::NT) {
+            const int r = t / (G::H / 2);
+            const int pi = t % (G::H / 2);
+            const int sr = r == 0 ? 0 : D - r;
+            const int64_t i = m0 - G::H + 2 * pi;
+            const float2 a = virt(in, hist, D * i + sr, n_in, L);
+            const float2 b = virt(in, hist, D * (i + 1) + sr, n_in, L);
+            v7_store_pair<D, QH>(buf, r, 2 * pi, a.x, b.x, a.y, b.y);
+        }
+    }
+}
+
+template <int D, int QH>
+__device__ __forceinline__ void v7_compute(const unsigned char* lds, const bf16x8 (&B)[D][3][QH / 2 + 1],
+                                           const bf16x4 (&T)[D][3], int64_t n_tile, int64_t n_out,
+                                           float2* __restrict__ out)
+{
+    using G = geom7<D, QH>;
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int rho = lane & 15;
+    const int c = rho & 1, b = rho >> 1;
+    const int g = lane >> 4;
+    const int phase = lane & 15;
+    const int row_base = c * G::IM_OFF + (G::HR + wave * (G::WAVE_OUT / 16) + b) * 32;
+    f32x4 hi[G::TILES], lo[G::TILES], hi_t[G::TILES], lo_t[G::TILES]; // _t: K tail (see v5_compute)
+#pragma unroll
+    for (int t = 0; t < G::TILES; ++t) {
+        hi[t] = f32x4{ 0.f, 0.f, 0.f, 0.f };
+        lo[t] = f32x4{ 0.f, 0.f, 0.f, 0.f };
+        hi_t[t] = f32x4{ 0.f, 0.f, 0.f, 0.f };
+        lo_t[t] = f32x4{ 0.f, 0.f, 0.f, 0.f };
+    }
+#pragma unroll
+    for (int r = 0; r < D; ++r) {
+        const unsigned char* ph = lds + r * G::PH;
+#pragma unroll
+        for (int st = 0; st < G::KS; ++st) {
+            const int q = 2 * st + (g >> 1);
+#pragma unroll
+            for (int t = 0; t < G::TILES; ++t) {
+                const int off = row_base + t * 8 * 32 - q * 32 + (g & 1) * 16;
+                const bf16x8 A0 = *reinterpret_cast<const bf16x8*>(ph + off);
+                const bf16x8 A1 = *reinterpret_cast<const bf16x8*>(ph + off + G::PLANE);
+                const bf16x8 A2 = *reinterpret_cast<const bf16x8*>(ph + off + 2 * G::PLANE);
+                hi[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A0, B[r][0][st], hi[t], 0, 0, 0);
+                lo[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A0, B[r][1][st], lo[t], 0, 0, 0);
+                lo[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A1, B[r][0][st], lo[t], 0, 0, 0);
+                lo[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A0, B[r][2][st], lo[t], 0, 0, 0);
+                lo[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A1, B[r][1][st], lo[t], 0, 0, 0);
+                lo[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A2, B[r][0][st], lo[t], 0, 0, 0);
+            }
+        }
+        if constexpr (G::TAIL) {
+#pragma unroll
+            for (int t = 0; t < G::TILES; ++t) {
+                const int off = row_base + t * 8 * 32 - (QH - 1) * 32 + g * 8;
+                const bf16x4 A0 = *reinterpret_cast<const bf16x4*>(ph + off);
+                const bf16x4 A1 = *reinterpret_cast<const bf16x4*>(ph + off + G::PLANE);
+                const bf16x4 A2 = *reinterpret_cast<const bf16x4*>(ph + off + 2 * G::PLANE);
+                hi_t[t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(A0, T[r][0], hi_t[t], 0, 0, 0);
+                lo_t[t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(A0, T[r][1], lo_t[t], 0, 0, 0);
+                lo_t[t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(A1, T[r][0], lo_t[t], 0, 0, 0);
+                lo_t[t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(A0, T[r][2], lo_t[t], 0, 0, 0);
+                lo_t[t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(A1, T[r][1], lo_t[t], 0, 0, 0);
+                lo_t[t] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(A2, T[r][0], lo_t[t], 0, 0, 0);
+            }
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < G::TILES; ++t) {
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+            const int blk = t * 8 + 2 * g + half;
+            const int64_t n = n_tile + (int64_t)wave * G::WAVE_OUT + blk * 16 + phase;
+            if (n < n_out) {
+                nf2 o = { (hi[t][2 * half] + hi_t[t][2 * half]) + (lo[t][2 * half] + lo_t[t][2 * half]),
+                          (hi[t][2 * half + 1] + hi_t[t][2 * half + 1]) + (lo[t][2 * half + 1] + lo_t[t][2 * half + 1]) };
+                __builtin_nontemporal_store(o, reinterpret_cast<nf2*>(out + n));
+            }
+        }
+    }
+}
+
+template <int D, int QH>
+__global__ __launch_bounds__(256, 2) void k_fir_mfma7(const float2* __restrict__ in,
+                                                     const float2* __restrict__ hist_in,
+                                                     float2* __restrict__ hist_out,
+                                                     float2* __restrict__ out,
+                                                     const unsigned short* __restrict__ frag,
+                                                     int L,
+                                                     int64_t n_out,
+                                                     int in_aligned)
+{
+    using G = geom7<D, QH>;
+    constexpr int KS = G::KS;
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int64_t n_in = n_out * D;
+
+    if (blockIdx.x == 0) {
+        for (int j = tid; j < L - 1; j += G::NT) hist_out[j] = virt(in, hist_in, n_in - (L - 1) + j, n_in, L);
+    }
+
+    // fragments: per phase r: [3][KS][64] bf16x8, then [3][64] bf16x4 tail
+    constexpr int PER_PHASE = 3 * KS * 64 * 8 + (G::TAIL ? 3 * 64 * 4 : 0); // bf16 elements
+    bf16x8 B[D][3][KS + 1];
+    bf16x4 T[D][3] = {};
+#pragma unroll
+    for (int r = 0; r < D; ++r) {
+        const unsigned short* fr = frag + (size_t)r * PER_PHASE;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+#pragma unroll
+            for (int st = 0; st < KS; ++st) B[r][k][st] = reinterpret_cast<const bf16x8*>(fr)[(k * KS + st) * 64 + lane];
+            if constexpr (G::TAIL) T[r][k] = reinterpret_cast<const bf16x4*>(fr + 3 * KS * 64 * 8)[k * 64 + lane];
+        }
+    }
+
+    const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
+    const int64_t per = (nchunks + gridDim.x - 1) / gridDim.x;
+    const int64_t c_begin = (int64_t)blockIdx.x * per;
+    const int64_t c_end = c_begin + per < nchunks ? c_begin + per : nchunks;
+    if (c_begin >= c_end) return;
+    const int64_t c_last = c_end - 1;
+    const bool al = in_aligned != 0;
+    auto clamp = [&](int64_t x) { return x <= c_last ? x : c_last; };
+
+    float4 va[G::VPT], vb[G::VPT];
+    v7_load_store_halo<D, QH>(lds, in, hist_in, c_begin, n_in, L);
+    v7_load_main<D, QH>(va, in, hist_in, c_begin, n_in, L, al);
+    v7_store_main<D, QH>(va, lds);
+    v7_load_main<D, QH>(va, in, hist_in, clamp(c_begin + 1), n_in, L, al);
+    __syncthreads();
+
+    auto step = [&](float4 (&nxt)[G::VPT], float4 (&ld)[G::VPT], int64_t ch) {
+        unsigned char* cur = lds + ((ch - c_begin) & 1) * G::BUF;
+        unsigned char* nbuf = lds + (((ch - c_begin) & 1) ^ 1) * G::BUF;
+        v7_load_main<D, QH>(ld, in, hist_in, clamp(ch + 2), n_in, L, al);
+        v7_copy_halo<D, QH>(cur, nbuf);
+        v7_store_main<D, QH>(nxt, nbuf);
+        v7_compute<D, QH>(cur, B, T, ch * G::CHUNK, n_out, out);
+        __syncthreads();
+    };
+    int64_t ch = c_begin;
+    for (; ch + 1 <= c_last; ch += 2) {
+        step(va, vb, ch);
+        step(vb, va, ch + 1);
+    }
+    if (ch <= c_last) step(va, vb, ch);
+}
+
+template <int D, int QH>
+int launch_v7(const nsh_fir_plan* p, const float2* in, const float2* hin, float2* hout, float2* out, int64_t n_out,
+              hipStream_t s)
+{
+    using G = geom7<D, QH>;
+    static bool attr_set = false;
+    if (!attr_set) {
+        NSH_CK(hipFuncSetAttribute((const void*)k_fir_mfma7<D, QH>, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
+        attr_set = true;
+    }
+    const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
+    int n_cu = 256;
+    (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, p->dev);
+    const int wg_per_cu = (160 * 1024) / G::LDS >= 3 ? 3 : 2; // LDS-bound residency (VGPRs allow 3)
+    const int64_t max_grid = (int64_t)n_cu * wg_per_cu;
+    const unsigned grid = (unsigned)(nchunks < max_grid ? nchunks : max_grid);
+    const int aligned = ((uintptr_t)in % 16 == 0) ? 1 : 0;
+    hipLaunchKernelGGL((k_fir_mfma7<D, QH>), dim3(grid), dim3(G::NT), G::LDS, s, in, hin, hout, out,
+                       (const unsigned short*)p->fragd_dev, p->L, n_out, aligned);
+    NSH_CK_LAUNCH("nsh_fir_ccf(mfma decim)");
+    return 0;
+}
+
+template <int D>
+int launch_dec(const nsh_fir_plan* p, const float2* in, const float2* hin, float2* hout, float2* out, int64_t n_out,
+               hipStream_t s)
+{
+    switch (p->QHD) {
+    case 2: return launch_v7<D, 2>(p, in, hin, hout, out, n_out, s);
+    case 3: return launch_v7<D, 3>(p, in, hin, hout, out, n_out, s);
+    case 4: return launch_v7<D, 4>(p, in, hin, hout, out, n_out, s);
+    case 5: return launch_v7<D, 5>(p, in, hin, hout, out, n_out, s);
+    case 6: return launch_v7<D, 6>(p, in, hin, hout, out, n_out, s);
+    default: return nsh::fail_msg("nsh_fir_ccf(mfma decim): unsupported tap count");
+    }
+}
+
 // Host-side bf16 round-to-nearest-even (taps are finite).
 unsigned short bf16_rne(float f)
 {
@@ -1159,18 +1495,75 @@ int launch_q(const nsh_fir_plan* p, const float2* in, const float2* hin, float2*
 
 } // namespace
 
+namespace {
+int decim_qh(const nsh_fir_plan* p) { return ((p->L + p->D - 1) / p->D + 1 + 15 + 15) / 16; }
+bool finite_taps(const nsh_fir_plan* p)
+{
+    for (float t : p->taps_host)
+        if (!(t == t) || t - t != 0.f) return false;
+    return true;
+}
+} // namespace
+
 bool nsh_fir_mfma_supported(const nsh_fir_plan* p)
 {
+    if (!finite_taps(p)) return false;
+    if (p->D == 2 || p->D == 4) return decim_qh(p) <= 6;
     if (p->D != 1) return false;
     const int Q = (p->L + 30) / 32 + 1;
-    for (float t : p->taps_host)
-        if (!(t == t) || t - t != 0.f) return false; // finite taps only
     return Q <= QMAX;
+}
+
+int nsh_fir_mfma_prepare_decim(nsh_fir_plan* p)
+{
+    // polyphase taps h'_0[j] = h[D j], h'_r[j] = h[D (j - 1) + r] (r >= 1, j >= 1), laid out
+    // per phase as the 16-sample form's fragments (see k_fir_mfma7)
+    const int D = p->D, QH = decim_qh(p), KS = QH / 2;
+    const bool tail = QH % 2;
+    p->QHD = QH;
+    const size_t per_phase = (size_t)3 * KS * 64 * 8 + (tail ? (size_t)3 * 64 * 4 : 0);
+    std::vector<unsigned short> f((size_t)D * per_phase, 0);
+    auto tap = [&](int r, int j) -> float {
+        const int k = r == 0 ? D * j : (j >= 1 ? D * (j - 1) + r : -1);
+        return (k >= 0 && k < p->L) ? p->taps_host[k] : 0.f;
+    };
+    auto put3 = [&](float hv, size_t i0, size_t i1, size_t i2) {
+        const unsigned short h1 = bf16_rne(hv);
+        const float r1 = hv - bf16_to_f(h1);
+        const unsigned short h2 = bf16_rne(r1);
+        f[i0] = h1;
+        f[i1] = h2;
+        f[i2] = bf16_rne(r1 - bf16_to_f(h2));
+    };
+    for (int r = 0; r < D; ++r) {
+        const size_t base = (size_t)r * per_phase;
+        for (int st = 0; st < KS; ++st)
+            for (int lane = 0; lane < 64; ++lane)
+                for (int j = 0; j < 8; ++j) {
+                    const int kk = 8 * (lane >> 4) + j;
+                    const float hv = tap(r, (lane & 15) - (kk & 15) + 16 * (2 * st + (kk >> 4)));
+                    put3(hv, base + (((size_t)0 * KS + st) * 64 + lane) * 8 + j, base + (((size_t)1 * KS + st) * 64 + lane) * 8 + j,
+                         base + (((size_t)2 * KS + st) * 64 + lane) * 8 + j);
+                }
+        if (tail) {
+            const size_t t0 = base + (size_t)3 * KS * 64 * 8;
+            for (int lane = 0; lane < 64; ++lane)
+                for (int j = 0; j < 4; ++j) {
+                    const float hv = tap(r, (lane & 15) - (4 * (lane >> 4) + j) + 16 * (QH - 1));
+                    put3(hv, t0 + ((size_t)0 * 64 + lane) * 4 + j, t0 + ((size_t)1 * 64 + lane) * 4 + j,
+                         t0 + ((size_t)2 * 64 + lane) * 4 + j);
+                }
+        }
+    }
+    NSH_CK(hipMalloc(&p->fragd_dev, f.size() * sizeof(unsigned short)));
+    NSH_CK(hipMemcpy(p->fragd_dev, f.data(), f.size() * sizeof(unsigned short), hipMemcpyHostToDevice));
+    return 0;
 }
 
 int nsh_fir_mfma_prepare(nsh_fir_plan* p)
 {
     if (const char* v = std::getenv("NSH_FIR_MFMA_VARIANT")) p->variant = std::atoi(v);
+    if (p->D > 1) return nsh_fir_mfma_prepare_decim(p);
     const int Q = (p->L + 30) / 32 + 1;
     const int S = 2 * Q;
     p->Q = Q;
@@ -1270,6 +1663,8 @@ int nsh_fir_mfma16_run(const nsh_fir_plan* p, const float2* in, const float2* hi
 
 int nsh_fir_mfma_run(const nsh_fir_plan* p, const float2* in, const float2* hist_in, float2* hist_out, float2* out, int64_t n_out, hipStream_t s)
 {
+    if (p->D == 2) return launch_dec<2>(p, in, hist_in, hist_out, out, n_out, s);
+    if (p->D == 4) return launch_dec<4>(p, in, hist_in, hist_out, out, n_out, s);
     if (p->variant >= 20) return nsh_fir_mfma16_run(p, in, hist_in, hist_out, out, n_out, s); // A/B tuning
     switch (p->Q) {
     case 1: return launch_q<1>(p, in, hist_in, hist_out, out, n_out, s);

@@ -20,6 +20,10 @@ struct nsh_fir_plan {
     // 32; [part(3)][kstep][lane(64)][8] bf16.
     int QH = 0;
     void* frag16_dev = nullptr;
+    // decimating polyphase form (D = 2, 4): per phase QHD tap blocks of 16,
+    // [phase][part(3)][kstep][lane][8] + [phase][part][lane][4] tail, bf16.
+    int QHD = 0;
+    void* fragd_dev = nullptr;
     int variant = 0;      // MFMA kernel tuning variant (0 = default)
 };
 

@@ -177,6 +177,32 @@ def test_fir_decim_vs_oracle(torch_cuda, decim):
         np.testing.assert_array_equal(hout, h_ref)
 
 
+@pytest.mark.parametrize("decim", [2, 4])
+@pytest.mark.parametrize("ntaps", [1, 2, 15, 16, 17, 33, 64, 127, 128, 160])
+@pytest.mark.parametrize("n_out", [1, 100, 1023, 1024, 1025, 33333])
+def test_fir_decim_mfma_vs_oracle(torch_cuda, decim, ntaps, n_out):
+    """Polyphase MFMA form (k_fir_mfma7): every phase/halo/tail shape against the oracle."""
+    torch = torch_cuda
+    rng = np.random.default_rng(ntaps * 7919 + n_out * decim)
+    h = rng.standard_normal(ntaps).astype(np.float32) * 0.1
+    x = orc.synth(n_out * decim, 11 + n_out)
+    hist = orc.synth(max(ntaps - 1, 1), 5 * 10 ** 6)[: ntaps - 1]
+    plan = nsh.FirPlan(h, decim, nsh.FIR_MFMA)
+    assert plan.algo == nsh.FIR_MFMA
+    y, hout = run_fir(torch, plan, x, n_out, hist=hist if ntaps > 1 else None)
+    y_ref, h_ref = orc.fir_ccf(x, h, decim=decim, hist=hist if ntaps > 1 else None, return_hist=True)
+    ok, err, scale = orc.tol_ok(y, y_ref)
+    assert ok, (decim, ntaps, n_out, err, scale)
+    np.testing.assert_array_equal(hout, h_ref)
+
+
+def test_fir_decim_auto_picks_mfma(torch_cuda):
+    h = np.hanning(127).astype(np.float32)
+    assert nsh.FirPlan(h, 2).algo == nsh.FIR_MFMA
+    assert nsh.FirPlan(h, 4).algo == nsh.FIR_MFMA
+    assert nsh.FirPlan(h, 8).algo == nsh.FIR_DIRECT
+
+
 def test_fir_decim2_golden_chain(torch_cuda, golden):
     torch = torch_cuda
     g = golden("fir127_decim2.npz")

@@ -57,9 +57,11 @@ def main():
     ms = timeit(lambda: nsh.channelizer1024(x, y, w, n // 1024, stream=s), a.reps, s)
     res["chan1024"] = {"ms": ms, "GS/s": n / ms / 1e6, "GB/s": 16 * n / ms / 1e6}
     for dd in (2, 4):
-        p = nsh.FirPlan(ss.firwin(127, 0.45).astype(np.float32), dd, nsh.FIR_DIRECT)
-        ms = timeit(lambda: p(x, hin, hout, y, n // dd, stream=s), a.reps, s)
-        res[f"fir_direct_d{dd}"] = {"ms": ms, "GS/s_in": n / ms / 1e6}
+        for nm, al in (("direct", nsh.FIR_DIRECT), ("mfma", nsh.FIR_MFMA)):
+            p = nsh.FirPlan(ss.firwin(127, 0.45).astype(np.float32), dd, al)
+            ms = timeit(lambda: p(x, hin, hout, y, n // dd, stream=s), a.reps, s)
+            gbs = (8 + 8 / dd) * n / ms / 1e6
+            res[f"fir_{nm}_d{dd}"] = {"ms": ms, "GS/s_in": n / ms / 1e6, "GB/s": gbs, "hbm_frac": gbs / 8000}
     print(json.dumps(res, indent=1))
 
 
