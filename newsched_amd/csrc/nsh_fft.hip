@@ -6,13 +6,20 @@
 //   forward  X[k] = sum_n x[n] e^{-2 pi i kn/1024}            (= numpy.fft.fft)
 //   inverse  x[n] = sum_k X[k] e^{+2 pi i kn/1024}            (= 1024 * numpy.fft.ifft)
 //
-// One 256-thread workgroup per 1024-sample frame (grid-stride over frames): Stockham
-// autosort radix-4, five passes, each thread owning one radix-4 butterfly per pass; pass 0
-// reads HBM (coalesced: thread j reads samples j, j+256, j+512, j+768), passes ping-pong
-// through two 8 KiB LDS images, the last pass writes HBM. Twiddles come from a 1024-entry
-// table computed in double on the host (accuracy ~log2(N) * 2^-24 relative).
-// The channelizer keeps the spectrum in LDS between the forward and inverse transforms,
-// so a frame crosses HBM once each way (16 B/sample instead of 48 B unfused).
+// One wavefront per 1024-sample frame (4 frames per 256-thread workgroup, grid-stride):
+// Stockham autosort in three passes, radix 16 / 16 / 4, each lane owning 16 samples:
+//   pass 1 (Ns = 1):   lane j loads x[j + 64 r] (coalesced), DFT16 in registers -> LDS
+//   pass 2 (Ns = 16):  reads LDS[j + 64 r], twiddles W_256^{k r}, DFT16 -> LDS
+//   pass 3 (Ns = 256): 4 radix-4 butterflies per lane, twiddles W_1024^{k r} -> HBM
+// DFT16 = 4 x DFT4, internal W_16 twiddles, 4 x DFT4 (index transpose at compile time). The
+// LDS image (one per wave, 8.5 KiB) has one pad sample per 16 so every exchange is
+// bank-conflict-free; a wave's LDS operations complete in order, so the passes need no
+// workgroup barriers. Twiddles come from a 1024-entry table computed in double on the host
+// and staged in LDS once per workgroup. The next frame's samples are prefetched into
+// registers while the current frame transforms. The channelizer multiplies the spectrum
+// by W in registers and runs the inverse transform directly: pass 3 leaves lane j holding
+// indices j + 64 m (m < 16), exactly pass 1's input layout, so a frame crosses HBM once
+// each way (16 B/sample instead of 48 B unfused) and LDS twice per transform.
 #include "nsh_common.hpp"
 
 #include <cmath>
@@ -34,89 +41,179 @@ __device__ __forceinline__ float2 rot(float2 a)
     return INV ? make_float2(-a.y, a.x) : make_float2(a.y, -a.x);
 }
 
-// One Stockham radix-4 pass for butterfly j (0..255): Ns = size of finished sub-FFTs.
+// In-place DFT4 of (a, b, c, d): X_k = sum_n x_n W_4^{nk}, W_4 = e^{-+i pi/2}.
 template <bool INV>
-__device__ __forceinline__ void pass(float2 (&v)[4], int j, int Ns, const float2* __restrict__ tw)
+__device__ __forceinline__ void dft4(float2& a, float2& b, float2& c, float2& d)
 {
-    const int k = j & (Ns - 1);
-    if (Ns > 1) {
-        // twiddle exp(-+2 pi i k r / (4 Ns)) = W[k r N/(4 Ns)], W[t] = e^{-2 pi i t/N}
-        const int step = (N / 4) / Ns * k;
-#pragma unroll
-        for (int r = 1; r < 4; ++r) {
-            float2 w = tw[(step * r) & (N - 1)];
-            if (INV) w.y = -w.y;
-            v[r] = cmul(v[r], w);
-        }
-    }
-    const float2 a0 = cadd(v[0], v[2]);
-    const float2 a1 = csub(v[0], v[2]);
-    const float2 a2 = cadd(v[1], v[3]);
-    const float2 a3 = rot<INV>(csub(v[1], v[3]));
-    v[0] = cadd(a0, a2);
-    v[1] = cadd(a1, a3);
-    v[2] = csub(a0, a2);
-    v[3] = csub(a1, a3);
+    const float2 s0 = cadd(a, c), d0 = csub(a, c);
+    const float2 s1 = cadd(b, d), d1 = rot<INV>(csub(b, d));
+    a = cadd(s0, s1);
+    c = csub(s0, s1);
+    b = cadd(d0, d1);
+    d = csub(d0, d1);
 }
 
-__device__ __forceinline__ int expand(int j, int Ns) { return (j / Ns) * Ns * 4 + (j & (Ns - 1)); }
-
-// Full transform of a frame already in LDS image `a` (natural order) -> registers of the
-// last pass written to `dst` (global or LDS) in natural order.
-template <bool INV, bool FROM_GLOBAL>
-__device__ __forceinline__ void fft_frame(const float2* __restrict__ src, float2* __restrict__ dst,
-                                          float2* __restrict__ la, float2* __restrict__ lb,
-                                          const float2* __restrict__ tw, const float2* __restrict__ mulw)
+// W_16^m, m = 0..9 (forward; conjugated for the inverse)
+template <bool INV>
+__device__ __forceinline__ float2 w16(int m)
 {
-    const int j = threadIdx.x;
-    float2 v[4];
-    int Ns = 1;
-    const float2* cur = src;
-    float2* bufs[2] = { la, lb };
-    int pp = 0;
-#pragma unroll
-    for (int s = 0; s < 5; ++s) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = cur[j + r * (N / 4)];
-        pass<INV>(v, j, Ns, tw);
-        const int e = expand(j, Ns);
-        float2* o = (s == 4) ? dst : bufs[pp];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            float2 y = v[r];
-            if (s == 4 && mulw) y = cmul(y, mulw[e + r * Ns]);
-            o[e + r * Ns] = y;
-        }
-        if (s < 4) {
-            __syncthreads();
-            cur = bufs[pp];
-            pp ^= 1;
-        }
-        Ns *= 4;
+    constexpr float C1 = 0.92387953251128674f, S1 = 0.38268343236508978f, R2 = 0.70710678118654757f;
+    float2 w;
+    switch (m) {
+    case 1: w = make_float2(C1, -S1); break;
+    case 2: w = make_float2(R2, -R2); break;
+    case 3: w = make_float2(S1, -C1); break;
+    case 4: w = make_float2(0.f, -1.f); break;
+    case 6: w = make_float2(-R2, -R2); break;
+    case 9: w = make_float2(-C1, S1); break;
+    default: w = make_float2(1.f, 0.f); break;
     }
-    (void)FROM_GLOBAL;
+    if (INV) w.y = -w.y;
+    return w;
 }
+
+// In-place DFT16, natural order in and out: n = 4 n1 + n2, k = k1 + 4 k2,
+// X[k] = sum_n2 W_4^{n2 k2} W_16^{n2 k1} sum_n1 x[4 n1 + n2] W_4^{n1 k1}.
+template <bool INV>
+__device__ __forceinline__ void dft16(float2 (&v)[16])
+{
+#pragma unroll
+    for (int n2 = 0; n2 < 4; ++n2) dft4<INV>(v[n2], v[n2 + 4], v[n2 + 8], v[n2 + 12]); // v[n2 + 4 k1] = Y[n2][k1]
+#pragma unroll
+    for (int n2 = 1; n2 < 4; ++n2)
+#pragma unroll
+        for (int k1 = 1; k1 < 4; ++k1) v[n2 + 4 * k1] = cmul(v[n2 + 4 * k1], w16<INV>(n2 * k1));
+#pragma unroll
+    for (int k1 = 0; k1 < 4; ++k1) dft4<INV>(v[4 * k1], v[4 * k1 + 1], v[4 * k1 + 2], v[4 * k1 + 3]); // v[4 k1 + k2] = X[k1 + 4 k2]
+    float2 t[16];
+#pragma unroll
+    for (int k1 = 0; k1 < 4; ++k1)
+#pragma unroll
+        for (int k2 = 0; k2 < 4; ++k2) t[k1 + 4 * k2] = v[4 * k1 + k2];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v[k] = t[k];
+}
+
+constexpr int WLDS = N + N / 16; // one wave's padded image
+__device__ __forceinline__ int pad(int i) { return i + (i >> 4); }
+
+template <bool INV>
+__device__ __forceinline__ float2 twid(const float2* __restrict__ tw, int t)
+{
+    float2 w = tw[t & (N - 1)];
+    if (INV) w.y = -w.y;
+    return w;
+}
+
+// Transform of one frame held as v[m] = x[lane + 64 m]; on return v[m] = X[lane + 64 m]
+// (pass 3 output kept in registers: m = b + 4 r for butterfly b, output r).
+template <bool INV>
+__device__ __forceinline__ void fft_wave(float2 (&v)[16], float2* __restrict__ img, const float2* __restrict__ tw)
+{
+    const int j = threadIdx.x & 63;
+    // pass 1: Ns = 1, radix 16 -> dst[16 j + r]
+    dft16<INV>(v);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) img[pad(16 * j + r)] = v[r];
+    __builtin_amdgcn_wave_barrier();
+    // pass 2: Ns = 16, radix 16: src[j + 64 r], twiddle W_256^{k r} = W_1024^{4 k r} -> dst[(j >> 4) 256 + k + 16 r]
+    const int k2 = j & 15;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = img[pad(j + 64 * r)];
+#pragma unroll
+    for (int r = 1; r < 16; ++r) v[r] = cmul(v[r], twid<INV>(tw, 4 * k2 * r));
+    dft16<INV>(v);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) img[pad((j >> 4) * 256 + k2 + 16 * r)] = v[r];
+    __builtin_amdgcn_wave_barrier();
+    // pass 3: Ns = 256, radix 4; butterfly b of this lane: j' = j + 64 b, src[j' + 256 r],
+    // twiddle W_1024^{j' r}, output index j' + 256 r  -> v[b + 4 r]
+    float2 o[16];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const int jp = j + 64 * b;
+        float2 a0 = img[pad(jp)], a1 = img[pad(jp + 256)], a2 = img[pad(jp + 512)], a3 = img[pad(jp + 768)];
+        a1 = cmul(a1, twid<INV>(tw, jp));
+        a2 = cmul(a2, twid<INV>(tw, 2 * jp));
+        a3 = cmul(a3, twid<INV>(tw, 3 * jp));
+        dft4<INV>(a0, a1, a2, a3);
+        o[b] = a0;
+        o[b + 4] = a1;
+        o[b + 8] = a2;
+        o[b + 12] = a3;
+    }
+    __builtin_amdgcn_wave_barrier(); // the image is rewritten by this wave's next transform
+#pragma unroll
+    for (int m = 0; m < 16; ++m) v[m] = o[m];
+}
+
+__device__ __forceinline__ void load_frame16(float2 (&v)[16], const float2* __restrict__ src)
+{
+    const int j = threadIdx.x & 63;
+#pragma unroll
+    for (int m = 0; m < 16; ++m) v[m] = src[j + 64 * m];
+}
+__device__ __forceinline__ void store_frame16(const float2 (&v)[16], float2* __restrict__ dst)
+{
+    const int j = threadIdx.x & 63;
+#pragma unroll
+    for (int m = 0; m < 16; ++m) dst[j + 64 * m] = v[m];
+}
+
+constexpr int FPW = NT / 64; // frames (waves) per workgroup
 
 template <bool INV>
 __global__ __launch_bounds__(NT) void k_fft1024(const float2* __restrict__ in, float2* __restrict__ out, int64_t nframes,
-                                                const float2* __restrict__ tw)
+                                                const float2* __restrict__ tw_g)
 {
-    __shared__ float2 la[N], lb[N];
-    for (int64_t f = blockIdx.x; f < nframes; f += gridDim.x) {
-        fft_frame<INV, true>(in + f * N, out + f * N, la, lb, tw, nullptr);
-        __syncthreads();
+    __shared__ float2 tw[N];
+    __shared__ float2 img_all[FPW * WLDS];
+    for (int t = threadIdx.x; t < N; t += NT) tw[t] = tw_g[t];
+    __syncthreads();
+    float2* img = img_all + (threadIdx.x >> 6) * WLDS;
+    const int64_t stride = (int64_t)gridDim.x * FPW;
+    int64_t f = (int64_t)blockIdx.x * FPW + (threadIdx.x >> 6);
+    if (f >= nframes) return;
+    float2 v[16], nx[16];
+    load_frame16(v, in + f * N);
+    for (; f < nframes; f += stride) {
+        const int64_t fn = f + stride;
+        if (fn < nframes) load_frame16(nx, in + fn * N);
+        fft_wave<INV>(v, img, tw);
+        store_frame16(v, out + f * N);
+#pragma unroll
+        for (int m = 0; m < 16; ++m) v[m] = nx[m];
     }
 }
 
 __global__ __launch_bounds__(NT) void k_chan1024(const float2* __restrict__ in, float2* __restrict__ out, int64_t nframes,
-                                                 const float2* __restrict__ tw, const float2* __restrict__ w)
+                                                 const float2* __restrict__ tw_g, const float2* __restrict__ w)
 {
-    __shared__ float2 la[N], lb[N], lc[N];
-    for (int64_t f = blockIdx.x; f < nframes; f += gridDim.x) {
-        fft_frame<false, true>(in + f * N, lc, la, lb, tw, w); // spectrum * w -> lc
-        __syncthreads();
-        fft_frame<true, false>(lc, out + f * N, la, lb, tw, nullptr);
-        __syncthreads();
+    __shared__ float2 tw[N];
+    __shared__ float2 img_all[FPW * WLDS];
+    for (int t = threadIdx.x; t < N; t += NT) tw[t] = tw_g[t];
+    __syncthreads();
+    float2* img = img_all + (threadIdx.x >> 6) * WLDS;
+    const int j = threadIdx.x & 63;
+    float2 wr[16]; // this lane's spectral weights W[j + 64 m]
+#pragma unroll
+    for (int m = 0; m < 16; ++m) wr[m] = w[j + 64 * m];
+    const int64_t stride = (int64_t)gridDim.x * FPW;
+    int64_t f = (int64_t)blockIdx.x * FPW + (threadIdx.x >> 6);
+    if (f >= nframes) return;
+    float2 v[16], nx[16];
+    load_frame16(v, in + f * N);
+    for (; f < nframes; f += stride) {
+        const int64_t fn = f + stride;
+        if (fn < nframes) load_frame16(nx, in + fn * N);
+        fft_wave<false>(v, img, tw);
+#pragma unroll
+        for (int m = 0; m < 16; ++m) v[m] = cmul(v[m], wr[m]);
+        fft_wave<true>(v, img, tw);
+        store_frame16(v, out + f * N);
+#pragma unroll
+        for (int m = 0; m < 16; ++m) v[m] = nx[m];
     }
 }
 
@@ -144,8 +241,9 @@ int twiddles(int dev, const float2** tw)
 
 unsigned frame_grid(int64_t nframes)
 {
-    const int64_t cap = 256 * 32;
-    return (unsigned)(nframes < cap ? nframes : cap);
+    const int64_t groups = (nframes + FPW - 1) / FPW;
+    const int64_t cap = 256 * 16;
+    return (unsigned)(groups < cap ? groups : cap);
 }
 
 } // namespace
