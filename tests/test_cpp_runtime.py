@@ -11,11 +11,11 @@ from tests.conftest import ROOT
 BIN = os.path.join(ROOT, "build", "tests")
 
 
-def run(name, timeout):
+def run(name, timeout, *cases):
     exe = os.path.join(BIN, name)
     if not os.path.exists(exe):
         subprocess.run(["make", "-s", "-C", ROOT, "tests"], check=True)
-    p = subprocess.run([exe], capture_output=True, text=True, timeout=timeout)
+    p = subprocess.run([exe, *cases], capture_output=True, text=True, timeout=timeout)
     print(p.stdout)
     print(p.stderr)
     assert p.returncode == 0, p.stdout + p.stderr
@@ -31,3 +31,15 @@ def test_scheduler_mt_behaviour():
 def test_hip_flowgraphs():
     out = run("qa_hip_flowgraph", 900)
     assert "0 failure(s)" in out
+
+
+def test_tags_reference_counts():
+    """Reference schedulers/mt/test/qa_tags.cpp OneToOne/t1/t2/t3 with its expected counts."""
+    out = run("qa_tags", 300, "SchedulerMTTags")
+    assert "4 test(s), 0 failure(s)" in out
+
+
+@pytest.mark.gpu
+def test_tags_through_device_edges():
+    out = run("qa_tags", 300, "DeviceTags")
+    assert "1 test(s), 0 failure(s)" in out
