@@ -2,14 +2,14 @@
 // real taps, optional decimation), y[m] = sum_k h[k] x[m D - k], zero initial history.
 // Absent from the reference; this is the CPU-baseline FIR the bench
 // times on the host cores (thread per block, 8192-item vmcircbuf edges), vectorised for
-// AVX-512/AVX2 by function multiversioning, fp32 accumulation in tap order. It derives
-// from gr::block (not sync_block) so decimation can consume D items per output.
+// AVX-512/AVX2 by function multiversioning, fp32 accumulation in tap order. A
+// gr::decim_block: the runtime clamps and consumes D items per output.
 #pragma once
-#include <gnuradio/block.hpp>
+#include <gnuradio/decim_block.hpp>
 
 namespace gr {
 namespace blocks {
-class fir_filter_ccf : public block
+class fir_filter_ccf : public decim_block
 {
 public:
     using sptr = std::shared_ptr<fir_filter_ccf>;

@@ -1,16 +1,17 @@
 // gr::hip::fir_filter_ccf -- the MI355X hot path (BASELINE config C3/C5).
-// Complex fp32 stream, real fp32 taps, optional decimation D (n_consumed = D*n_produced).
+// Complex fp32 stream, real fp32 taps, optional decimation D (a gr::decim_block: the
+// runtime clamps the call to D readable items per output and consumes D*n_produced).
 // The block owns the device tap plan and two (ntaps-1)-sample history buffers it
 // ping-pongs between work() calls, because the block API has no history (reference
 // runtime/include/gnuradio/sync_block.hpp:36-86). Device state is created on the first
 // start() on the partition thread (right device and stream) and the history is zeroed on
 // every start() (a fresh stream). Algorithm: nsh_fir_algo (AUTO = MFMA for D = 1).
 #pragma once
-#include <gnuradio/block.hpp>
+#include <gnuradio/decim_block.hpp>
 
 namespace gr {
 namespace hip {
-class fir_filter_ccf : public block
+class fir_filter_ccf : public decim_block
 {
 public:
     using sptr = std::shared_ptr<fir_filter_ccf>;

@@ -125,7 +125,7 @@ template class arith_cc<0>;
 template class arith_cc<1>;
 
 fir_filter_ccf::fir_filter_ccf(const std::vector<float>& taps, int decim)
-    : block("fir_filter_ccf"), _taps(taps), _decim(decim)
+    : decim_block("fir_filter_ccf", (unsigned)decim), _taps(taps), _decim(decim)
 {
     if (taps.empty()) throw std::invalid_argument("fir_filter_ccf: no taps");
     if (decim < 1) throw std::invalid_argument("fir_filter_ccf: decimation < 1");
@@ -140,8 +140,7 @@ bool fir_filter_ccf::start()
 work_return_code_t fir_filter_ccf::work(std::vector<block_work_input>& in, std::vector<block_work_output>& out)
 {
     const int L = (int)_taps.size();
-    const int n_out = std::min(out[0].n_items, in[0].n_items / _decim);
-    if (n_out <= 0) return work_return_code_t::WORK_INSUFFICIENT_INPUT_ITEMS;
+    const int n_out = out[0].n_items; // decim_block::do_work: in[0].n_items == D * n_out
     const size_t n_in = (size_t)n_out * _decim;
     const gr_complex* x = static_cast<const gr_complex*>(in[0].buffer->read_ptr());
     _ext.resize((size_t)(L - 1) + n_in);
@@ -151,7 +150,6 @@ work_return_code_t fir_filter_ccf::work(std::vector<block_work_input>& in, std::
     // keep the last L-1 inputs as history
     std::memmove(_ext.data(), _ext.data() + n_in, (size_t)(L - 1) * sizeof(gr_complex));
     _ext.resize((size_t)(L - 1));
-    in[0].n_consumed = (int)n_in;
     out[0].n_produced = n_out;
     return work_return_code_t::WORK_OK;
 }

@@ -86,7 +86,7 @@ template class arith_cc<1>;
 
 // ---- FIR ---------------------------------------------------------------------------
 fir_filter_ccf::fir_filter_ccf(const std::vector<float>& taps, int decim, int algo)
-    : block("fir_filter_ccf (hip)"), _taps(taps), _decim(decim), _algo(algo)
+    : decim_block("fir_filter_ccf (hip)", (unsigned)decim), _taps(taps), _decim(decim), _algo(algo)
 {
     if (taps.empty()) throw std::invalid_argument("hip::fir_filter_ccf: no taps");
     if (decim != 1 && decim != 2 && decim != 4 && decim != 8)
@@ -140,8 +140,7 @@ bool fir_filter_ccf::start()
 
 work_return_code_t fir_filter_ccf::work(std::vector<block_work_input>& in, std::vector<block_work_output>& out)
 {
-    const int n_out = std::min(out[0].n_items, in[0].n_items / _decim);
-    if (n_out <= 0) return work_return_code_t::WORK_INSUFFICIENT_INPUT_ITEMS;
+    const int n_out = out[0].n_items; // decim_block::do_work: in[0].n_items == D * n_out
     void* s = current_stream();
     std::pair<void*, void*>* ev = nullptr;
     if (_timing) {
@@ -163,7 +162,6 @@ work_return_code_t fir_filter_ccf::work(std::vector<block_work_input>& in, std::
     }
     _cur ^= 1;
     ++_launches;
-    in[0].n_consumed = n_out * _decim;
     out[0].n_produced = n_out;
     return work_return_code_t::WORK_OK;
 }

@@ -58,6 +58,12 @@ public:
         return work(work_input, work_output);
     }
 
+    // Output items per input item (1 for sync blocks, 1/D for decim_block) and the output
+    // granularity; buffer managers size edges from them.
+    virtual double relative_rate() const { return 1.0; }
+    int output_multiple() const { return d_output_multiple; }
+    void set_output_multiple(int m) { d_output_multiple = m > 0 ? m : 1; }
+
     // weak: the scheduler owns its blocks (a strong back-reference would leak both)
     void set_scheduler(std::shared_ptr<scheduler> s) { p_scheduler = s; }
     std::shared_ptr<scheduler> get_scheduler() const { return p_scheduler.lock(); }
@@ -70,6 +76,7 @@ protected:
 private:
     bool d_running = false;
     tag_propagation_policy_t d_tag_propagation_policy;
+    int d_output_multiple = 1;
 };
 
 using block_sptr = block::sptr;

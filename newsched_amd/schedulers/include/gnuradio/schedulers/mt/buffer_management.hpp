@@ -22,8 +22,11 @@ public:
     std::vector<buffer_sptr>& get_output_buffers(port_sptr p) { return d_block_buffers.at(p); }
     std::vector<buffer_sptr> all_buffers() const;
 
-private:
+    // Items for the edge buffer: 2 * fixed_buf_size / itemsize, at least 2 * D *
+    // output_multiple when the downstream block decimates by D.
     size_t get_buffer_num_items(edge_sptr e, flat_graph_sptr fg) const;
+
+private:
     const size_t s_fixed_buf_size;
     std::map<port_sptr, std::vector<buffer_sptr>> d_block_buffers;
     std::map<edge*, buffer_sptr> d_edge_buffers;

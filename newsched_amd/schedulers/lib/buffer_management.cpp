@@ -1,4 +1,6 @@
 // Edge buffers (reference schedulers/mt/lib/buffer_management.cpp:8-148).
+#include <cmath>
+#include <gnuradio/block.hpp>
 #include <gnuradio/domain_adapter.hpp>
 #include <gnuradio/domain_adapter_direct.hpp>
 #include <gnuradio/schedulers/mt/buffer_management.hpp>
@@ -56,7 +58,18 @@ size_t buffer_manager::get_buffer_num_items(edge_sptr e, flat_graph_sptr) const
 {
     // 2x: buffers are filled at most half way (reference buffer_management.cpp:110-148).
     const size_t isz = e->itemsize() ? e->itemsize() : 1;
-    return std::max<size_t>((2 * s_fixed_buf_size) / isz, 2);
+    size_t nitems = std::max<size_t>((2 * s_fixed_buf_size) / isz, 2);
+    // A decimator needs D * output_multiple readable items per call: size its input edge
+    // for two such calls (the reference's commented-out rule, :125-145). The edge object
+    // carries both endpoints, so domain adapters do not hide the downstream block here.
+    if (auto b = std::dynamic_pointer_cast<block>(e->dst().node())) {
+        const double rr = b->relative_rate();
+        if (rr > 0 && rr < 1.0) {
+            const size_t need = 2 * (size_t)std::ceil(1.0 / rr) * (size_t)b->output_multiple();
+            nitems = std::max(nitems, need);
+        }
+    }
+    return nitems;
 }
 
 } // namespace schedulers
