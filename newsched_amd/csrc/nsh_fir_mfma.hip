@@ -20,7 +20,8 @@
 // bf16 keeps the fp32 exponent range, so no input scaling is needed. Non-finite inputs
 // are not supported by this form (use NSH_FIR_DIRECT).
 //
-// Data movement (v2, the default; v1 below is kept for A/B runs): a 256-thread workgroup
+// Data movement (v2, the NSH_FIR_MFMA kernel; the 16-sample form v5 and the decimating
+// form v7 follow below): a 256-thread workgroup
 // (2 per CU) walks a contiguous range of 2048-output chunks. Each chunk's 2048 samples are
 // loaded with 16-byte nontemporal global loads into registers two chunks ahead, split, and
 // written as six bf16 planes (re/im x 3 terms) to one of two LDS buffers while the MFMAs
@@ -40,7 +41,9 @@
 #include "nsh_fir_plan.hpp"
 
 // Ablation hooks for tools/probe/fir_ablate.sh only (bit mask; 0 in every product build):
-// 1 = no MFMA, 2 = no global loads, 4 = no bf16 split, 8 = no global stores.
+// 1 = no MFMA, 2 = no global loads, 4 = no bf16 split, 8 = no global stores; timing-only
+// (wrong results): 16 = half the MFMAs, 32 = int8 MFMA instruction count, 64 = the same
+// FLOPs as 16x16x32 MFMAs, 128 = A fragments read once and reused.
 #ifndef NSH_FIR_ABLATE
 #define NSH_FIR_ABLATE 0
 #endif
@@ -56,36 +59,6 @@ typedef float nf2 __attribute__((ext_vector_type(2)));
 constexpr int TILE = 512;   // outputs per wave per chunk
 constexpr int QMAX = 6;     // L <= 161
 
-// NW waves per workgroup (one 512-output tile each); DEPTH chunks of input in flight
-// per workgroup (register prefetch).
-template <int Q, int NW = 4>
-struct geom {
-    static constexpr int NT = 64 * NW;                        // threads per workgroup
-    static constexpr int CHUNK = TILE * NW;                   // outputs per chunk
-    static constexpr int S = 2 * Q;                           // k-steps of 16
-    static constexpr int H = 32 * (Q - 1);                    // halo samples
-    static constexpr int NS = CHUNK + H;                      // staged samples per chunk
-    static constexpr int NB = NS / 32;                        // staged 32-sample rows
-    static constexpr int PLANE = (NB * 80 + 255) / 256 * 256; // bytes per bf16 plane
-    static constexpr int LDS = 6 * PLANE;
-    static constexpr int NV = NS / 2;                         // 16-byte vectors per chunk
-    static constexpr int VPT = (NV + NT - 1) / NT;            // vectors per thread
-};
-
-__device__ __forceinline__ void split3(float x, __bf16& t1, __bf16& t2, __bf16& t3)
-{
-    t1 = (__bf16)x;
-    const float r1 = x - (float)t1; // exact
-    t2 = (__bf16)r1;
-    const float r2 = r1 - (float)t2; // exact
-    t3 = (__bf16)r2;                 // exact for finite normal x
-}
-
-__device__ __forceinline__ unsigned pack2(__bf16 a, __bf16 b)
-{
-    return (unsigned)__builtin_bit_cast(unsigned short, a) | ((unsigned)__builtin_bit_cast(unsigned short, b) << 16);
-}
-
 __device__ __forceinline__ float2 virt(const float2* __restrict__ in, const float2* __restrict__ hist, int64_t g, int64_t n_in, int L)
 {
     if (g >= 0) return g < n_in ? in[g] : make_float2(0.f, 0.f);
@@ -93,69 +66,9 @@ __device__ __forceinline__ float2 virt(const float2* __restrict__ in, const floa
     return make_float2(0.f, 0.f);
 }
 
-template <int Q, int NW, int NV_>
-__device__ __forceinline__ void stage_load(float4 (&v)[NV_],
-                                           const float2* __restrict__ in,
-                                           const float2* __restrict__ hist,
-                                           int64_t chunk,
-                                           int64_t n_in,
-                                           int L,
-                                           bool in_aligned)
-{
-    using G = geom<Q, NW>;
-    constexpr int NT = G::NT;
-    const int64_t g0 = chunk * G::CHUNK - G::H;
-    const bool interior = in_aligned && g0 >= 0 && g0 + G::NS <= n_in;
-    if (interior) {
-        const float4* src = reinterpret_cast<const float4*>(in + g0);
-#pragma unroll
-        for (int u = 0; u < G::VPT; ++u) {
-            const int vi = threadIdx.x + NT * u;
-            if (G::NV % NT == 0 || vi < G::NV) {
-                const nf4 t = __builtin_nontemporal_load(reinterpret_cast<const nf4*>(src + vi));
-                v[u] = make_float4(t.x, t.y, t.z, t.w);
-            }
-        }
-    } else {
-#pragma unroll
-        for (int u = 0; u < G::VPT; ++u) {
-            const int vi = threadIdx.x + NT * u;
-            if (G::NV % NT == 0 || vi < G::NV) {
-                const float2 a = virt(in, hist, g0 + 2 * vi, n_in, L);
-                const float2 b = virt(in, hist, g0 + 2 * vi + 1, n_in, L);
-                v[u] = make_float4(a.x, a.y, b.x, b.y);
-            }
-        }
-    }
-}
 
-template <int Q, int NW, int NV_>
-__device__ __forceinline__ void stage_store(const float4 (&v)[NV_], unsigned char* lds)
-{
-    using G = geom<Q, NW>;
-    constexpr int NT = G::NT;
-#pragma unroll
-    for (int u = 0; u < G::VPT; ++u) {
-        const int vi = threadIdx.x + NT * u;
-        if (G::NV % NT == 0 || vi < G::NV) {
-            const int s = 2 * vi; // even local sample
-            const int off = (s >> 5) * 80 + (s & 31) * 2;
-            __bf16 r1a, r2a, r3a, i1a, i2a, i3a, r1b, r2b, r3b, i1b, i2b, i3b;
-            split3(v[u].x, r1a, r2a, r3a);
-            split3(v[u].y, i1a, i2a, i3a);
-            split3(v[u].z, r1b, r2b, r3b);
-            split3(v[u].w, i1b, i2b, i3b);
-            *reinterpret_cast<unsigned*>(lds + 0 * G::PLANE + off) = pack2(r1a, r1b);
-            *reinterpret_cast<unsigned*>(lds + 1 * G::PLANE + off) = pack2(r2a, r2b);
-            *reinterpret_cast<unsigned*>(lds + 2 * G::PLANE + off) = pack2(r3a, r3b);
-            *reinterpret_cast<unsigned*>(lds + 3 * G::PLANE + off) = pack2(i1a, i1b);
-            *reinterpret_cast<unsigned*>(lds + 4 * G::PLANE + off) = pack2(i2a, i2b);
-            *reinterpret_cast<unsigned*>(lds + 5 * G::PLANE + off) = pack2(i3a, i3b);
-        }
-    }
-}
 
-template <int Q, int NW, int PLANE_ = geom<Q, NW>::PLANE>
+template <int Q, int NW, int PLANE_>
 __device__ __forceinline__ void compute_tile(const unsigned char* lds,
                                              const bf16x8 (&B0)[2 * Q],
                                              const bf16x8 (&B1)[2 * Q],
@@ -258,82 +171,6 @@ __device__ __forceinline__ void compute_tile(const unsigned char* lds,
 #endif
             nf2 o = { re, im };
             __builtin_nontemporal_store(o, reinterpret_cast<nf2*>(out + n));
-        }
-    }
-}
-
-template <int Q, int NW, int DEPTH>
-__global__ __launch_bounds__(64 * NW, (NW >= 8 ? 2 : 2)) void k_fir_mfma(const float2* __restrict__ in,
-                                                                       const float2* __restrict__ hist_in,
-                                                                       float2* __restrict__ hist_out,
-                                                                       float2* __restrict__ out,
-                                                                       const bf16x8* __restrict__ frag, // [3][S][64]
-                                                                       int L,
-                                                                       int64_t n_out,
-                                                                       int in_aligned)
-{
-    using G = geom<Q, NW>;
-    constexpr int S = G::S;
-    constexpr int NT = G::NT;
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = tid >> 6;
-    const int64_t n_in = n_out;
-
-    if (blockIdx.x == 0) {
-        for (int j = tid; j < L - 1; j += NT) hist_out[j] = virt(in, hist_in, n_in - (L - 1) + j, n_in, L);
-    }
-
-    // Tap fragments for the whole launch.
-    bf16x8 B0[S], B1[S], B2[S];
-#pragma unroll
-    for (int st = 0; st < S; ++st) {
-        B0[st] = frag[(0 * S + st) * 64 + lane];
-        B1[st] = frag[(1 * S + st) * 64 + lane];
-        B2[st] = frag[(2 * S + st) * 64 + lane];
-    }
-
-    const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
-    const int64_t per = (nchunks + gridDim.x - 1) / gridDim.x;
-    const int64_t c_begin = (int64_t)blockIdx.x * per;
-    const int64_t c_end = c_begin + per < nchunks ? c_begin + per : nchunks;
-    if (c_begin >= c_end) return;
-
-    // A-fragment addressing: row rho = b + 16c; lane half h selects k offset 8h.
-    const int rho = lane & 31;
-    const int b = rho & 15;
-    const int c = rho >> 4;
-    const int h = lane >> 5;
-    const int a_base = c * 3 * G::PLANE + ((Q - 1) + 16 * wave + b) * 80 + 16 * h; // bytes, k-step 0
-    // Output addressing: C[row][col], col = lane&31 = phase, row = (reg&3) + 8(reg>>2) + 4h.
-    const int phase = lane & 31;
-    const bool al = in_aligned != 0;
-
-    float4 va[G::VPT];
-    float4 vb[G::VPT];
-    stage_load<Q, NW>(va, in, hist_in, c_begin, n_in, L, al);
-    if constexpr (DEPTH > 1) {
-        if (c_begin + 1 < c_end) stage_load<Q, NW>(vb, in, hist_in, c_begin + 1, n_in, L, al);
-    }
-
-    for (int64_t ch = c_begin; ch < c_end; ch += DEPTH) {
-        // chunk ch from va
-        if (ch != c_begin) __syncthreads(); // previous chunk's fragment reads are done
-        stage_store<Q, NW>(va, lds);
-        __syncthreads();
-        if (ch + DEPTH < c_end) stage_load<Q, NW>(va, in, hist_in, ch + DEPTH, n_in, L, al);
-        compute_tile<Q, NW>(lds, B0, B1, B2, a_base, ch * G::CHUNK + (int64_t)wave * TILE, h, phase, n_out, out);
-        if constexpr (DEPTH > 1) {
-            if (ch + 1 < c_end) {
-                __syncthreads();
-                stage_store<Q, NW>(vb, lds);
-                __syncthreads();
-                if (ch + 1 + DEPTH < c_end) stage_load<Q, NW>(vb, in, hist_in, ch + 1 + DEPTH, n_in, L, al);
-                compute_tile<Q, NW>(lds, B0, B1, B2, a_base, (ch + 1) * G::CHUNK + (int64_t)wave * TILE, h, phase, n_out,
-                                    out);
-            }
         }
     }
 }
@@ -562,205 +399,6 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma2(const float2* __restrict__
         if (ch <= c_last) step(va, vc, ch++);
         if (ch <= c_last) step(vb, va, ch);
     }
-}
-
-// ---- v6: ping-pong workgroup (two 4-wave groups, one wave of each per SIMD) ----------------
-// v2's two 256-thread workgroups per CU do identical work in lockstep, so both waves of a SIMD
-// split (VALU + ds_write) at the same time and the matrix pipe idles meanwhile: with no HBM
-// traffic at all the MFMA (~55 us) and LDS (~45 us) parts of a 2^25-sample launch simply add
-// up (ablation masks 14/15). Here one 512-thread workgroup per CU runs two groups in
-// alternating roles: in phase p group (p & 1) computes chunk p from LDS buffer p & 1 while the
-// other group copies that buffer's tail (the next halo) and splits chunk p + 1 into the other
-// buffer, then loads chunk p + 3 for its next split; one barrier per phase. Every SIMD always
-// hosts one computing wave, and the splitting wave fills the MFMA issue gaps.
-template <int Q>
-__device__ __forceinline__ void g_load_main(float4 (&v)[geom2<Q>::VPT], const float2* __restrict__ in,
-                                           const float2* __restrict__ hist, int64_t ch, int64_t n_in, int L,
-                                           bool in_aligned, int gt)
-{
-    using G = geom2<Q>;
-    const int64_t g0 = ch * G::CHUNK;
-#if NSH_FIR_ABLATE & 2
-    for (int u = 0; u < G::VPT; ++u) v[u] = make_float4((float)g0, (float)u, (float)gt, 1.f);
-    return;
-#endif
-    if (in_aligned && g0 + G::CHUNK <= n_in) {
-        const nf4* src = reinterpret_cast<const nf4*>(in + g0);
-#pragma unroll
-        for (int u = 0; u < G::VPT; ++u) {
-            const nf4 t = __builtin_nontemporal_load(src + gt + G::NT * u);
-            v[u] = make_float4(t.x, t.y, t.z, t.w);
-        }
-    } else {
-#pragma unroll
-        for (int u = 0; u < G::VPT; ++u) {
-            const int vi = gt + G::NT * u;
-            const float2 a = virt(in, hist, g0 + 2 * vi, n_in, L);
-            const float2 b = virt(in, hist, g0 + 2 * vi + 1, n_in, L);
-            v[u] = make_float4(a.x, a.y, b.x, b.y);
-        }
-    }
-}
-
-template <int Q>
-__device__ __forceinline__ void g_store_pair(unsigned char* buf, int s, float a_re, float b_re, float a_im, float b_im)
-{
-    using G = geom2<Q>;
-    const int off = (s >> 5) * 80 + (s & 31) * 2;
-    unsigned r1, r2, r3, i1, i2, i3;
-#if NSH_FIR_ABLATE & 4
-    r1 = r2 = r3 = __float_as_uint(a_re);
-    i1 = i2 = i3 = __float_as_uint(a_im);
-#else
-    split_pair(a_re, b_re, r1, r2, r3);
-    split_pair(a_im, b_im, i1, i2, i3);
-#endif
-    *reinterpret_cast<unsigned*>(buf + 0 * G::PLANE + off) = r1;
-    *reinterpret_cast<unsigned*>(buf + 1 * G::PLANE + off) = r2;
-    *reinterpret_cast<unsigned*>(buf + 2 * G::PLANE + off) = r3;
-    *reinterpret_cast<unsigned*>(buf + 3 * G::PLANE + off) = i1;
-    *reinterpret_cast<unsigned*>(buf + 4 * G::PLANE + off) = i2;
-    *reinterpret_cast<unsigned*>(buf + 5 * G::PLANE + off) = i3;
-}
-
-template <int Q>
-__device__ __forceinline__ void g_store_main(const float4 (&v)[geom2<Q>::VPT], unsigned char* buf, int gt)
-{
-    using G = geom2<Q>;
-#pragma unroll
-    for (int u = 0; u < G::VPT; ++u)
-        g_store_pair<Q>(buf, G::H + 2 * (gt + G::NT * u), v[u].x, v[u].z, v[u].y, v[u].w);
-}
-
-template <int Q>
-__device__ __forceinline__ void g_copy_halo(const unsigned char* cur, unsigned char* nxt, int gt)
-{
-    using G = geom2<Q>;
-    constexpr int PIECES = 6 * G::HR * 4;
-    if constexpr (PIECES > 0) {
-        for (int t = gt; t < PIECES; t += G::NT) {
-            const int plane = t / (G::HR * 4);
-            const int rem = t % (G::HR * 4);
-            const int row = rem >> 2, q16 = rem & 3;
-            const uint4 d = *reinterpret_cast<const uint4*>(cur + plane * G::PLANE + (G::NB - G::HR + row) * 80 + q16 * 16);
-            *reinterpret_cast<uint4*>(nxt + plane * G::PLANE + row * 80 + q16 * 16) = d;
-        }
-    }
-}
-
-template <int Q>
-__device__ __forceinline__ void g_load_store_halo(unsigned char* buf, const float2* __restrict__ in,
-                                                  const float2* __restrict__ hist, int64_t ch, int64_t n_in, int L, int gt)
-{
-    using G = geom2<Q>;
-    if constexpr (G::H > 0) {
-        const int64_t g0 = ch * G::CHUNK - G::H;
-        for (int p = gt; p < G::H / 2; p += G::NT) {
-            const float2 a = virt(in, hist, g0 + 2 * p, n_in, L);
-            const float2 b = virt(in, hist, g0 + 2 * p + 1, n_in, L);
-            g_store_pair<Q>(buf, 2 * p, a.x, b.x, a.y, b.y);
-        }
-    }
-}
-
-template <int Q>
-__global__ __launch_bounds__(512, 1) void k_fir_mfma6(const float2* __restrict__ in,
-                                                     const float2* __restrict__ hist_in,
-                                                     float2* __restrict__ hist_out,
-                                                     float2* __restrict__ out,
-                                                     const bf16x8* __restrict__ frag, // [3][S][64]
-                                                     int L,
-                                                     int64_t n_out,
-                                                     int in_aligned,
-                                                     int prio)
-{
-    using G = geom2<Q>;
-    constexpr int S = G::S;
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    const int tid = threadIdx.x;
-    const int grp = tid >> 8;                    // wave-uniform: waves 0-3 / 4-7
-    const int gt = tid & 255;
-    const int lane = tid & 63;
-    const int gwave = (tid >> 6) & 3;
-    const int64_t n_in = n_out;
-
-    if (blockIdx.x == 0) {
-        for (int j = tid; j < L - 1; j += 512) hist_out[j] = virt(in, hist_in, n_in - (L - 1) + j, n_in, L);
-    }
-
-    bf16x8 B0[S], B1[S], B2[S];
-#pragma unroll
-    for (int st = 0; st < S; ++st) {
-        B0[st] = frag[(0 * S + st) * 64 + lane];
-        B1[st] = frag[(1 * S + st) * 64 + lane];
-        B2[st] = frag[(2 * S + st) * 64 + lane];
-    }
-
-    const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
-    const int64_t per = (nchunks + gridDim.x - 1) / gridDim.x;
-    const int64_t c_begin = (int64_t)blockIdx.x * per;
-    const int64_t c_end = c_begin + per < nchunks ? c_begin + per : nchunks;
-    if (c_begin >= c_end) return;
-    const int64_t n = c_end - c_begin; // chunks of this workgroup, offsets 0 .. n-1
-    const bool al = in_aligned != 0;
-    auto chunk = [&](int64_t k) { return c_begin + (k < n ? k : n - 1); };
-
-    const int rho = lane & 31;
-    const int b = rho & 15;
-    const int c = rho >> 4;
-    const int h = lane >> 5;
-    const int a_base = c * 3 * G::PLANE + ((Q - 1) + 16 * gwave + b) * 80 + 16 * h;
-    const int phase = lane & 31;
-
-    // Group g splits offsets g, g+2, ... and computes the same offsets one phase later.
-    // Registers `v` always hold this group's next chunk to split.
-    float4 v[G::VPT];
-    if (grp == 0) {
-        g_load_store_halo<Q>(lds, in, hist_in, chunk(0), n_in, L, gt);
-        g_load_main<Q>(v, in, hist_in, chunk(0), n_in, L, al, gt);
-        g_store_main<Q>(v, lds, gt);
-        g_load_main<Q>(v, in, hist_in, chunk(2), n_in, L, al, gt);
-    } else {
-        g_load_main<Q>(v, in, hist_in, chunk(1), n_in, L, al, gt);
-    }
-    __syncthreads();
-
-    for (int64_t p = 0; p < n; ++p) {
-        unsigned char* cur = lds + (p & 1) * G::BUF;
-        unsigned char* nxt = lds + ((p & 1) ^ 1) * G::BUF;
-        if (grp == (int)(p & 1)) {
-            if (prio) __builtin_amdgcn_s_setprio(1);
-            compute_tile<Q, 4, G::PLANE>(cur, B0, B1, B2, a_base, (c_begin + p) * G::CHUNK + (int64_t)gwave * TILE, h,
-                                         phase, n_out, out);
-            if (prio) __builtin_amdgcn_s_setprio(0);
-        } else if (p + 1 < n) {
-            g_copy_halo<Q>(cur, nxt, gt);
-            g_store_main<Q>(v, nxt, gt);
-            g_load_main<Q>(v, in, hist_in, chunk(p + 3), n_in, L, al, gt);
-        }
-        __syncthreads();
-    }
-}
-
-template <int Q>
-int launch_v6(const nsh_fir_plan* p, const float2* in, const float2* hin, float2* hout, float2* out, int64_t n_out,
-              hipStream_t s, int prio)
-{
-    using G = geom2<Q>;
-    static bool attr_set = false;
-    if (!attr_set) {
-        NSH_CK(hipFuncSetAttribute((const void*)k_fir_mfma6<Q>, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
-        attr_set = true;
-    }
-    const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
-    int n_cu = 256;
-    (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, p->dev);
-    const unsigned grid = (unsigned)(nchunks < n_cu ? nchunks : n_cu);
-    const int aligned = ((uintptr_t)in % 16 == 0) ? 1 : 0;
-    hipLaunchKernelGGL(k_fir_mfma6<Q>, dim3(grid), dim3(512), G::LDS, s, in, hin, hout, out,
-                       (const bf16x8*)p->frag_dev, p->L, n_out, aligned, prio);
-    NSH_CK_LAUNCH("nsh_fir_ccf(mfma6)");
-    return 0;
 }
 
 // ---- v5: 16-phase blocks on v_mfma_f32_16x16x32_bf16 -------------------------------------
@@ -1431,27 +1069,6 @@ float bf16_to_f(unsigned short b)
     return f;
 }
 
-template <int Q, int NW, int DEPTH>
-int launch_v(const nsh_fir_plan* p, const float2* in, const float2* hin, float2* hout, float2* out, int64_t n_out,
-             hipStream_t s, int wg_per_cu)
-{
-    using G = geom<Q, NW>;
-    static bool attr_set = false;
-    if (!attr_set) {
-        NSH_CK(hipFuncSetAttribute((const void*)k_fir_mfma<Q, NW, DEPTH>, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
-        attr_set = true;
-    }
-    const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
-    int n_cu = 256;
-    (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, p->dev);
-    const int64_t max_grid = (int64_t)n_cu * wg_per_cu;
-    const unsigned grid = (unsigned)(nchunks < max_grid ? nchunks : max_grid);
-    const int aligned = ((uintptr_t)in % 16 == 0) ? 1 : 0;
-    hipLaunchKernelGGL((k_fir_mfma<Q, NW, DEPTH>), dim3(grid), dim3(G::NT), G::LDS, s, in, hin, hout, out,
-                       (const bf16x8*)p->frag_dev, p->L, n_out, aligned);
-    NSH_CK_LAUNCH("nsh_fir_ccf(mfma)");
-    return 0;
-}
 
 template <int Q, int DEPTH>
 int launch_v2(const nsh_fir_plan* p, const float2* in, const float2* hin, float2* hout, float2* out, int64_t n_out,
@@ -1480,15 +1097,8 @@ template <int Q>
 int launch_q(const nsh_fir_plan* p, const float2* in, const float2* hin, float2* hout, float2* out, int64_t n_out, hipStream_t s)
 {
     switch (p->variant) {
-    case 1: return launch_v<Q, 4, 1>(p, in, hin, hout, out, n_out, s, 2);
-    case 2: return launch_v<Q, 4, 2>(p, in, hin, hout, out, n_out, s, 2);
-    case 3: return launch_v<Q, 8, 1>(p, in, hin, hout, out, n_out, s, 2);
-    case 4: return launch_v<Q, 8, 2>(p, in, hin, hout, out, n_out, s, 2);
-    case 5: return launch_v<Q, 8, 2>(p, in, hin, hout, out, n_out, s, 1);
     case 6: return launch_v2<Q, 1>(p, in, hin, hout, out, n_out, s, 2);
     case 7: return launch_v2<Q, 2>(p, in, hin, hout, out, n_out, s, 2);
-    case 8: return launch_v6<Q>(p, in, hin, hout, out, n_out, s, 0);
-    case 9: return launch_v6<Q>(p, in, hin, hout, out, n_out, s, 1);
     default: return launch_v2<Q, 2>(p, in, hin, hout, out, n_out, s, 2);
     }
 }
