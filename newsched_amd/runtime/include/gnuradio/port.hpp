@@ -67,7 +67,8 @@ public:
     // Wake the threads owning every connected port.
     void notify_connected_ports(scheduler_message_sptr msg)
     {
-        for (auto& p : _connected_ports) p->push_message(msg);
+        for (auto& w : _connected_ports)
+            if (auto p = w.lock()) p->push_message(msg);
     }
 
     virtual void push_message(scheduler_message_sptr msg)
@@ -76,17 +77,30 @@ public:
         _parent_intf->push_message(std::move(msg));
     }
 
+    // Peers are held weakly: each port is owned by its node, and two connected ports holding
+    // each other strongly would keep both (and everything they reference) alive forever.
     void connect(sptr other)
     {
-        if (std::find(_connected_ports.begin(), _connected_ports.end(), other) == _connected_ports.end())
-            _connected_ports.push_back(std::move(other));
+        for (auto& w : _connected_ports)
+            if (w.lock() == other) return;
+        _connected_ports.push_back(other);
     }
     void disconnect(const sptr& other)
     {
-        _connected_ports.erase(std::remove(_connected_ports.begin(), _connected_ports.end(), other),
+        _connected_ports.erase(std::remove_if(_connected_ports.begin(), _connected_ports.end(),
+                                              [&](const std::weak_ptr<port_base>& w) {
+                                                  auto p = w.lock();
+                                                  return !p || p == other;
+                                              }),
                                _connected_ports.end());
     }
-    const std::vector<sptr>& connected_ports() const { return _connected_ports; }
+    std::vector<sptr> connected_ports() const
+    {
+        std::vector<sptr> r;
+        for (auto& w : _connected_ports)
+            if (auto p = w.lock()) r.push_back(std::move(p));
+        return r;
+    }
 
 protected:
     std::string _name;
@@ -99,7 +113,7 @@ protected:
     int _multiplicity;
     size_t _datasize = 0;
     size_t _itemsize = 0;
-    std::vector<sptr> _connected_ports;
+    std::vector<std::weak_ptr<port_base>> _connected_ports;
     neighbor_interface_sptr _parent_intf = nullptr;
 };
 
