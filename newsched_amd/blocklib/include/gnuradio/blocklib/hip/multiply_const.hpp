@@ -3,12 +3,14 @@
 // blocklib/cuda/multiply_const.hpp:8-45 + lib/multiply_const.cu:1-18 -- float only, and
 // its make() never stores k, Appendix A). Same per-product rounding as the CPU block.
 #pragma once
+#include <gnuradio/hip_fusion.hpp>
 #include <gnuradio/sync_block.hpp>
+#include <type_traits>
 
 namespace gr {
 namespace hip {
 template <class T>
-class multiply_const : public sync_block
+class multiply_const : public sync_block, public elementwise_cc
 {
 public:
     using sptr = std::shared_ptr<multiply_const>;
@@ -22,6 +24,15 @@ public:
     multiply_const(T k, size_t vlen) : sync_block("multiply_const (hip)"), d_k(k), d_vlen(vlen) {}
     work_return_code_t work(std::vector<block_work_input>& in, std::vector<block_work_output>& out) override;
     T k() const { return d_k; }
+    bool elementwise_stages(std::vector<gr_complex>& ks) const override
+    {
+        if constexpr (std::is_same_v<T, gr_complex>) {
+            ks.push_back(d_k);
+            return true;
+        } else {
+            return false;
+        }
+    }
 
 private:
     T d_k;
@@ -32,8 +43,9 @@ using multiply_const_ff = multiply_const<float>;
 
 // Fused chain of multiply_const_cc stages in one pass over HBM (BASELINE config C2):
 // identical results to the unfused chain (each stage's products rounded in order), 16 B
-// per sample of traffic instead of 16 B per stage.
-class multiply_const_chain_cc : public sync_block
+// per sample of traffic instead of 16 B per stage. scheduler_hip builds these itself from
+// chains of separate elementwise blocks (hip_fusion.hpp); no stages = a copy.
+class multiply_const_chain_cc : public sync_block, public elementwise_cc
 {
 public:
     using sptr = std::shared_ptr<multiply_const_chain_cc>;
@@ -49,6 +61,12 @@ public:
     {
     }
     work_return_code_t work(std::vector<block_work_input>& in, std::vector<block_work_output>& out) override;
+    const std::vector<gr_complex>& ks() const { return d_ks; }
+    bool elementwise_stages(std::vector<gr_complex>& ks) const override
+    {
+        ks.insert(ks.end(), d_ks.begin(), d_ks.end());
+        return true;
+    }
 
 private:
     std::vector<gr_complex> d_ks;

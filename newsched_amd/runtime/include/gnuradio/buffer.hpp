@@ -44,8 +44,13 @@ public:
     virtual void copy_items(std::shared_ptr<buffer> from, int nitems) = 0;
 
     // ---- tags (host side) ----
+    // The buffer whose tag list and counters these calls use: this one, or for a domain
+    // adapter the edge buffer it stands for (so tags cross in-process domain boundaries).
+    virtual buffer* tag_target() { return this; }
+
     virtual std::vector<tag_t> get_tags(unsigned int num_items)
     {
+        if (auto* t = tag_target(); t != this) return t->get_tags(num_items);
         std::lock_guard<std::mutex> g(_buf_mutex);
         std::vector<tag_t> r;
         for (auto& t : _tags)
@@ -54,13 +59,26 @@ public:
     }
     virtual void add_tags(unsigned int num_items, std::vector<tag_t>& tags)
     {
+        if (auto* t = tag_target(); t != this) return t->add_tags(num_items, tags);
         std::lock_guard<std::mutex> g(_buf_mutex);
         for (auto& t : tags)
             if (t.offset + num_items >= _total_written && t.offset < _total_written) _tags.push_back(t);
     }
-    const std::vector<tag_t>& tags() const { return _tags; }
+    bool has_tags()
+    {
+        auto* t = tag_target();
+        std::lock_guard<std::mutex> g(t->_buf_mutex);
+        return !t->_tags.empty();
+    }
+    std::vector<tag_t> tags()
+    {
+        auto* t = tag_target();
+        std::lock_guard<std::mutex> g(t->_buf_mutex);
+        return t->_tags;
+    }
     std::vector<tag_t> tags_in_window(uint64_t item_start, uint64_t item_end)
     {
+        if (auto* t = tag_target(); t != this) return t->tags_in_window(item_start, item_end);
         std::lock_guard<std::mutex> g(_buf_mutex);
         std::vector<tag_t> r;
         for (auto& t : _tags)
@@ -69,28 +87,26 @@ public:
     }
     void add_tag(tag_t tag)
     {
+        if (auto* t = tag_target(); t != this) return t->add_tag(std::move(tag));
         std::lock_guard<std::mutex> g(_buf_mutex);
         _tags.push_back(std::move(tag));
     }
     void add_tag(uint64_t offset, pmtf::pmt_sptr key, pmtf::pmt_sptr value, pmtf::pmt_sptr srcid = nullptr)
     {
-        std::lock_guard<std::mutex> g(_buf_mutex);
-        _tags.emplace_back(offset, std::move(key), std::move(value), std::move(srcid));
+        add_tag(tag_t(offset, std::move(key), std::move(value), std::move(srcid)));
     }
     // Copy tags of `in` that fall in the window this block is about to write.
     void propagate_tags(std::shared_ptr<buffer> in, int n_consumed)
     {
-        std::vector<tag_t> src;
-        {
-            std::lock_guard<std::mutex> g(in->_buf_mutex);
-            src = in->_tags;
-        }
+        if (auto* t = tag_target(); t != this) return t->propagate_tags(std::move(in), n_consumed);
+        std::vector<tag_t> src = in->tags();
         std::lock_guard<std::mutex> g(_buf_mutex);
         for (auto& t : src)
             if (t.offset >= _total_written && t.offset < _total_written + (uint64_t)n_consumed) _tags.push_back(t);
     }
     void prune_tags(int n_consumed)
     {
+        if (auto* t = tag_target(); t != this) return t->prune_tags(n_consumed);
         std::lock_guard<std::mutex> g(_buf_mutex);
         const uint64_t lim = _total_read + (uint64_t)n_consumed;
         _tags.erase(std::remove_if(_tags.begin(), _tags.end(), [lim](const tag_t& t) { return t.offset < lim; }),
@@ -100,8 +116,18 @@ public:
     void set_name(const std::string& n) { _name = n; }
     std::string name() const { return _name; }
     std::string type() const { return _type; }
-    uint64_t total_written() const { return _total_written; }
-    uint64_t total_read() const { return _total_read; }
+    // Absolute item counters (tag offsets are relative to these); a domain adapter reports
+    // those of the edge buffer it stands for.
+    uint64_t total_written()
+    {
+        auto* t = tag_target();
+        return t == this ? _total_written : t->total_written();
+    }
+    uint64_t total_read()
+    {
+        auto* t = tag_target();
+        return t == this ? _total_read : t->total_read();
+    }
 
     // ---- completion bookkeeping (drain-correct termination) ----
     // virtual so domain adapters can forward them to the buffer they stand for

@@ -66,6 +66,7 @@ public:
     void post_read(int n) override { target()->post_read(n); }
     void post_write(int n) override { target()->post_write(n); }
     void copy_items(buffer_sptr from, int n) override { target()->copy_items(std::move(from), n); }
+    gr::buffer* tag_target() override { return target().get(); }
     void set_writer_done() override { target()->set_writer_done(); }
     void set_reader_done() override { target()->set_reader_done(); }
     bool writer_done() const override { return const_cast<domain_adapter_direct*>(this)->target()->writer_done(); }

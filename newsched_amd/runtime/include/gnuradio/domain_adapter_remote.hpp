@@ -94,6 +94,8 @@ public:
     bool writer_done() const override;
     bool reader_done() const override;
     void reset_flags() override;
+    // Tags live on the LOCAL ring; they are not carried over the process boundary.
+    gr::buffer* tag_target() override { return _buffer ? _buffer.get() : this; }
 
     void buffer_ready() override; // connect, handshake, start the receive thread
 

@@ -1,0 +1,46 @@
+// Elementwise fusion for the GPU scheduler domain. Not in the reference (its blocks each
+// launch and sync per work() call, blocklib/cuda/lib/copy.cpp:49-58); here a device block
+// whose work() is a per-sample complex map y = x·k_1·…·k_m (copy: m = 0) says so by
+// implementing elementwise_cc, and scheduler_hip rewrites every maximal chain of such
+// blocks joined by device-to-device edges into ONE block that makes a single pass over HBM
+// (the same per-stage rounding, so results are bit-identical to the unfused chain).
+//
+// What fusion changes, observably: the chain's interior edges get no buffer and the
+// interior blocks' work() is not called (their nitems counters stay 0); the fused block
+// reads the head's input edge and writes the tail's output edge, whose port connections
+// are rewired to it. Tags pass through unchanged (every stage is 1:1 with the same
+// propagation policy; chains with mixed policies are not fused).
+#pragma once
+#include <gnuradio/flat_graph.hpp>
+#include <gnuradio/types.hpp>
+#include <vector>
+
+namespace gr {
+namespace hip {
+
+class elementwise_cc
+{
+public:
+    virtual ~elementwise_cc() = default;
+    // Append this block's stages (complex multipliers, applied in order) to `ks` and
+    // return true; return false if this instance is not a complex map (e.g. a float
+    // specialisation), which makes it a chain boundary.
+    virtual bool elementwise_stages(std::vector<gr_complex>& ks) const = 0;
+};
+
+struct fusion_result {
+    flat_graph_sptr graph;            // the rewritten partition (== input if nothing fused)
+    std::vector<block_sptr> fused;    // the blocks that replaced chains
+    std::vector<std::vector<block_sptr>> chains; // fused[i] replaced chains[i]
+};
+
+// Stages per fused block (the fused kernel's limit); longer chains become several blocks.
+constexpr size_t max_fused_stages = 16;
+
+// The pass (host logic only; touches no device). A chain is >= 2 elementwise_cc blocks,
+// each with one input and one output stream port, linked by edges that are the only edge
+// of their output port and carry no custom buffer or a hip_buffer of type D2D.
+fusion_result fuse_elementwise_cc(flat_graph_sptr fg);
+
+} // namespace hip
+} // namespace gr

@@ -630,6 +630,7 @@ void domain_adapter_remote::pump()
         if (!_buffer->read_info(ri) || ri.n_items <= 0) break;
         const int m = std::min(ri.n_items, _max_chunk);
         _ch->send_msg_with(remote::M_DATA, (uint64_t)m, [&] { _tr->send(*_ch, ri.ptr, (size_t)m * _isz); });
+        _buffer->prune_tags(m); // tags do not cross processes; drop them with their items
         _buffer->post_read(m);
         _moved.fetch_add((uint64_t)m);
     }

@@ -8,8 +8,14 @@
 // call, versus the reference's 32 KiB / 4096-sample chunks (scheduler_mt.hpp:22,
 // vmcircbuf.cpp:83). On flush the thread drains the stream before reporting, so the run
 // only completes when the device is idle. One scheduler_hip per GPU (device index).
+//
+// Before buffers are allocated, initialize() fuses every maximal chain of elementwise
+// device blocks (multiply_const_cc, copy, multiply_const_chain_cc joined by D2D edges)
+// into one block with one launch per work() call (gnuradio/hip_fusion.hpp). Results are
+// bit-identical; set_fusion(false) keeps every block and edge as connected.
 #pragma once
 #include <gnuradio/hip_buffer.hpp>
+#include <gnuradio/hip_fusion.hpp>
 #include <gnuradio/schedulers/mt/scheduler_mt.hpp>
 
 namespace gr {
@@ -29,13 +35,24 @@ public:
     int device() const { return _device; }
     void* stream() const { return _stream; }
 
+    void initialize(flat_graph_sptr fg, flowgraph_monitor_sptr fgmon,
+                    neighbor_interface_map block_sched_map = neighbor_interface_map()) override;
+    // Elementwise fusion on (default) or off; takes effect at the next initialize().
+    void set_fusion(bool on) { _fusion = on; }
+    bool fusion() const { return _fusion; }
+    // What the last initialize() fused: blocks that replaced chains, and the chains.
+    const hip::fusion_result& fusion_plan() const { return _plan; }
+
 protected:
     thread_hooks hooks_for_group(const block_group_properties&) override;
     std::vector<block_group_properties> plan_groups(flat_graph_sptr fg) override;
 
 private:
+    void release_fused();
     int _device;
     void* _stream = nullptr;
+    bool _fusion = true;
+    hip::fusion_result _plan;
 };
 
 } // namespace schedulers

@@ -153,7 +153,7 @@ std::map<nodeid_t, executor_iteration_status> graph_executor::run_one_iteration(
         for (size_t i = 0; i < in_ports.size(); ++i) {
             auto buf = win[i].buffer;
             const int consumed = std::max(win[i].n_consumed, 0);
-            if (!buf->tags().empty()) {
+            if (buf->has_tags()) {
                 const auto pol = b->tag_propagation_policy();
                 for (size_t o = 0; o < out_ports.size(); ++o)
                     if (pol == tag_propagation_policy_t::TPP_ALL_TO_ALL ||

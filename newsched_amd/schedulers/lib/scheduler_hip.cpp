@@ -19,10 +19,31 @@ scheduler_hip::~scheduler_hip()
 {
     for (auto& t : _threads) t->stop(); // threads use the stream: stop them first
     _threads.clear();
+    release_fused();
     if (_stream) {
         nsh_stream_sync(_stream);
         nsh_stream_destroy(_stream);
     }
+}
+
+void scheduler_hip::release_fused()
+{
+    // fused blocks are owned here; their ports point at this scheduler's threads
+    for (auto& f : _plan.fused)
+        for (auto& p : f->all_ports()) p->set_parent_intf(nullptr);
+    _plan = hip::fusion_result();
+}
+
+void scheduler_hip::initialize(flat_graph_sptr fg, flowgraph_monitor_sptr fgmon, neighbor_interface_map nbr)
+{
+    for (auto& t : _threads) t->stop();
+    _threads.clear();
+    release_fused();
+    if (_fusion) {
+        _plan = hip::fuse_elementwise_cc(fg);
+        fg = _plan.graph;
+    }
+    scheduler_mt::initialize(fg, fgmon, nbr);
 }
 
 std::vector<block_group_properties> scheduler_hip::plan_groups(flat_graph_sptr fg)

@@ -47,6 +47,7 @@ inline void fail(const char* file, int line, const std::string& what)
     do {                                                        \
         if (!(c)) qa::fail(__FILE__, __LINE__, #c);             \
     } while (0)
+#define EXPECT_FALSE(c) EXPECT_TRUE(!(c))
 #define EXPECT_EQ(a, b)                                                         \
     do {                                                                        \
         if (!((a) == (b))) qa::fail(__FILE__, __LINE__, #a " == " #b);          \

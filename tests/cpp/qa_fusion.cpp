@@ -1,0 +1,179 @@
+// The scheduler_hip elementwise-fusion pass (gnuradio/hip_fusion.hpp) as host logic: which
+// chains it finds, how it splits them, and how it rewires the graph and ports. No device is
+// touched (block constructors and the pass are host-only), so this runs in the CPU suite;
+// the fused flowgraphs' results are checked on the GPU in qa_hip_flowgraph.cpp.
+#include "qa.hpp"
+
+#include <algorithm>
+#include <gnuradio/blocklib/blocks/null_sink.hpp>
+#include <gnuradio/blocklib/blocks/vector_source.hpp>
+#include <gnuradio/blocklib/hip/arith.hpp>
+#include <gnuradio/blocklib/hip/copy.hpp>
+#include <gnuradio/blocklib/hip/multiply_const.hpp>
+#include <gnuradio/flowgraph.hpp>
+#include <gnuradio/hip_buffer.hpp>
+#include <gnuradio/hip_fusion.hpp>
+
+using namespace gr;
+using hip::multiply_const_cc;
+
+static gr_complex K(int i) { return gr_complex(1.0f + 0.25f * (float)i, -0.5f * (float)i); }
+
+static flat_graph_sptr flat(const flowgraph::sptr& fg) { return flat_graph::make_flat(fg); }
+
+static bool connected(const port_sptr& a, const port_sptr& b)
+{
+    auto v = a->connected_ports();
+    return std::find(v.begin(), v.end(), b) != v.end();
+}
+
+static std::vector<gr_complex> fused_ks(const block_sptr& b)
+{
+    return std::dynamic_pointer_cast<hip::multiply_const_chain_cc>(b)->ks();
+}
+
+// src -> m0 -> m1 -> copy -> m2 -[D2H]-> sink: one chain of four blocks, three stages
+TEST(Fusion, LinearChainRewired)
+{
+    auto src = blocks::vector_source_c::make(std::vector<gr_complex>(16));
+    auto m0 = multiply_const_cc::make(K(0));
+    auto m1 = multiply_const_cc::make(K(1));
+    auto cp = hip::copy::make(1);
+    auto m2 = multiply_const_cc::make(K(2));
+    auto snk = blocks::null_sink::make(sizeof(gr_complex));
+    auto fg = flowgraph::make();
+    fg->connect(src, 0, m0, 0)->set_custom_buffer(HIP_BUFFER_ARGS_H2D);
+    fg->connect(m0, 0, m1, 0);
+    fg->connect(m1, 0, cp, 0)->set_custom_buffer(HIP_BUFFER_ARGS_D2D);
+    fg->connect(cp, 0, m2, 0);
+    fg->connect(m2, 0, snk, 0)->set_custom_buffer(HIP_BUFFER_ARGS_D2H);
+    // an in-process domain crossing keeps the original port pair linked outside the
+    // partition graph: that link must move to the fused block too
+    auto remote = blocks::null_sink::make(sizeof(gr_complex));
+    auto xin = remote->input_stream_ports()[0];
+    m2->output_stream_ports()[0]->connect(xin);
+    xin->connect(m2->output_stream_ports()[0]);
+    auto r = hip::fuse_elementwise_cc(flat(fg));
+    ASSERT_TRUE(r.fused.size() == 1u);
+    EXPECT_TRUE(r.chains[0].size() == 4u);
+    EXPECT_TRUE(connected(xin, r.fused[0]->output_stream_ports()[0]));
+    EXPECT_TRUE(connected(r.fused[0]->output_stream_ports()[0], xin));
+    EXPECT_FALSE(connected(xin, m2->output_stream_ports()[0]));
+    EXPECT_TRUE((fused_ks(r.fused[0]) == std::vector<gr_complex>{ K(0), K(1), K(2) }));
+    auto& e = r.graph->edges();
+    ASSERT_TRUE(e.size() == 2u);
+    auto f = r.fused[0];
+    auto fin = f->input_stream_ports()[0], fout = f->output_stream_ports()[0];
+    auto sout = src->output_stream_ports()[0], kin = snk->input_stream_ports()[0];
+    EXPECT_TRUE(e[0]->src().node() == src && e[0]->dst().port() == fin);
+    EXPECT_TRUE(e[1]->src().port() == fout && e[1]->dst().node() == snk);
+    // custom buffers of the boundary edges carried over
+    auto p0 = std::dynamic_pointer_cast<hip_buffer_properties>(e[0]->buf_properties());
+    auto p1 = std::dynamic_pointer_cast<hip_buffer_properties>(e[1]->buf_properties());
+    EXPECT_TRUE(p0 && p0->buffer_type() == hip_buffer_type::H2D);
+    EXPECT_TRUE(p1 && p1->buffer_type() == hip_buffer_type::D2H);
+    // port notifications now go to the fused block, and the chain is detached
+    EXPECT_TRUE(connected(sout, fin) && connected(fin, sout));
+    EXPECT_TRUE(connected(kin, fout) && connected(fout, kin));
+    EXPECT_FALSE(connected(sout, m0->input_stream_ports()[0]));
+    EXPECT_TRUE(m1->output_stream_ports()[0]->connected_ports().empty());
+    auto blocks = r.graph->calc_used_blocks();
+    EXPECT_TRUE(blocks.size() == 3u);
+}
+
+// Fan-out ends a chain: m0 -> {m1, m2}; m1 -> m3 -> sink0; m2 -> sink1
+TEST(Fusion, FanOutIsABoundary)
+{
+    auto src = blocks::vector_source_c::make(std::vector<gr_complex>(16));
+    std::vector<multiply_const_cc::sptr> m;
+    for (int i = 0; i < 4; ++i) m.push_back(multiply_const_cc::make(K(i)));
+    auto s0 = blocks::null_sink::make(sizeof(gr_complex));
+    auto s1 = blocks::null_sink::make(sizeof(gr_complex));
+    auto fg = flowgraph::make();
+    fg->connect(src, 0, m[0], 0);
+    fg->connect(m[0], 0, m[1], 0);
+    fg->connect(m[0], 0, m[2], 0);
+    fg->connect(m[1], 0, m[3], 0);
+    fg->connect(m[3], 0, s0, 0);
+    fg->connect(m[2], 0, s1, 0);
+    auto r = hip::fuse_elementwise_cc(flat(fg));
+    ASSERT_TRUE(r.fused.size() == 1u);
+    EXPECT_TRUE(r.chains[0].size() == 2u && r.chains[0][0] == m[1] && r.chains[0][1] == m[3]);
+    EXPECT_TRUE((fused_ks(r.fused[0]) == std::vector<gr_complex>{ K(1), K(3) }));
+    EXPECT_TRUE(r.graph->edges().size() == 5u); // src->m0, m0->F, m0->m2, F->s0, m2->s1
+    EXPECT_TRUE(connected(m[0]->output_stream_ports()[0], r.fused[0]->input_stream_ports()[0]));
+    EXPECT_TRUE(connected(m[0]->output_stream_ports()[0], m[2]->input_stream_ports()[0]));
+}
+
+// Host-visible interior edges, float blocks, non-elementwise blocks and mixed tag policies
+// are boundaries.
+TEST(Fusion, Boundaries)
+{
+    auto src = blocks::vector_source_c::make(std::vector<gr_complex>(16));
+    auto a = multiply_const_cc::make(K(0));
+    auto b = multiply_const_cc::make(K(1)); // a -[D2H]-> b: not fused
+    auto c = multiply_const_cc::make(K(2));
+    auto add = hip::add_cc::make(1);       // not elementwise_cc
+    auto d = multiply_const_cc::make(K(3));
+    auto e = multiply_const_cc::make(K(4)); // other tag policy
+    auto snk = blocks::null_sink::make(sizeof(gr_complex));
+    e->set_tag_propagation_policy(tag_propagation_policy_t::TPP_DONT);
+    auto fg = flowgraph::make();
+    fg->connect(src, 0, a, 0);
+    fg->connect(a, 0, b, 0)->set_custom_buffer(HIP_BUFFER_ARGS_D2H);
+    fg->connect(b, 0, c, 0); // b, c fuse
+    fg->connect(c, 0, add, 0);
+    fg->connect(add, 0, d, 0);
+    fg->connect(d, 0, e, 0);
+    fg->connect(e, 0, snk, 0);
+    auto r = hip::fuse_elementwise_cc(flat(fg));
+    ASSERT_TRUE(r.fused.size() == 1u);
+    EXPECT_TRUE(r.chains[0].size() == 2u && r.chains[0][0] == b && r.chains[0][1] == c);
+
+    auto fsrc = blocks::vector_source_f::make(std::vector<float>(16));
+    auto f1 = hip::multiply_const_ff::make(2.0f);
+    auto f2 = hip::multiply_const_ff::make(3.0f);
+    auto fsnk = blocks::null_sink::make(sizeof(float));
+    auto fg2 = flowgraph::make();
+    fg2->connect(fsrc, 0, f1, 0);
+    fg2->connect(f1, 0, f2, 0);
+    fg2->connect(f2, 0, fsnk, 0);
+    auto r2 = hip::fuse_elementwise_cc(flat(fg2));
+    EXPECT_TRUE(r2.fused.empty());
+    EXPECT_TRUE(r2.graph->edges().size() == 3u);
+}
+
+// Long chains are cut at the fused kernel's 16-stage limit (the reference's
+// BasicBlockGrouping builds chains of up to 128 multiply_const blocks).
+TEST(Fusion, LongChainsSplitAtStageLimit)
+{
+    auto src = blocks::vector_source_c::make(std::vector<gr_complex>(16));
+    auto snk = blocks::null_sink::make(sizeof(gr_complex));
+    auto fg = flowgraph::make();
+    // a 10-stage hand-fused block, then 30 single stages with a copy in the middle
+    std::vector<gr_complex> ten;
+    for (int i = 0; i < 10; ++i) ten.push_back(K(i));
+    block_sptr prev = hip::multiply_const_chain_cc::make(ten);
+    fg->connect(src, 0, prev, 0);
+    for (int i = 0; i < 31; ++i) {
+        block_sptr nb = i == 15 ? block_sptr(hip::copy::make(1)) : block_sptr(multiply_const_cc::make(K(i)));
+        fg->connect(prev, 0, nb, 0);
+        prev = nb;
+    }
+    fg->connect(prev, 0, snk, 0);
+    auto r = hip::fuse_elementwise_cc(flat(fg));
+    // stages: 10 + 30 = 40 -> 16 (chain10 + 6), 16 (9 singles, the copy, 6 singles... ), rest
+    size_t total = 0, blocks_total = 0;
+    for (size_t i = 0; i < r.fused.size(); ++i) {
+        EXPECT_TRUE(fused_ks(r.fused[i]).size() <= hip::max_fused_stages);
+        total += fused_ks(r.fused[i]).size();
+        blocks_total += r.chains[i].size();
+    }
+    EXPECT_TRUE(total == 40u);
+    EXPECT_TRUE(blocks_total == 32u);
+    EXPECT_TRUE(r.fused.size() == 3u);
+    EXPECT_TRUE(fused_ks(r.fused[0]).size() == 16u && r.chains[0].size() == 7u);
+    // the fused blocks form one path src -> F0 -> F1 -> F2 -> snk
+    EXPECT_TRUE(r.graph->edges().size() == 4u);
+    EXPECT_TRUE(r.graph->calc_used_blocks().size() == 5u);
+}

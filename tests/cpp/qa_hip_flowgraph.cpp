@@ -2,6 +2,8 @@
 // blocks -> graph_executor -> work() -> libnsh_hip.so, with hip_buffer edges.
 //   CudaCopy{Basic,MultiThreaded}  restate schedulers/mt/test/cuda/qa_scheduler_mt_cuda_copy.cpp:20-86
 //                                  (H2D -> copy -> D2D -> copy -> D2H, exact equality)
+//   Fusion*                        scheduler_hip's elementwise fusion (bit-identical on/off;
+//                                  BasicBlockGrouping's 128-block identity chain restated)
 //   the others cover BASELINE configs C2-C5 in the GPU scheduler domain against in-test
 //   CPU references (bit-exact where the arithmetic is the same formula; 1e-5 norm-wise
 //   for FIR/FFT), restart, and cross-thread device edges (event ordering).
@@ -99,6 +101,9 @@ TEST(HipDomain, DirectFirBitExactAcrossRuns)
 
 TEST(HipDomain, MultiplyChainC2)
 {
+    // variant 0: one hand-built multiply_const_chain_cc; 1: four multiply_const_cc blocks,
+    // fused by scheduler_hip; 2: the same four blocks with fusion off (every edge in HBM).
+    // All bit-identical to the per-stage product.
     const size_t n = 1u << 22;
     const std::vector<gr_complex> ks = { std::polar(1.0f, 0.1f), std::polar(1.0f, 0.2f), std::polar(1.0f, 0.3f),
                                          std::polar(1.0f, 0.4f) };
@@ -106,11 +111,11 @@ TEST(HipDomain, MultiplyChainC2)
     std::vector<gr_complex> ref(x);
     for (auto k : ks)
         for (auto& v : ref) v = cmul(v, k);
-    for (int fused = 0; fused < 2; ++fused) {
+    for (int variant = 0; variant < 3; ++variant) {
         auto src = hip::synth_source::make(0, n);
         auto snk = blocks::vector_sink_c::make(1, n);
         auto fg = flowgraph::make();
-        if (fused) {
+        if (variant == 0) {
             auto ch = hip::multiply_const_chain_cc::make(ks);
             fg->connect(src, 0, ch, 0);
             fg->connect(ch, 0, snk, 0)->set_custom_buffer(HIP_BUFFER_ARGS_D2H);
@@ -121,10 +126,85 @@ TEST(HipDomain, MultiplyChainC2)
             for (size_t i = 1; i < m.size(); ++i) fg->connect(m[i - 1], 0, m[i], 0);
             fg->connect(m.back(), 0, snk, 0)->set_custom_buffer(HIP_BUFFER_ARGS_D2H);
         }
-        fg->set_scheduler(schedulers::scheduler_hip::make("hip", 0, 4u << 20));
+        auto sched = schedulers::scheduler_hip::make("hip", 0, 4u << 20);
+        sched->set_fusion(variant != 2);
+        fg->set_scheduler(sched);
         fg->validate();
+        EXPECT_EQ(sched->fusion_plan().fused.size(), variant == 1 ? 1u : 0u);
         fg->run();
         EXPECT_TRUE(snk->data() == ref);
+        if (variant == 1) { // restart through the fused graph
+            fg->run();
+            EXPECT_TRUE(snk->data() == ref);
+        }
+    }
+}
+
+// Reference BasicBlockGrouping (schedulers/mt/test/qa_block_grouping.cpp:15-66) in the GPU
+// domain: 128 chained multiply_const(1) blocks are the identity. scheduler_hip fuses them
+// into 8 blocks of 16 stages (the fused kernel's limit).
+TEST(HipDomain, Fusion128BlockIdentityChain)
+{
+    const size_t n = 1000003;
+    auto src = hip::synth_source::make(0, n);
+    auto snk = blocks::vector_sink_c::make(1, n);
+    auto fg = flowgraph::make();
+    block_sptr prev = src;
+    for (int i = 0; i < 128; ++i) {
+        auto m = hip::multiply_const_cc::make(gr_complex(1.0f, 0.0f));
+        fg->connect(prev, 0, m, 0);
+        prev = m;
+    }
+    fg->connect(prev, 0, snk, 0)->set_custom_buffer(HIP_BUFFER_ARGS_D2H);
+    auto sched = schedulers::scheduler_hip::make("hip", 0, 1u << 20);
+    fg->set_scheduler(sched);
+    fg->validate();
+    EXPECT_EQ(sched->fusion_plan().fused.size(), 8u);
+    fg->run();
+    EXPECT_TRUE(snk->data() == synth(n));
+}
+
+// A fused chain whose ends are domain crossings (CPU -[H2D]-> m1 -> copy -> m2 -[D2H]-> CPU)
+// and a fan-out inside the GPU domain: results identical with fusion on and off.
+TEST(HipDomain, FusionAcrossDomainsAndFanOut)
+{
+    const size_t n = 400000;
+    auto x = synth(n, 4242);
+    const gr_complex k1(0.5f, -0.25f), k2(-1.5f, 0.75f), k3(0.0f, 1.0f);
+    std::vector<gr_complex> r1(x), r2(x);
+    for (auto& v : r1) v = cmul(cmul(v, k1), k2);
+    for (auto& v : r2) v = cmul(cmul(v, k1), k3);
+    for (int fuse = 1; fuse >= 0; --fuse) {
+        auto src = blocks::vector_source_c::make(x);
+        auto m1 = hip::multiply_const_cc::make(k1);
+        auto cp = hip::copy::make(1);
+        auto m2 = hip::multiply_const_cc::make(k2);
+        auto m3 = hip::multiply_const_cc::make(k3);
+        auto cp3 = hip::copy::make(1);
+        auto s1 = blocks::vector_sink_c::make(1, n);
+        auto s2 = blocks::vector_sink_c::make(1, n);
+        auto fg = flowgraph::make();
+        fg->connect(src, 0, m1, 0)->set_custom_buffer(HIP_BUFFER_ARGS_H2D);
+        fg->connect(m1, 0, cp, 0);  // m1 fans out: a chain boundary
+        fg->connect(m1, 0, m3, 0);
+        fg->connect(cp, 0, m2, 0);  // cp -> m2 fused
+        fg->connect(m3, 0, cp3, 0); // m3 -> cp3 fused
+        fg->connect(m2, 0, s1, 0)->set_custom_buffer(HIP_BUFFER_ARGS_D2H);
+        fg->connect(cp3, 0, s2, 0)->set_custom_buffer(HIP_BUFFER_ARGS_D2H);
+        auto cpu = schedulers::scheduler_mt::make("cpu", 1u << 16);
+        auto gpu = schedulers::scheduler_hip::make("gpu", 0, 1u << 18);
+        gpu->set_fusion(fuse);
+        fg->add_scheduler(cpu);
+        fg->add_scheduler(gpu);
+        auto da = domain_adapter_direct_conf::make(buffer_preference_t::DOWNSTREAM);
+        domain_conf_vec dc{ domain_conf(cpu, { src, s1, s2 }, da), domain_conf(gpu, { m1, cp, m2, m3, cp3 }, da) };
+        fg->partition(dc);
+        EXPECT_EQ(gpu->fusion_plan().fused.size(), fuse ? 2u : 0u);
+        for (int run = 0; run < 2; ++run) {
+            fg->run();
+            EXPECT_TRUE(s1->data() == r1);
+            EXPECT_TRUE(s2->data() == r2);
+        }
     }
 }
 

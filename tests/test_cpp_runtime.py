@@ -34,12 +34,19 @@ def test_hip_flowgraphs():
 
 
 def test_tags_reference_counts():
-    """Reference schedulers/mt/test/qa_tags.cpp OneToOne/t1/t2/t3 with its expected counts."""
+    """Reference schedulers/mt/test/qa_tags.cpp OneToOne/t1/t2/t3 with its expected counts, plus
+    tags across an in-process domain boundary."""
     out = run("qa_tags", 300, "SchedulerMTTags")
-    assert "4 test(s), 0 failure(s)" in out
+    assert "5 test(s), 0 failure(s)" in out
 
 
 @pytest.mark.gpu
 def test_tags_through_device_edges():
     out = run("qa_tags", 300, "DeviceTags")
-    assert "1 test(s), 0 failure(s)" in out
+    assert "2 test(s), 0 failure(s)" in out
+
+
+def test_fusion_pass_graph_rewrite():
+    """scheduler_hip's elementwise-fusion pass as host logic (no device touched)."""
+    out = run("qa_fusion", 120)
+    assert "4 test(s), 0 failure(s)" in out

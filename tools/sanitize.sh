@@ -25,7 +25,7 @@ done
 wait
 g++ -shared $SAN -pthread -o "$OUT/libnewsched.so" "${objs[@]}" -Lnewsched_amd/lib -lnsh_hip \
     -Wl,-rpath,"$PWD/newsched_amd/lib"
-for t in qa_scheduler_mt qa_tags qa_remote_edge; do
+for t in qa_scheduler_mt qa_tags qa_remote_edge qa_fusion; do
     g++ $FLAGS -Itests/cpp -o "$OUT/$t" "tests/cpp/$t.cpp" -L"$OUT" -lnewsched \
         -Lnewsched_amd/lib -lnsh_hip -Wl,-rpath,"$OUT:$PWD/newsched_amd/lib" &
 done
@@ -35,6 +35,7 @@ export UBSAN_OPTIONS=print_stacktrace=1
 rc=0
 timeout -k 5 600 "$OUT/qa_scheduler_mt" >"$OUT/sched.log" 2>&1 || { echo "qa_scheduler_mt FAILED"; rc=1; }
 timeout -k 5 300 "$OUT/qa_tags" SchedulerMTTags >"$OUT/tags.log" 2>&1 || { echo "qa_tags FAILED"; rc=1; }
+timeout -k 5 120 "$OUT/qa_fusion" >"$OUT/fusion.log" 2>&1 || { echo "qa_fusion FAILED"; rc=1; }
 port=$((30000 + RANDOM % 20000))
 for c in RemoteCpu.ChainRestart RemoteCpu.TwoCrossingsBothWays RemoteCpu.ReaderFinishesFirst; do
     QA_RANK=0 QA_PORT=$port timeout -k 5 120 "$OUT/qa_remote_edge" "$c" >"$OUT/remote0.log" 2>&1 &
