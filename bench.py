@@ -55,7 +55,8 @@ def cpu_model():
 def load_pmc_traffic(kernel, samples_per_launch):
     """HBM bytes per launch from the committed PMC summary (profiles/pmc_fir.json, produced
     by tools/pmc_summary.py from separate rocprofv3 --pmc passes, gfx950 FETCH_SIZE x2
-    correction applied there), scaled to this launch size. kernel: "fir_mfma" | "fir_direct"."""
+    correction applied there), scaled to this launch size. kernel: the template name the
+    plan reports (nsh_fir_plan_kernel), e.g. "k_fir_mfma8<5>"."""
     p = os.path.join(ROOT, "profiles", "pmc_fir.json")
     try:
         with open(p) as f:
@@ -71,7 +72,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--log2n", type=int, default=28)
-    ap.add_argument("--algo", default="auto", choices=["auto", "mfma", "mfma16", "direct"])
+    ap.add_argument("--algo", default="auto", choices=["auto", "mfma", "mfma_x3", "mfma16", "direct"])
     ap.add_argument("--out-buf-mib", type=int, default=2048, help="FIR output hip_buffer (default: one launch per 2^28-sample step)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-log2n", type=int, default=28, help="CPU baseline sample (default: the full stream)")
@@ -94,7 +95,8 @@ def main():
     from newsched_amd import nsh, nsr
     from oracle import oracle as orc  # checker only: tail parity + CPU-baseline inputs
 
-    algo = {"auto": nsh.FIR_AUTO, "mfma": nsh.FIR_MFMA, "mfma16": nsh.FIR_MFMA16, "direct": nsh.FIR_DIRECT}[a.algo]
+    algo = {"auto": nsh.FIR_AUTO, "mfma": nsh.FIR_MFMA, "mfma16": nsh.FIR_MFMA16, "mfma_x3": nsh.FIR_MFMA_BF16X3,
+            "direct": nsh.FIR_DIRECT}[a.algo]
     n = 1 << a.log2n
     taps = firwin127()
     first = rank * n  # this rank's time shard
@@ -124,7 +126,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     st = fb.stats()
-    algo_used = {1: "direct", 2: "mfma", 3: "mfma16"}.get(st["algo"], str(st["algo"]))
+    algo_used = {1: "direct", 2: "mfma", 3: "mfma16", 4: "mfma_x3"}.get(st["algo"], str(st["algo"]))
+    kernel = st["kernel"]
     timed_launches = st["launches"] - launches0
     launches_per_run = timed_launches / a.steps
     per_launch_samples = samples / timed_launches
@@ -171,7 +174,7 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": None,
-            "kernel": {"mfma": "k_fir_mfma2<5,2>", "mfma16": "k_fir_mfma5<9,1>"}.get(algo_used, "k_fir_direct<1,8>"),
+            "kernel": kernel,
             "avg_launch_us": round(avg_launch_ms * 1e3, 2),
             "algorithmic_bytes_per_launch": int(BYTES_PER_SAMPLE * per_launch_samples),
             "kernel_gflops": round(FLOP_PER_SAMPLE * per_launch_samples / (avg_launch_ms * 1e-3) / 1e9, 1),
@@ -179,7 +182,7 @@ def main():
         "parity": {"check": "last 4096 outputs of the last step vs oracle (double accumulation)",
                    "max_abs_err": err, "scale": scale, "ok": bool(ok)},
     }
-    tr = load_pmc_traffic("fir_" + algo_used, per_launch_samples)
+    tr = load_pmc_traffic(kernel, per_launch_samples)
     if tr is not None:
         out["roofline"]["traffic"] = int(tr)
 

@@ -101,14 +101,17 @@ int nsh_synth_cf32(float* out, int64_t n, uint64_t first_index, uint64_t seed, v
  *   hist_in  : ntaps-1 samples that precede in[0] (device; zeros at stream start)
  *   hist_out : receives the ntaps-1 samples that precede the NEXT call's in[0]
  *              (must not alias hist_in -- ping-pong two buffers)
- * algo: NSH_FIR_AUTO picks by measurement, NSH_FIR_DIRECT is the fp32 VALU
- * direct form, NSH_FIR_MFMA is the bf16x3 split-precision Toeplitz MFMA form on 32-sample
- * blocks (decim 1, ntaps <= 161), NSH_FIR_MFMA16 the same on 16-sample blocks
- * (v_mfma_f32_16x16x32_bf16, decim 1, ntaps <= 145). */
-enum nsh_fir_algo { NSH_FIR_AUTO = 0, NSH_FIR_DIRECT = 1, NSH_FIR_MFMA = 2, NSH_FIR_MFMA16 = 3 };
+ * algo: NSH_FIR_AUTO picks by measurement; NSH_FIR_DIRECT is the fp32 VALU
+ * direct form; NSH_FIR_MFMA is the split-precision Toeplitz form on the matrix cores
+ * (decim 1: 32-sample blocks, ntaps <= 161, per-chunk scaled fp16x2 with three products,
+ * or bf16x3 with six when the taps span more than 2^28; decim 2/4: polyphase bf16x3);
+ * NSH_FIR_MFMA16 is the bf16x3 form on 16-sample blocks (decim 1, ntaps <= 145);
+ * NSH_FIR_MFMA_BF16X3 is NSH_FIR_MFMA with the bf16x3 kernel forced for decim 1. */
+enum nsh_fir_algo { NSH_FIR_AUTO = 0, NSH_FIR_DIRECT = 1, NSH_FIR_MFMA = 2, NSH_FIR_MFMA16 = 3, NSH_FIR_MFMA_BF16X3 = 4 };
 int nsh_fir_plan_create(int dev, const float* taps_host, int ntaps, int decim, int algo, void** plan);
 int nsh_fir_plan_destroy(void* plan);
 int nsh_fir_plan_algo(void* plan);          /* the algorithm AUTO resolved to */
+const char* nsh_fir_plan_kernel(void* plan); /* the kernel nsh_fir_ccf launches, e.g. "k_fir_mfma8<5>" */
 int nsh_fir_ccf(void* plan, const float* in, const float* hist_in, float* hist_out,
                 float* out, int64_t n_out, void* stream);
 

@@ -28,6 +28,7 @@ public:
     work_return_code_t work(std::vector<block_work_input>& in, std::vector<block_work_output>& out) override;
     int decimation() const { return _decim; }
     int algo() const; // resolved algorithm (after start())
+    std::string kernel() const; // the kernel its work() launches (after start())
     uint64_t launches() const { return _launches; }
 
     // History loaded at start() instead of zeros: the ntaps-1 samples that precede this

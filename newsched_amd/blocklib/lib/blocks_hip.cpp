@@ -111,6 +111,7 @@ void fir_filter_ccf::release()
 }
 
 int fir_filter_ccf::algo() const { return _plan ? nsh_fir_plan_algo(_plan) : _algo; }
+std::string fir_filter_ccf::kernel() const { return _plan ? nsh_fir_plan_kernel(_plan) : std::string(); }
 
 bool fir_filter_ccf::start()
 {

@@ -132,6 +132,14 @@ int nsr_fir_bench_stats(void* handle, double* kernel_ms, uint64_t* launches, uin
     });
 }
 
+const char* nsr_fir_bench_kernel(void* handle)
+{
+    static thread_local std::string name;
+    name.clear();
+    (void)guarded([&] { name = static_cast<fir_bench*>(handle)->fir->kernel(); });
+    return name.c_str();
+}
+
 int nsr_fir_bench_tail(void* handle, int64_t count, float* out_host)
 {
     return guarded([&] {

@@ -14,12 +14,14 @@
 //    staged samples; taps come from the scalar cache (s_load, uniform index). LDS rows
 //    are padded by one sample every R*D samples so the per-lane ds_read_b64 of the window
 //    is bank-conflict-free. Exact fp32 products, fp32 accumulation in tap order.
-//  * MFMA / MFMA16 -- bf16x3 split-precision Toeplitz MFMA on 32- / 16-sample blocks
-//    (nsh_fir_mfma.hip), decim 1.
+//  * MFMA / MFMA16 / MFMA_BF16X3 -- split-precision Toeplitz MFMA (nsh_fir_mfma.hip):
+//    decim 1 on 32-sample blocks as scaled fp16x2 (default) or bf16x3, on 16-sample blocks
+//    as bf16x3; decim 2 and 4 as a polyphase bf16x3 form.
 #include "nsh_common.hpp"
 
 #include <algorithm>
 #include <cmath>
+#include <string>
 #include <vector>
 
 #include "nsh_fir_plan.hpp"
@@ -160,12 +162,16 @@ int nsh_fir_plan_create(int dev, const float* taps_host, int ntaps, int decim, i
         delete p;
         return nsh::fail(e, "nsh_fir_plan_create: taps upload");
     }
-    if (algo < NSH_FIR_AUTO || algo > NSH_FIR_MFMA16) {
+    if (algo < NSH_FIR_AUTO || algo > NSH_FIR_MFMA_BF16X3) {
         (void)hipFree(p->taps_dev);
         delete p;
         return nsh::fail_msg("nsh_fir_plan_create: unknown algorithm");
     }
     int resolved = algo;
+    if (algo == NSH_FIR_MFMA_BF16X3) {
+        resolved = NSH_FIR_MFMA;
+        p->force_x3 = true;
+    }
     if (algo == NSH_FIR_AUTO) resolved = nsh_fir_mfma_supported(p) ? NSH_FIR_MFMA : NSH_FIR_DIRECT;
     if (resolved == NSH_FIR_MFMA16 && !nsh_fir_mfma16_supported(p)) {
         (void)hipFree(p->taps_dev);
@@ -186,7 +192,13 @@ int nsh_fir_plan_create(int dev, const float* taps_host, int ntaps, int decim, i
             return rc;
         }
     }
-    p->algo = resolved;
+    p->algo = p->force_x3 ? NSH_FIR_MFMA_BF16X3 : resolved;
+    if (resolved == NSH_FIR_DIRECT) {
+        static const int R[9] = { 0, 8, 8, 0, 4, 0, 0, 0, 2 };
+        p->kernel = "k_fir_direct<" + std::to_string(p->D) + "," + std::to_string(R[p->D]) + ">";
+    } else {
+        p->kernel = nsh_fir_mfma_kernel_name(p);
+    }
     *plan = p;
     return 0;
 }
@@ -198,12 +210,14 @@ int nsh_fir_plan_destroy(void* plan)
     if (p->taps_dev) (void)hipFree(p->taps_dev);
     if (p->frag_dev) (void)hipFree(p->frag_dev);
     if (p->frag16_dev) (void)hipFree(p->frag16_dev);
+    if (p->frag8_dev) (void)hipFree(p->frag8_dev);
     if (p->fragd_dev) (void)hipFree(p->fragd_dev);
     delete p;
     return 0;
 }
 
 int nsh_fir_plan_algo(void* plan) { return static_cast<nsh_fir_plan*>(plan)->algo; }
+const char* nsh_fir_plan_kernel(void* plan) { return plan ? static_cast<nsh_fir_plan*>(plan)->kernel.c_str() : ""; }
 
 int nsh_fir_ccf(void* plan, const float* in, const float* hist_in, float* hist_out, float* out, int64_t n_out, void* stream)
 {
@@ -212,7 +226,7 @@ int nsh_fir_ccf(void* plan, const float* in, const float* hist_in, float* hist_o
     if (n_out <= 0) return 0;
     if (hist_in == hist_out && p->L > 1) return nsh::fail_msg("nsh_fir_ccf: hist_out must not alias hist_in");
     hipStream_t s = nsh::S(stream);
-    if (p->algo == NSH_FIR_MFMA)
+    if (p->algo == NSH_FIR_MFMA || p->algo == NSH_FIR_MFMA_BF16X3)
         return nsh_fir_mfma_run(p, (const float2*)in, (const float2*)hist_in, (float2*)hist_out, (float2*)out, n_out, s);
     if (p->algo == NSH_FIR_MFMA16)
         return nsh_fir_mfma16_run(p, (const float2*)in, (const float2*)hist_in, (float2*)hist_out, (float2*)out, n_out, s);

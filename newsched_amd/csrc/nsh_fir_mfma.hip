@@ -34,8 +34,11 @@
 // of a store cover 32 consecutive samples (256 contiguous bytes).
 #include "nsh_common.hpp"
 
+#include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <string>
 #include <vector>
 
 #include "nsh_fir_plan.hpp"
@@ -1053,6 +1056,276 @@ int launch_dec(const nsh_fir_plan* p, const float2* in, const float2* hin, float
     }
 }
 
+// ---- v8: per-chunk scaled fp16x2 split, three products (default for decim 1) ----------------
+// Same Toeplitz GEMM, data movement and LDS row layout as v2, on v_mfma_f32_32x32x16_f16.
+// fp16 keeps 11 significant bits, so a two-term split x = x0 + x1 (both RNE) keeps 22 and
+// three products x0h0 + x0h1 + x1h0 suffice (dropped x1h1 <= 2^-22 |xh|), where bf16 needs
+// three terms and six products: half the matrix work, which is what bounds v2 (DESIGN.md
+// section 4). fp16's narrow exponent range is handled by power-of-two scaling, which is
+// exact:
+//  * taps: scaled once on the host so max |h| * 2^sh lies in [2^14, 2^15);
+//  * samples: per 2048-sample chunk, 2^s with s from the largest magnitude in the chunk and
+//    in its predecessor (which holds the chunk's halo), so every scaled sample is < 2^15
+//    (no fp16 overflow) and outputs are unscaled with one ldexp (exact unless subnormal).
+// Per sample the split is then exact to 2^-22 relative, or 2^-39 of the chunk maximum for
+// samples far below it (fp16 subnormal low term) -- below the fp32 direct form's own
+// rounding error. A chunk holding a non-finite value, or a nonzero sample more than 2^28
+// below the chunk maximum (its high term would be fp16-subnormal), is computed instead by
+// the fp32 direct form inside the same kernel (exact fp32 semantics, including inf/NaN).
+// The scale of chunk c+1 is agreed across the workgroup on the barrier of step c-1 (a wave
+// maximum per slot in LDS); because the scale differs between chunks, the halo of chunk
+// c+1 is re-split from the raw fp32 tail of chunk c kept in an LDS stash, not copied.
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
+typedef __attribute__((ext_vector_type(2))) _Float16 f16x2;
+
+template <int Q>
+struct geom8 {
+    static constexpr int NT = 256;
+    static constexpr int CHUNK = 2048;
+    static constexpr int S = 2 * Q;
+    static constexpr int H = 32 * (Q - 1);
+    static constexpr int HP = H / 2;                          // halo sample pairs
+    static constexpr int NB = (CHUNK + H) / 32;
+    static constexpr int PLANE = (NB * 80 + 255) / 256 * 256;
+    static constexpr int BUF = 4 * PLANE;                     // re0 re1 im0 im1
+    static constexpr int STASH = HP * 16;                     // raw fp32 tail of one chunk
+    static constexpr int SLOTS = 2 * BUF + 2 * STASH;          // u32 max[2][4], flag[2][4]
+    static constexpr int LDS = SLOTS + 64;
+    static constexpr int VPT = 4;
+    static_assert(geom2<Q>::VPT == VPT && geom2<Q>::CHUNK == CHUNK, "v8 reuses v2's load_main");
+    static_assert(HP <= NT, "halo pairs: one per thread");
+};
+
+__device__ __forceinline__ unsigned mag(float x) { return __float_as_uint(x) & 0x7fffffffu; }
+__device__ __forceinline__ unsigned max_mag(const float4& v)
+{
+    return max(max(mag(v.x), mag(v.y)), max(mag(v.z), mag(v.w)));
+}
+// scale exponent: max magnitude (bit pattern) * 2^s in [2^14, 2^15) (zero/subnormal: 2^141)
+__device__ __forceinline__ int scale_of(unsigned maxbits) { return 141 - (int)(maxbits >> 23); }
+__device__ __forceinline__ unsigned wave_max(unsigned v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, (unsigned)__shfl_xor((int)v, o));
+    return v;
+}
+// a scaled sample needs the exact path: non-finite, or nonzero below fp16's normal range
+__device__ __forceinline__ bool needs_exact(float xs)
+{
+    const unsigned m = mag(xs);
+    return m >= 0x7f800000u || (m != 0u && m < 0x38800000u);
+}
+
+// Split two consecutive samples (a, b) of one component, scaled by 2^s, into packed fp16
+// pairs (high terms, low terms).
+__device__ __forceinline__ void split16_pair(float a, float b, int s, unsigned& p0, unsigned& p1, bool& exact)
+{
+    const float as = __builtin_ldexpf(a, s), bs = __builtin_ldexpf(b, s);
+    const _Float16 a0 = (_Float16)as, b0 = (_Float16)bs;
+    const _Float16 a1 = (_Float16)(as - (float)a0), b1 = (_Float16)(bs - (float)b0);
+    p0 = __builtin_bit_cast(unsigned, f16x2{ a0, b0 });
+    p1 = __builtin_bit_cast(unsigned, f16x2{ a1, b1 });
+    exact = exact || needs_exact(as) || needs_exact(bs);
+}
+
+// One float4 (samples s, s+1 of both components) -> the four planes at local sample s.
+template <int Q>
+__device__ __forceinline__ void store_pair8(const float4& v, unsigned char* buf, int s, int sc, bool& exact)
+{
+    using G = geom8<Q>;
+    const int off = (s >> 5) * 80 + (s & 31) * 2;
+    unsigned r0, r1, i0, i1;
+    split16_pair(v.x, v.z, sc, r0, r1, exact);
+    split16_pair(v.y, v.w, sc, i0, i1, exact);
+    *reinterpret_cast<unsigned*>(buf + 0 * G::PLANE + off) = r0;
+    *reinterpret_cast<unsigned*>(buf + 1 * G::PLANE + off) = r1;
+    *reinterpret_cast<unsigned*>(buf + 2 * G::PLANE + off) = i0;
+    *reinterpret_cast<unsigned*>(buf + 3 * G::PLANE + off) = i1;
+}
+
+template <int Q>
+__device__ __forceinline__ void compute_tile8(const unsigned char* lds, const f16x8 (&B0)[2 * Q],
+                                              const f16x8 (&B1)[2 * Q], int a_base, int64_t n_tile, int h,
+                                              int phase, int64_t n_out, int unscale, float2* __restrict__ out)
+{
+    using G = geom8<Q>;
+    f32x16 acc_hi = {};
+    f32x16 acc_lo = {};
+#pragma unroll
+    for (int st = 0; st < 2 * Q; ++st) {
+        const int off = a_base - (st >> 1) * 80 + 32 * (st & 1);
+        const f16x8 A0 = *reinterpret_cast<const f16x8*>(lds + off);
+        const f16x8 A1 = *reinterpret_cast<const f16x8*>(lds + off + G::PLANE);
+        acc_hi = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, B0[st], acc_hi, 0, 0, 0);
+        acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, B1[st], acc_lo, 0, 0, 0);
+        acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, B0[st], acc_lo, 0, 0, 0);
+    }
+#pragma unroll
+    for (int reg = 0; reg < 8; ++reg) {
+        const int blk = (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        const int64_t n = n_tile + 32 * blk + phase;
+        if (n < n_out) {
+            nf2 o = { __builtin_ldexpf(acc_hi[reg] + acc_lo[reg], unscale),
+                      __builtin_ldexpf(acc_hi[reg + 8] + acc_lo[reg + 8], unscale) };
+            __builtin_nontemporal_store(o, reinterpret_cast<nf2*>(out + n));
+        }
+    }
+}
+
+// The exact path for one chunk: fp32 direct form, outputs tid, tid + 256, ...
+__device__ __noinline__ void direct_chunk(const float2* __restrict__ in, const float2* __restrict__ hist,
+                                          const float* __restrict__ taps, int L, int64_t ch, int64_t n_out,
+                                          float2* __restrict__ out)
+{
+    for (int j = threadIdx.x; j < 2048; j += blockDim.x) {
+        const int64_t n = ch * 2048 + j;
+        if (n >= n_out) break;
+        float re = 0.f, im = 0.f;
+        for (int k = 0; k < L; ++k) {
+            const float2 x = virt(in, hist, n - k, n_out, L);
+            re = fmaf(taps[k], x.x, re);
+            im = fmaf(taps[k], x.y, im);
+        }
+        out[n] = make_float2(re, im);
+    }
+}
+
+template <int Q>
+__global__ __launch_bounds__(256, 2) void k_fir_mfma8(const float2* __restrict__ in,
+                                                     const float2* __restrict__ hist_in,
+                                                     float2* __restrict__ hist_out,
+                                                     float2* __restrict__ out,
+                                                     const f16x8* __restrict__ frag, // [2][S][64]
+                                                     const float* __restrict__ taps,
+                                                     int L,
+                                                     int sh,
+                                                     int64_t n_out,
+                                                     int in_aligned)
+{
+    using G = geom8<Q>;
+    constexpr int S = G::S;
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    float4* stash = reinterpret_cast<float4*>(lds + 2 * G::BUF); // [2][HP]
+    unsigned* slot_max = reinterpret_cast<unsigned*>(lds + G::SLOTS);
+    unsigned* slot_exact = slot_max + 8;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int64_t n_in = n_out;
+
+    if (blockIdx.x == 0) {
+        for (int j = tid; j < L - 1; j += G::NT) hist_out[j] = virt(in, hist_in, n_in - (L - 1) + j, n_in, L);
+    }
+
+    f16x8 B0[S], B1[S];
+#pragma unroll
+    for (int st = 0; st < S; ++st) {
+        B0[st] = frag[(0 * S + st) * 64 + lane];
+        B1[st] = frag[(1 * S + st) * 64 + lane];
+    }
+
+    const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
+    const int64_t per = (nchunks + gridDim.x - 1) / gridDim.x;
+    const int64_t c_begin = (int64_t)blockIdx.x * per;
+    const int64_t c_end = c_begin + per < nchunks ? c_begin + per : nchunks;
+    if (c_begin >= c_end) return;
+    const int64_t c_last = c_end - 1;
+
+    const int rho = lane & 31;
+    const int b = rho & 15;
+    const int c = rho >> 4;
+    const int h = lane >> 5;
+    const int a_base = c * 2 * G::PLANE + ((Q - 1) + 16 * wave + b) * 80 + 16 * h;
+    const int phase = lane & 31;
+    const bool al = in_aligned != 0;
+    const bool tail_owner = tid >= G::NT - G::HP; // holds the chunk's last H samples in v[3]
+    auto clamp = [&](int64_t x) { return x <= c_last ? x : c_last; };
+
+    // ---- prologue: chunk c_begin (its halo from global memory), chunks +1, +2 in flight
+    float4 va[G::VPT], vb[G::VPT], vc[G::VPT];
+    float4 hv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (G::HP > 0 && tid < G::HP) {
+        const int64_t g = c_begin * G::CHUNK - G::H + 2 * tid;
+        const float2 x0 = virt(in, hist_in, g, n_in, L), x1 = virt(in, hist_in, g + 1, n_in, L);
+        hv = make_float4(x0.x, x0.y, x1.x, x1.y);
+    }
+    load_main<Q>(va, in, hist_in, c_begin, n_in, L, al);
+    {
+        unsigned m = max_mag(hv);
+#pragma unroll
+        for (int u = 0; u < G::VPT; ++u) m = max(m, max_mag(va[u]));
+        m = wave_max(m);
+        if (lane == 0) slot_max[wave] = m;
+    }
+    __syncthreads();
+    unsigned m_prev = max(max(slot_max[0], slot_max[1]), max(slot_max[2], slot_max[3]));
+    int s_cur = scale_of(m_prev);
+    bool ex = false;
+    if (G::HP > 0 && tid < G::HP) store_pair8<Q>(hv, lds, 2 * tid, s_cur, ex);
+#pragma unroll
+    for (int u = 0; u < G::VPT; ++u) store_pair8<Q>(va[u], lds, G::H + 2 * (tid + G::NT * u), s_cur, ex);
+    if (G::HP > 0 && tail_owner) stash[tid - (G::NT - G::HP)] = va[G::VPT - 1];
+    load_main<Q>(va, in, hist_in, clamp(c_begin + 1), n_in, L, al);
+    load_main<Q>(vb, in, hist_in, clamp(c_begin + 2), n_in, L, al);
+    {
+        unsigned m = 0;
+#pragma unroll
+        for (int u = 0; u < G::VPT; ++u) m = max(m, max_mag(va[u]));
+        m = wave_max(m);
+        const bool any_ex = __any(ex);
+        __syncthreads(); // everyone has read slot_max[0..3] above
+        if (lane == 0) {
+            slot_max[4 + wave] = m;   // chunk 1 -> parity 1
+            slot_exact[wave] = any_ex; // chunk 0 -> parity 0
+        }
+    }
+    __syncthreads();
+
+    // step i (chunk ch = c_begin + i): nxt = chunk ch+1 (split into the other buffer now),
+    // nn = chunk ch+2 (its maximum is published for the next step), ld receives ch+3.
+    auto step = [&](float4 (&nxt)[G::VPT], float4 (&nn)[G::VPT], float4 (&ld)[G::VPT], int64_t ch) {
+        const int i = (int)(ch - c_begin);
+        const int pi = i & 1, pn = pi ^ 1;
+        unsigned char* cur = lds + pi * G::BUF;
+        unsigned char* nbuf = lds + pn * G::BUF;
+        const bool exact_cur = (slot_exact[4 * pi] | slot_exact[4 * pi + 1] | slot_exact[4 * pi + 2] |
+                                slot_exact[4 * pi + 3]) != 0u;
+        const unsigned m_nxt = max(max(slot_max[4 * pn], slot_max[4 * pn + 1]), max(slot_max[4 * pn + 2], slot_max[4 * pn + 3]));
+        const int s_nxt = scale_of(max(m_prev, m_nxt));
+        load_main<Q>(ld, in, hist_in, clamp(ch + 3), n_in, L, al);
+        bool ex2 = false;
+        if (G::HP > 0 && tid < G::HP) store_pair8<Q>(stash[pi * G::HP + tid], nbuf, 2 * tid, s_nxt, ex2);
+#pragma unroll
+        for (int u = 0; u < G::VPT; ++u) store_pair8<Q>(nxt[u], nbuf, G::H + 2 * (tid + G::NT * u), s_nxt, ex2);
+        if (G::HP > 0 && tail_owner) stash[pn * G::HP + tid - (G::NT - G::HP)] = nxt[G::VPT - 1];
+        if (exact_cur)
+            direct_chunk(in, hist_in, taps, L, ch, n_out, out);
+        else
+            compute_tile8<Q>(cur, B0, B1, a_base, ch * G::CHUNK + (int64_t)wave * TILE, h, phase, n_out, -(s_cur + sh), out);
+        unsigned m = 0;
+#pragma unroll
+        for (int u = 0; u < G::VPT; ++u) m = max(m, max_mag(nn[u]));
+        m = wave_max(m);
+        const bool any_ex = __any(ex2);
+        if (lane == 0) {
+            slot_max[4 * pi + wave] = m;       // chunk ch+2 has this step's parity
+            slot_exact[4 * pn + wave] = any_ex; // chunk ch+1
+        }
+        m_prev = m_nxt;
+        s_cur = s_nxt;
+        __syncthreads();
+    };
+    int64_t ch = c_begin;
+    for (; ch + 2 <= c_last; ch += 3) {
+        step(va, vb, vc, ch);
+        step(vb, vc, va, ch + 1);
+        step(vc, va, vb, ch + 2);
+    }
+    if (ch <= c_last) step(va, vb, vc, ch++);
+    if (ch <= c_last) step(vb, vc, va, ch);
+}
+
 // Host-side bf16 round-to-nearest-even (taps are finite).
 unsigned short bf16_rne(float f)
 {
@@ -1092,10 +1365,34 @@ int launch_v2(const nsh_fir_plan* p, const float2* in, const float2* hin, float2
     return 0;
 }
 
+template <int Q>
+int launch_v8(const nsh_fir_plan* p, const float2* in, const float2* hin, float2* hout, float2* out, int64_t n_out,
+              hipStream_t s)
+{
+    using G = geom8<Q>;
+    static bool attr_set = false;
+    if (!attr_set) {
+        NSH_CK(hipFuncSetAttribute((const void*)k_fir_mfma8<Q>, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
+        attr_set = true;
+    }
+    const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
+    int n_cu = 256;
+    (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, p->dev);
+    const int64_t max_grid = (int64_t)n_cu * 2;
+    const unsigned grid = (unsigned)(nchunks < max_grid ? nchunks : max_grid);
+    const int aligned = ((uintptr_t)in % 16 == 0) ? 1 : 0;
+    hipLaunchKernelGGL((k_fir_mfma8<Q>), dim3(grid), dim3(G::NT), G::LDS, s, in, hin, hout, out,
+                       (const f16x8*)p->frag8_dev, (const float*)p->taps_dev, p->L, p->sh8, n_out, aligned);
+    NSH_CK_LAUNCH("nsh_fir_ccf(mfma fp16x2)");
+    return 0;
+}
+
 // Tuning variants (selected by NSH_FIR_MFMA_VARIANT for A/B runs; default = measured best).
 template <int Q>
 int launch_q(const nsh_fir_plan* p, const float2* in, const float2* hin, float2* hout, float2* out, int64_t n_out, hipStream_t s)
 {
+    if (p->frag8_dev && !p->force_x3 && p->variant != 6 && p->variant != 7)
+        return launch_v8<Q>(p, in, hin, hout, out, n_out, s);
     switch (p->variant) {
     case 6: return launch_v2<Q, 1>(p, in, hin, hout, out, n_out, s, 2);
     case 7: return launch_v2<Q, 2>(p, in, hin, hout, out, n_out, s, 2);
@@ -1199,6 +1496,39 @@ int nsh_fir_mfma_prepare(nsh_fir_plan* p)
     NSH_CK(hipMalloc(&p->frag_dev, frag.size() * sizeof(unsigned short)));
     NSH_CK(hipMemcpy(p->frag_dev, frag.data(), frag.size() * sizeof(unsigned short), hipMemcpyHostToDevice));
 
+    // v8: taps scaled by 2^sh8 (max |h| * 2^sh8 in [2^14, 2^15)), split into two fp16 terms
+    // (RNE), same lane order as v2. A tap far below the largest (e.g. firwin's ~1e-18 taps
+    // at the sinc zeros) lands in fp16's subnormal range or flushes: it is then exact to
+    // 2^-39 of the largest tap, which moves an output by at most 2^-39 max|h| sum|x|, far
+    // below fp32's own rounding of the sum. So every finite tap set qualifies.
+    {
+        unsigned maxbits = 0;
+        for (float t : p->taps_host) {
+            unsigned u;
+            std::memcpy(&u, &t, 4);
+            maxbits = std::max(maxbits, u & 0x7fffffffu);
+        }
+        const int sh = 141 - (int)(maxbits >> 23);
+        {
+            std::vector<_Float16> f8((size_t)2 * S * 64 * 8, (_Float16)0.f);
+            for (int st = 0; st < S; ++st)
+                for (int lane = 0; lane < 64; ++lane)
+                    for (int j = 0; j < 8; ++j) {
+                        const int i = lane & 31;
+                        const int r = 16 * (st & 1) + 8 * (lane >> 5) + j;
+                        const int t = i - r + 32 * (st >> 1);
+                        const float hs = (t >= 0 && t < p->L) ? std::ldexp(p->taps_host[t], sh) : 0.f;
+                        const _Float16 h0 = (_Float16)hs;
+                        const _Float16 h1 = (_Float16)(hs - (float)h0);
+                        f8[(((size_t)0 * S + st) * 64 + lane) * 8 + j] = h0;
+                        f8[(((size_t)1 * S + st) * 64 + lane) * 8 + j] = h1;
+                    }
+            p->sh8 = sh;
+            NSH_CK(hipMalloc(&p->frag8_dev, f8.size() * sizeof(_Float16)));
+            NSH_CK(hipMemcpy(p->frag8_dev, f8.data(), f8.size() * sizeof(_Float16), hipMemcpyHostToDevice));
+        }
+    }
+
     // v5: QH/2 k-steps of 32 for v_mfma_f32_16x16x32_bf16 (lane l holds B[k = 8(l >> 4) + j]
     // [col = l & 15], k = 32 st + kk -> q = 2 st + (kk >> 4), r = kk & 15), then for odd QH a
     // tail for v_mfma_f32_16x16x16_bf16 (q = QH - 1, lane l holds B[r = 4(l >> 4) + j][l & 15]).
@@ -1240,6 +1570,18 @@ int nsh_fir_mfma_prepare(nsh_fir_plan* p)
         NSH_CK(hipMemcpy(p->frag16_dev, f16.data(), f16.size() * sizeof(unsigned short), hipMemcpyHostToDevice));
     }
     return 0;
+}
+
+std::string nsh_fir_mfma_kernel_name(const nsh_fir_plan* p)
+{
+    auto t = [](const char* k, int a, int b = -1) {
+        return std::string(k) + "<" + std::to_string(a) + (b >= 0 ? "," + std::to_string(b) : std::string()) + ">";
+    };
+    if (p->algo == NSH_FIR_MFMA16) return t("k_fir_mfma5", p->QH, p->variant == 20 ? 2 : 1);
+    if (p->D > 1) return t("k_fir_mfma7", p->D, p->QHD);
+    if (p->frag8_dev && !p->force_x3 && p->variant != 6 && p->variant != 7) return t("k_fir_mfma8", p->Q);
+    if (p->variant >= 20) return t("k_fir_mfma5", p->QH, p->variant == 20 ? 2 : 1);
+    return t("k_fir_mfma2", p->Q, p->variant == 6 ? 1 : 2);
 }
 
 bool nsh_fir_mfma16_supported(const nsh_fir_plan* p)

@@ -1,6 +1,7 @@
 // Internal FIR plan shared by nsh_fir.hip (direct form, dispatch) and nsh_fir_mfma.hip.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <string>
 #include <vector>
 
 struct nsh_fir_plan {
@@ -24,8 +25,16 @@ struct nsh_fir_plan {
     // [phase][part(3)][kstep][lane][8] + [phase][part][lane][4] tail, bf16.
     int QHD = 0;
     void* fragd_dev = nullptr;
+    // scaled fp16x2 form (decim 1, default): taps * 2^sh8 split into two fp16 terms,
+    // [part(2)][kstep(S)][lane(64)][8]; null when the taps' range does not allow it.
+    void* frag8_dev = nullptr;
+    int sh8 = 0;
+    bool force_x3 = false; // NSH_FIR_MFMA_BF16X3: always the bf16x3 six-product kernel
     int variant = 0;      // MFMA kernel tuning variant (0 = default)
+    std::string kernel;   // the kernel nsh_fir_ccf launches (rocprof name without namespace)
 };
+
+std::string nsh_fir_mfma_kernel_name(const nsh_fir_plan* p);
 
 bool nsh_fir_mfma_supported(const nsh_fir_plan* p);
 bool nsh_fir_mfma16_supported(const nsh_fir_plan* p);

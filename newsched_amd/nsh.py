@@ -18,7 +18,7 @@ LIB_DIR = os.path.join(_HERE, "lib")
 HIP_LIB = os.path.join(LIB_DIR, "libnsh_hip.so")
 
 NSH_H2D, NSH_D2H, NSH_D2D, NSH_DEFAULT = 0, 1, 2, 3
-FIR_AUTO, FIR_DIRECT, FIR_MFMA, FIR_MFMA16 = 0, 1, 2, 3
+FIR_AUTO, FIR_DIRECT, FIR_MFMA, FIR_MFMA16, FIR_MFMA_BF16X3 = 0, 1, 2, 3, 4
 
 # name -> (restype, argtypes); mirrors include/nsh_hip.h exactly (tests check the header).
 _vp, _i, _i64, _u64, _sz, _f = C.c_void_p, C.c_int, C.c_int64, C.c_uint64, C.c_size_t, C.c_float
@@ -57,6 +57,7 @@ SIGNATURES = {
     "nsh_fir_plan_create": (_i, [_i, C.POINTER(_f), _i, _i, _i, C.POINTER(_vp)]),
     "nsh_fir_plan_destroy": (_i, [_vp]),
     "nsh_fir_plan_algo": (_i, [_vp]),
+    "nsh_fir_plan_kernel": (C.c_char_p, [_vp]),
     "nsh_fir_ccf": (_i, [_vp, _vp, _vp, _vp, _vp, _i64, _vp]),
     "nsh_fft1024_c2c": (_i, [_vp, _vp, _i64, _i, _vp]),
     "nsh_channelizer1024": (_i, [_vp, _vp, _vp, _i64, _vp]),
@@ -161,6 +162,7 @@ class FirPlan:
               "nsh_fir_plan_create")
         self._h = h
         self.algo = lib().nsh_fir_plan_algo(h)
+        self.kernel = lib().nsh_fir_plan_kernel(h).decode()
 
     def __call__(self, x, hist_in, hist_out, y, n_out: int, stream=None):
         check(lib().nsh_fir_ccf(self._h, ptr(x), ptr(hist_in), ptr(hist_out), ptr(y), n_out,

@@ -20,6 +20,7 @@ SIGNATURES = {
     "nsr_fir_bench_create": (_i, [_i, C.POINTER(C.c_float), _i, _i, _i64, _u64, _u64, _sz, _i, C.POINTER(_vp)]),
     "nsr_fir_bench_run": (_i, [_vp]),
     "nsr_fir_bench_stats": (_i, [_vp, C.POINTER(_d), C.POINTER(_u64), C.POINTER(_u64), C.POINTER(_i)]),
+    "nsr_fir_bench_kernel": (C.c_char_p, [_vp]),
     "nsr_fir_bench_tail": (_i, [_vp, _i64, C.POINTER(C.c_float)]),
     "nsr_fir_bench_destroy": (_i, [_vp]),
     "nsr_cpu_fir_run": (_i, [C.POINTER(C.c_float), _i, C.POINTER(C.c_float), _i64, _i64, _sz, C.POINTER(_d)]),
@@ -69,7 +70,8 @@ class FirBench:
         ms, la, sa, al = C.c_double(), C.c_uint64(), C.c_uint64(), C.c_int()
         check(lib().nsr_fir_bench_stats(self._h, C.byref(ms), C.byref(la), C.byref(sa), C.byref(al)),
               "nsr_fir_bench_stats")
-        return {"kernel_ms": ms.value, "launches": la.value, "samples": sa.value, "algo": al.value}
+        return {"kernel_ms": ms.value, "launches": la.value, "samples": sa.value, "algo": al.value,
+                "kernel": lib().nsr_fir_bench_kernel(self._h).decode()}
 
     def tail(self, count):
         out = np.empty(count, np.complex64)

@@ -114,8 +114,11 @@ def test_add_mul_cc_bit_exact(torch_cuda, n):
     np.testing.assert_array_equal(host(dy), orc.mul_cc(a, b))
 
 
-ALGOS = [("direct", nsh.FIR_DIRECT), ("mfma", nsh.FIR_MFMA), ("mfma16", nsh.FIR_MFMA16)]
-MAX_TAPS = {"direct": 4096, "mfma": 161, "mfma16": 145}
+# "mfma" is the default matrix-core kernel (decim 1: per-chunk scaled fp16x2, k_fir_mfma8),
+# "mfma_x3" forces the bf16x3 six-product kernel (k_fir_mfma2), "mfma16" the 16-sample form.
+ALGOS = [("direct", nsh.FIR_DIRECT), ("mfma", nsh.FIR_MFMA), ("mfma_x3", nsh.FIR_MFMA_BF16X3),
+         ("mfma16", nsh.FIR_MFMA16)]
+MAX_TAPS = {"direct": 4096, "mfma": 161, "mfma_x3": 161, "mfma16": 145}
 
 
 def run_fir(torch, plan, x, n_out, hist=None):
@@ -134,6 +137,8 @@ def test_fir127_golden(torch_cuda, golden, name, algo):
     g = golden("fir127.npz")
     plan = nsh.FirPlan(g["taps"], 1, algo)
     assert plan.algo == algo
+    if name == "mfma":
+        assert plan.kernel == "k_fir_mfma8<5>", plan.kernel
     y, hist = run_fir(torch, plan, g["x"], g["x"].size)
     ok, err, scale = orc.tol_ok(y, g["y"])
     assert ok, (name, err, scale)
@@ -272,6 +277,101 @@ def test_fir_linearity_large(torch_cuda, name, algo):
     lin = (0.5 * y + y2 - y3).abs().max().item()
     scale = y3.abs().max().item()
     assert lin <= 2e-6 * scale, (lin, scale)
+
+
+def _firwin127():
+    return np.asarray(__import__("scipy.signal", fromlist=["firwin"]).firwin(127, 0.2), np.float32)
+
+
+def _assert_nonfinite_pattern(y, ref):
+    for f in (np.isnan, np.isinf):
+        for part in (np.real, np.imag):
+            bad = np.nonzero(f(part(y)) != f(part(ref)))[0]
+            assert bad.size == 0, (f.__name__, part.__name__, bad.size, bad[:8].tolist(), bad[-8:].tolist(),
+                                   y[bad[:4]].tolist(), ref[bad[:4]].tolist())
+    inf = np.isinf(y.real)
+    np.testing.assert_array_equal(np.sign(y.real[inf]), np.sign(ref.real[inf]))
+    inf = np.isinf(y.imag)
+    np.testing.assert_array_equal(np.sign(y.imag[inf]), np.sign(ref.imag[inf]))
+
+
+def test_fir_mfma_nonfinite_inputs(torch_cuda):
+    """k_fir_mfma8 sends chunks holding inf/NaN (and their successors, whose halo and scale
+    include them) through the fp32 direct form in the same launch: the inf/NaN pattern of
+    every output equals the oracle's (IEEE double), and finite outputs meet the tolerance."""
+    torch = torch_cuda
+    h = _firwin127()
+    x = orc.synth(50_000, 9)
+    x[1000] = np.complex64(complex(np.inf, 0.5))
+    x[20_000] = np.complex64(complex(np.nan, 0.0))
+    x[30_000] = np.complex64(complex(0.25, -np.inf))
+    x[30_050] = np.complex64(complex(-np.inf, np.inf))
+    y, _ = run_fir(torch, nsh.FirPlan(h, 1, nsh.FIR_MFMA), x, x.size)
+    ref = orc.fir_ccf(x, h)
+    _assert_nonfinite_pattern(y, ref)
+    fin = np.isfinite(ref.real) & np.isfinite(ref.imag)
+    ok, err, scale = orc.tol_ok(y[fin], ref[fin])
+    assert ok, (err, scale)
+
+
+def test_fir_mfma_wide_dynamic_range(torch_cuda):
+    """One sample 2^60 above the rest: the samples sharing its chunk (and the next one)
+    would flush to zero in fp16 at the spike's scale, so those chunks take the exact path.
+    Outputs away from the spike are checked against the oracle on their own scale."""
+    torch = torch_cuda
+    h = _firwin127()
+    x = orc.synth(40_000, 21)
+    x[10_000] *= np.float32(2.0 ** 60)
+    y, _ = run_fir(torch, nsh.FirPlan(h, 1, nsh.FIR_MFMA), x, x.size)
+    ref = orc.fir_ccf(x, h)
+    for a, b in ((0, 10_000), (10_000, 10_127), (10_127, 40_000)):
+        ok, err, scale = orc.tol_ok(y[a:b], ref[a:b])
+        assert ok, (a, b, err, scale)
+
+
+def test_fir_mfma_per_chunk_scale(torch_cuda):
+    """Segments at amplitudes 1e-30, 1 and 1e30 (each far outside fp16's range unscaled):
+    the per-chunk power-of-two scale keeps every segment at fp32 accuracy, checked on the
+    segment's own scale; chunks mixing two amplitudes take the exact path."""
+    torch = torch_cuda
+    h = _firwin127()
+    seg = 20_480
+    x = orc.synth(3 * seg, 33)
+    x[:seg] *= np.float32(1e-30)
+    x[2 * seg:] *= np.float32(1e30)
+    y, _ = run_fir(torch, nsh.FirPlan(h, 1, nsh.FIR_MFMA), x, x.size)
+    ref = orc.fir_ccf(x, h)
+    for a, b in ((0, seg), (seg + 127, 2 * seg), (2 * seg + 127, 3 * seg)):
+        ok, err, scale = orc.tol_ok(y[a:b], ref[a:b])
+        assert ok, (a, b, err, scale)
+
+
+def test_fir_mfma_taps_far_below_max(torch_cuda):
+    """Taps 2^-40 below the largest (and firwin's ~1e-18 taps at its sinc zeros) fall into
+    fp16's subnormal range after scaling; the fp16x2 kernel still serves the plan and meets
+    the tolerance (such a tap moves an output by <= 2^-39 max|h| sum|x|)."""
+    torch = torch_cuda
+    h = _firwin127()
+    h[5] = np.float32(h.max() * 2.0 ** -40)
+    x = orc.synth(30_000, 4)
+    plan = nsh.FirPlan(h, 1, nsh.FIR_MFMA)
+    assert plan.kernel == "k_fir_mfma8<5>", plan.kernel
+    y, _ = run_fir(torch, plan, x, x.size)
+    ok, err, scale = orc.tol_ok(y, orc.fir_ccf(x, h))
+    assert ok, (err, scale)
+
+
+def test_fir_plan_kernels():
+    """Which kernel each algorithm runs (no silent fallback between the MFMA forms)."""
+    h = _firwin127()
+    assert nsh.FirPlan(h, 1, nsh.FIR_MFMA).kernel == "k_fir_mfma8<5>"
+    assert nsh.FirPlan(h, 1, nsh.FIR_AUTO).kernel == "k_fir_mfma8<5>"
+    assert nsh.FirPlan(h, 1, nsh.FIR_MFMA_BF16X3).kernel == "k_fir_mfma2<5,2>"
+    assert nsh.FirPlan(h, 1, nsh.FIR_MFMA16).kernel == "k_fir_mfma5<9,1>"
+    assert nsh.FirPlan(h, 1, nsh.FIR_DIRECT).kernel == "k_fir_direct<1,8>"
+    assert nsh.FirPlan(h, 2, nsh.FIR_MFMA).kernel == "k_fir_mfma7<2,5>"
+    for L in (1, 17, 33, 65, 97, 129, 161):
+        assert nsh.FirPlan(np.ones(L, np.float32), 1, nsh.FIR_MFMA).kernel == "k_fir_mfma8<%d>" % ((L + 30) // 32 + 1)
 
 
 def test_fft_golden(torch_cuda, golden):

@@ -12,7 +12,7 @@ import torch
 from newsched_amd import nsh
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--algo", default="mfma", choices=["mfma", "direct"])
+ap.add_argument("--algo", default="mfma", choices=["mfma", "mfma_x3", "direct"])
 ap.add_argument("--log2n", type=int, default=25)
 ap.add_argument("--reps", type=int, default=10)
 a = ap.parse_args()
@@ -23,10 +23,10 @@ nsh.synth(x, n, 0)
 y = torch.empty_like(x)
 hin = torch.zeros(126, dtype=torch.complex64, device="cuda")
 hout = torch.zeros_like(hin)
-p = nsh.FirPlan(h, 1, nsh.FIR_MFMA if a.algo == "mfma" else nsh.FIR_DIRECT)
+p = nsh.FirPlan(h, 1, {"mfma": nsh.FIR_MFMA, "mfma_x3": nsh.FIR_MFMA_BF16X3, "direct": nsh.FIR_DIRECT}[a.algo])
 for _ in range(a.reps):
     p(x, hin, hout, y, n)
 for _ in range(a.reps):
     nsh.copy(x, y, 8 * n)  # calibration: exactly 8n B read + 8n B written per launch
 torch.cuda.synchronize()
-print("done", n, a.algo)
+print("done", n, a.algo, p.kernel)

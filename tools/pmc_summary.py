@@ -7,6 +7,7 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
 from collections import defaultdict
 
@@ -27,9 +28,11 @@ def main(root, n_samples, out_json):
             continue
         for r in load(p):
             k = r["Kernel_Name"]
-            short = "fir_mfma" if "k_fir_mfma" in k else "fir_direct" if "k_fir_direct" in k else "copy" if "k_copy_v4" in k else None
-            if short is None:
+            # key: the kernel template name, as nsh_fir_plan_kernel() reports it ("k_fir_mfma8<5>")
+            m = re.search(r"(k_fir_\w+<[^>(]*>|k_copy_v4)", k)
+            if m is None:
                 continue
+            short = m.group(1).replace(" ", "")
             acc[short][r["Counter_Name"]] += float(r["Counter_Value"])
             disp[(short, r["Counter_Name"])].add(r["Dispatch_Id"])
     summ = {}
