@@ -56,7 +56,7 @@ def load_pmc_traffic(kernel, samples_per_launch):
     """HBM bytes per launch from the committed PMC summary (profiles/pmc_fir.json, produced
     by tools/pmc_summary.py from separate rocprofv3 --pmc passes, gfx950 FETCH_SIZE x2
     correction applied there), scaled to this launch size. kernel: the template name the
-    plan reports (nsh_fir_plan_kernel), e.g. "k_fir_mfma8<5>"."""
+    plan reports (nsh_fir_plan_kernel), e.g. "k_fir_mfma9<5>"."""
     p = os.path.join(ROOT, "profiles", "pmc_fir.json")
     try:
         with open(p) as f:
@@ -69,8 +69,8 @@ def load_pmc_traffic(kernel, samples_per_launch):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--log2n", type=int, default=28)
     ap.add_argument("--algo", default="auto", choices=["auto", "mfma", "mfma_x3", "mfma16", "direct"])
     ap.add_argument("--out-buf-mib", type=int, default=2048, help="FIR output hip_buffer (default: one launch per 2^28-sample step)")

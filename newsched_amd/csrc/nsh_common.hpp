@@ -37,6 +37,17 @@ inline unsigned stream_grid(int64_t n_vec, int block)
     return (unsigned)g;
 }
 
+// Workgroup barrier that orders LDS only. __syncthreads() is a workgroup-scope fence on all
+// address spaces, which on gfx950 waits for every outstanding global load and store
+// (s_waitcnt vmcnt(0)) -- in a streaming kernel that drains the register prefetch of the
+// next chunks at every step. Kernels whose waves share data only through LDS use this.
+__device__ __forceinline__ void lds_barrier()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 } // namespace nsh
 
 #define NSH_CK(expr)                                                    \

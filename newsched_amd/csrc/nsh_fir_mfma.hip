@@ -1090,7 +1090,7 @@ struct geom8 {
     static constexpr int BUF = 4 * PLANE;                     // re0 re1 im0 im1
     static constexpr int STASH = HP * 16;                     // raw fp32 tail of one chunk
     static constexpr int SLOTS = 2 * BUF + 2 * STASH;          // u32 max[2][4], flag[2][4]
-    static constexpr int LDS = SLOTS + 64;
+    static constexpr int LDS = SLOTS + 64;                     // u32 [2][4] x 2 (v8: max, exact; v9: max, mnz)
     static constexpr int VPT = 4;
     static_assert(geom2<Q>::VPT == VPT && geom2<Q>::CHUNK == CHUNK, "v8 reuses v2's load_main");
     static_assert(HP <= NT, "halo pairs: one per thread");
@@ -1326,6 +1326,297 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma8(const float2* __restrict__
     if (ch <= c_last) step(vb, vc, va, ch);
 }
 
+// ---- k_fir_mfma9: the fp16x2 form of k_fir_mfma8 with an exactly counted memory pipeline ----
+// Same GEMM, LDS planes, per-chunk scale and exact-path rule as k_fir_mfma8. What changes is
+// how the step's memory traffic is ordered, which k_fir_mfma8 lost twice over (its .s waits
+// vmcnt(0) once per step, i.e. for the prefetch of chunk ch+3 issued at the top of that step):
+//  * barriers order LDS only (nsh::lds_barrier); __syncthreads() is a fence on global memory too;
+//  * every step issues exactly 4 buffer loads (chunk ch+3) and 8 buffer stores per lane on a
+//    per-chunk resource: out-of-range lanes read 0 and drop their store, so the stream's
+//    partial last chunk needs no branch and the compiler's vmcnt waits count exactly;
+//  * the exact path issues no global memory operation: a chunk that needs it is staged in LDS
+//    as raw fp32 (instead of fp16 planes) one step ahead, and the direct form reads it there,
+//    producing the same 8 outputs per lane the MFMA tile does, stored by the same 8 stores;
+//  * the exact-path decision is per chunk, from the chunk maximum (non-finite) and minimum
+//    nonzero magnitude (fp16-subnormal after scaling) reduced alongside the scale: the same
+//    rule k_fir_mfma8 applies per sample, with the halo test widened to its whole source chunk.
+
+__device__ __forceinline__ unsigned wave_min(unsigned v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = min(v, (unsigned)__shfl_xor((int)v, o));
+    return v;
+}
+// min over components of (magnitude bits - 1): zero maps to 0xffffffff, so the chunk minimum
+// is (smallest nonzero magnitude - 1), or ~0u for an all-zero chunk
+__device__ __forceinline__ unsigned min_nz1(const float4& v)
+{
+    return min(min(mag(v.x) - 1u, mag(v.y) - 1u), min(mag(v.z) - 1u, mag(v.w) - 1u));
+}
+// needs_exact() over a whole chunk: non-finite iff its largest magnitude is; a nonzero sample
+// scales below fp16's normal range iff its smallest nonzero one does (ldexp is exact, monotonic)
+__device__ __forceinline__ bool chunk_needs_exact(unsigned maxbits, unsigned mnz1, int s)
+{
+    if (maxbits >= 0x7f800000u) return true;
+    if (mnz1 == ~0u) return false;
+    return __builtin_ldexpf(__uint_as_float(mnz1 + 1u), s) < 6.103515625e-05f; // 2^-14
+}
+
+// Raw buffer resource over chunk ch of a stream: [base + 2048 ch, + min(n - 2048 ch, 2048)
+// items), at least 0. Built from wave-uniform values only (no waterfall loops).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t chunk_rsrc(const float2* base, int64_t ch, int64_t n)
+{
+    int64_t items = n - ch * 2048;
+    items = items < 0 ? 0 : (items > 2048 ? 2048 : items);
+    const uint64_t a = (uint64_t)(base + ch * 2048);
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+    const int bytes = __builtin_amdgcn_readfirstlane((int)(items * 8));
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0, bytes, 0x00020000);
+}
+constexpr int AUX_NT = 2; // gfx950 cache policy bits: nt (streaming)
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+
+// chunk ch -> registers: lane t holds samples (2t, 2t+1) + 512 u, u < 4
+__device__ __forceinline__ void load_chunk9(float4 (&v)[4], const float2* __restrict__ in, int64_t ch, int64_t n_in)
+{
+    const __amdgpu_buffer_rsrc_t r = chunk_rsrc(in, ch, n_in);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const nf4 t = __builtin_bit_cast(nf4, __builtin_amdgcn_raw_buffer_load_b128(r, (threadIdx.x + 256 * u) * 16, 0, AUX_NT));
+        v[u] = make_float4(t.x, t.y, t.z, t.w);
+    }
+}
+
+// split without the per-sample test (k_fir_mfma9 decides per chunk)
+template <int Q>
+__device__ __forceinline__ void store_pair9(const float4& v, unsigned char* buf, int s, int sc)
+{
+    using G = geom8<Q>;
+    const int off = (s >> 5) * 80 + (s & 31) * 2;
+    const float ar = __builtin_ldexpf(v.x, sc), br = __builtin_ldexpf(v.z, sc);
+    const float ai = __builtin_ldexpf(v.y, sc), bi = __builtin_ldexpf(v.w, sc);
+    const _Float16 ar0 = (_Float16)ar, br0 = (_Float16)br, ai0 = (_Float16)ai, bi0 = (_Float16)bi;
+    *reinterpret_cast<unsigned*>(buf + 0 * G::PLANE + off) = __builtin_bit_cast(unsigned, f16x2{ ar0, br0 });
+    *reinterpret_cast<unsigned*>(buf + 1 * G::PLANE + off) =
+        __builtin_bit_cast(unsigned, f16x2{ (_Float16)(ar - (float)ar0), (_Float16)(br - (float)br0) });
+    *reinterpret_cast<unsigned*>(buf + 2 * G::PLANE + off) = __builtin_bit_cast(unsigned, f16x2{ ai0, bi0 });
+    *reinterpret_cast<unsigned*>(buf + 3 * G::PLANE + off) =
+        __builtin_bit_cast(unsigned, f16x2{ (_Float16)(ai - (float)ai0), (_Float16)(bi - (float)bi0) });
+}
+
+// MFMA tile (as compute_tile8) -> the lane's 8 outputs, unscaled
+template <int Q>
+__device__ __forceinline__ void mfma_tile9(const unsigned char* lds, const f16x8 (&B0)[2 * Q], const f16x8 (&B1)[2 * Q],
+                                           int a_base, int unscale, nf2 (&o)[8])
+{
+    using G = geom8<Q>;
+    f32x16 acc_hi = {};
+    f32x16 acc_lo = {};
+#pragma unroll
+    for (int st = 0; st < 2 * Q; ++st) {
+        const int off = a_base - (st >> 1) * 80 + 32 * (st & 1);
+        const f16x8 A0 = *reinterpret_cast<const f16x8*>(lds + off);
+        const f16x8 A1 = *reinterpret_cast<const f16x8*>(lds + off + G::PLANE);
+        acc_hi = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, B0[st], acc_hi, 0, 0, 0);
+        acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, B1[st], acc_lo, 0, 0, 0);
+        acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, B0[st], acc_lo, 0, 0, 0);
+    }
+#pragma unroll
+    for (int reg = 0; reg < 8; ++reg)
+        o[reg] = nf2{ __builtin_ldexpf(acc_hi[reg] + acc_lo[reg], unscale),
+                      __builtin_ldexpf(acc_hi[reg + 8] + acc_lo[reg + 8], unscale) };
+}
+
+// The exact path on a raw fp32 chunk in LDS (local sample j at float2 index j, halo first):
+// the lane's 8 outputs by the fp32 direct form, in direct_chunk's order.
+template <int Q>
+__device__ __forceinline__ void direct_tile9(const unsigned char* lds, const float* __restrict__ taps, int L, int wave, int h,
+                                             int phase, nf2 (&o)[8])
+{
+    using G = geom8<Q>;
+    const float2* raw = reinterpret_cast<const float2*>(lds);
+    for (int reg = 0; reg < 8; ++reg) {
+        const int blk = (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        const int j = G::H + wave * TILE + 32 * blk + phase;
+        float re = 0.f, im = 0.f;
+        for (int k = 0; k < L; ++k) {
+            const float2 x = raw[j - k];
+            re = fmaf(taps[k], x.x, re);
+            im = fmaf(taps[k], x.y, im);
+        }
+        o[reg] = nf2{ re, im };
+    }
+}
+
+template <int Q>
+__global__ __launch_bounds__(256, 2) void k_fir_mfma9(const float2* __restrict__ in,
+                                                     const float2* __restrict__ hist_in,
+                                                     float2* __restrict__ hist_out,
+                                                     float2* __restrict__ out,
+                                                     const f16x8* __restrict__ frag, // [2][S][64]
+                                                     const float* __restrict__ taps,
+                                                     int L,
+                                                     int sh,
+                                                     int64_t n_out)
+{
+    using G = geom8<Q>;
+    constexpr int S = G::S;
+    static_assert((G::HP + 4 * G::NT) * 16 <= G::BUF, "a raw fp32 chunk + halo fits one plane buffer");
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    float4* stash = reinterpret_cast<float4*>(lds + 2 * G::BUF); // [2][HP] raw fp32 chunk tails
+    unsigned* slot_max = reinterpret_cast<unsigned*>(lds + G::SLOTS); // [2][4]
+    unsigned* slot_mnz = slot_max + 8;                                 // [2][4]
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int64_t n_in = n_out;
+
+    if (blockIdx.x == 0) {
+        for (int j = tid; j < L - 1; j += G::NT) hist_out[j] = virt(in, hist_in, n_in - (L - 1) + j, n_in, L);
+    }
+
+    f16x8 B0[S], B1[S];
+#pragma unroll
+    for (int st = 0; st < S; ++st) {
+        B0[st] = frag[(0 * S + st) * 64 + lane];
+        B1[st] = frag[(1 * S + st) * 64 + lane];
+    }
+
+    const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
+    const int64_t per = (nchunks + gridDim.x - 1) / gridDim.x;
+    const int64_t c_begin = (int64_t)blockIdx.x * per;
+    const int64_t c_end = c_begin + per < nchunks ? c_begin + per : nchunks;
+    if (c_begin >= c_end) return;
+    const int64_t c_last = c_end - 1;
+
+    const int rho = lane & 31;
+    const int b = rho & 15;
+    const int c = rho >> 4;
+    const int h = lane >> 5;
+    const int a_base = c * 2 * G::PLANE + ((Q - 1) + 16 * wave + b) * 80 + 16 * h;
+    const int phase = lane & 31;
+    const bool tail_owner = tid >= G::NT - G::HP; // holds the chunk's last H samples in v[3]
+    auto clamp = [&](int64_t x) { return x <= c_last ? x : c_last; };
+    // chunk (halo pairs from hv_or_stash, main pairs from v) -> buffer, raw or split
+    auto put_chunk = [&](unsigned char* buf, const float4& halo, const float4 (&v)[4], bool raw, int sc) {
+        if (raw) {
+            float4* r = reinterpret_cast<float4*>(buf);
+            if (G::HP > 0 && tid < G::HP) r[tid] = halo;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) r[G::HP + tid + G::NT * u] = v[u];
+        } else {
+            if (G::HP > 0 && tid < G::HP) store_pair9<Q>(halo, buf, 2 * tid, sc);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) store_pair9<Q>(v[u], buf, G::H + 2 * (tid + G::NT * u), sc);
+        }
+    };
+    auto reduce = [&](const float4 (&v)[4], unsigned& m, unsigned& z) {
+        m = 0;
+        z = ~0u;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            m = max(m, max_mag(v[u]));
+            z = min(z, min_nz1(v[u]));
+        }
+        m = wave_max(m);
+        z = wave_min(z);
+    };
+    auto store_tile = [&](int64_t ch, const nf2 (&o)[8]) {
+        const __amdgpu_buffer_rsrc_t r = chunk_rsrc(out, ch, n_out);
+        const int base = wave * TILE + phase;
+#pragma unroll
+        for (int reg = 0; reg < 8; ++reg) {
+            const int blk = (reg & 3) + 8 * (reg >> 2) + 4 * h;
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, o[reg]), r, (base + 32 * blk) * 8, 0, AUX_NT);
+        }
+    };
+
+    // ---- prologue: chunk c_begin (its halo from global memory / history), +1, +2 in flight
+    float4 va[4], vb[4], vc[4];
+    float4 hv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (G::HP > 0 && tid < G::HP) {
+        const int64_t g = c_begin * G::CHUNK - G::H + 2 * tid;
+        const float2 x0 = virt(in, hist_in, g, n_in, L), x1 = virt(in, hist_in, g + 1, n_in, L);
+        hv = make_float4(x0.x, x0.y, x1.x, x1.y);
+    }
+    load_chunk9(va, in, c_begin, n_in);
+    {
+        unsigned m, z;
+        reduce(va, m, z);
+        m = max(m, wave_max(max_mag(hv)));
+        z = min(z, wave_min(min_nz1(hv)));
+        if (lane == 0) {
+            slot_max[wave] = m;
+            slot_mnz[wave] = z;
+        }
+    }
+    nsh::lds_barrier();
+    unsigned m_prev = max(max(slot_max[0], slot_max[1]), max(slot_max[2], slot_max[3]));
+    unsigned z_prev = min(min(slot_mnz[0], slot_mnz[1]), min(slot_mnz[2], slot_mnz[3]));
+    int s_cur = scale_of(m_prev);
+    bool ex_cur = chunk_needs_exact(m_prev, z_prev, s_cur);
+    put_chunk(lds, hv, va, ex_cur, s_cur);
+    if (G::HP > 0 && tail_owner) stash[tid - (G::NT - G::HP)] = va[3];
+    load_chunk9(va, in, clamp(c_begin + 1), n_in);
+    load_chunk9(vb, in, clamp(c_begin + 2), n_in);
+    {
+        unsigned m, z;
+        reduce(va, m, z);
+        nsh::lds_barrier(); // everyone has read slots [0..3] above
+        if (lane == 0) {
+            slot_max[4 + wave] = m; // chunk c_begin + 1 -> parity 1
+            slot_mnz[4 + wave] = z;
+        }
+    }
+    nsh::lds_barrier();
+
+    // step i (chunk ch = c_begin + i): nxt = chunk ch+1 (staged into the other buffer now),
+    // nn = chunk ch+2 (reduced for the next step), ld receives ch+3.
+    auto step = [&](float4 (&nxt)[4], float4 (&nn)[4], float4 (&ld)[4], int64_t ch) {
+        const int i = (int)(ch - c_begin);
+        const int pi = i & 1, pn = pi ^ 1;
+        const unsigned char* cur = lds + pi * G::BUF;
+        unsigned char* nbuf = lds + pn * G::BUF;
+        const unsigned m_nxt = max(max(slot_max[4 * pn], slot_max[4 * pn + 1]), max(slot_max[4 * pn + 2], slot_max[4 * pn + 3]));
+        const unsigned z_nxt = min(min(slot_mnz[4 * pn], slot_mnz[4 * pn + 1]), min(slot_mnz[4 * pn + 2], slot_mnz[4 * pn + 3]));
+        const unsigned m2 = max(m_prev, m_nxt);
+        const int s_nxt = scale_of(m2);
+        // chunk ch+1 is split with chunk ch's tail (its halo) at 2^s_nxt: the test covers
+        // all of chunk ch (a superset of the halo, so conservative)
+        const bool ex_nxt = chunk_needs_exact(m2, min(z_prev, z_nxt), s_nxt);
+        load_chunk9(ld, in, clamp(ch + 3), n_in);
+        put_chunk(nbuf, G::HP > 0 && tid < G::HP ? stash[pi * G::HP + tid] : make_float4(0.f, 0.f, 0.f, 0.f), nxt, ex_nxt, s_nxt);
+        if (G::HP > 0 && tail_owner) stash[pn * G::HP + tid - (G::NT - G::HP)] = nxt[3];
+        nf2 o[8];
+        if (ex_cur)
+            direct_tile9<Q>(cur, taps, L, wave, h, phase, o);
+        else
+            mfma_tile9<Q>(cur, B0, B1, a_base, -(s_cur + sh), o);
+        store_tile(ch, o);
+        unsigned m, z;
+        reduce(nn, m, z);
+        if (lane == 0) {
+            slot_max[4 * pi + wave] = m; // chunk ch+2 has this step's parity
+            slot_mnz[4 * pi + wave] = z;
+        }
+        m_prev = m_nxt;
+        z_prev = z_nxt;
+        ex_cur = ex_nxt;
+        s_cur = s_nxt;
+        nsh::lds_barrier();
+    };
+    int64_t ch = c_begin;
+    for (; ch + 2 <= c_last; ch += 3) {
+        step(va, vb, vc, ch);
+        step(vb, vc, va, ch + 1);
+        step(vc, va, vb, ch + 2);
+    }
+    if (ch <= c_last) step(va, vb, vc, ch++);
+    if (ch <= c_last) step(vb, vc, va, ch);
+}
+
 // Host-side bf16 round-to-nearest-even (taps are finite).
 unsigned short bf16_rne(float f)
 {
@@ -1387,12 +1678,33 @@ int launch_v8(const nsh_fir_plan* p, const float2* in, const float2* hin, float2
     return 0;
 }
 
+template <int Q>
+int launch_v9(const nsh_fir_plan* p, const float2* in, const float2* hin, float2* hout, float2* out, int64_t n_out,
+              hipStream_t s)
+{
+    using G = geom8<Q>;
+    static bool attr_set = false;
+    if (!attr_set) {
+        NSH_CK(hipFuncSetAttribute((const void*)k_fir_mfma9<Q>, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
+        attr_set = true;
+    }
+    const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
+    int n_cu = 256;
+    (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, p->dev);
+    const int64_t max_grid = (int64_t)n_cu * 2;
+    const unsigned grid = (unsigned)(nchunks < max_grid ? nchunks : max_grid);
+    hipLaunchKernelGGL((k_fir_mfma9<Q>), dim3(grid), dim3(G::NT), G::LDS, s, in, hin, hout, out,
+                       (const f16x8*)p->frag8_dev, (const float*)p->taps_dev, p->L, p->sh8, n_out);
+    NSH_CK_LAUNCH("nsh_fir_ccf(mfma fp16x2 v9)");
+    return 0;
+}
+
 // Tuning variants (selected by NSH_FIR_MFMA_VARIANT for A/B runs; default = measured best).
 template <int Q>
 int launch_q(const nsh_fir_plan* p, const float2* in, const float2* hin, float2* hout, float2* out, int64_t n_out, hipStream_t s)
 {
     if (p->frag8_dev && !p->force_x3 && p->variant != 6 && p->variant != 7)
-        return launch_v8<Q>(p, in, hin, hout, out, n_out, s);
+        return p->variant == 8 ? launch_v8<Q>(p, in, hin, hout, out, n_out, s) : launch_v9<Q>(p, in, hin, hout, out, n_out, s);
     switch (p->variant) {
     case 6: return launch_v2<Q, 1>(p, in, hin, hout, out, n_out, s, 2);
     case 7: return launch_v2<Q, 2>(p, in, hin, hout, out, n_out, s, 2);
@@ -1579,7 +1891,8 @@ std::string nsh_fir_mfma_kernel_name(const nsh_fir_plan* p)
     };
     if (p->algo == NSH_FIR_MFMA16) return t("k_fir_mfma5", p->QH, p->variant == 20 ? 2 : 1);
     if (p->D > 1) return t("k_fir_mfma7", p->D, p->QHD);
-    if (p->frag8_dev && !p->force_x3 && p->variant != 6 && p->variant != 7) return t("k_fir_mfma8", p->Q);
+    if (p->frag8_dev && !p->force_x3 && p->variant != 6 && p->variant != 7)
+        return t(p->variant == 8 ? "k_fir_mfma8" : "k_fir_mfma9", p->Q);
     if (p->variant >= 20) return t("k_fir_mfma5", p->QH, p->variant == 20 ? 2 : 1);
     return t("k_fir_mfma2", p->Q, p->variant == 6 ? 1 : 2);
 }

@@ -2,6 +2,7 @@
 (no compute calls -- there is no GPU in the build container)."""
 import ctypes
 import os
+import shutil
 import re
 import subprocess
 
@@ -42,8 +43,10 @@ def test_hip_shim_loads_and_reports():
 def test_hip_shim_is_gfx950_code_object(tmp_path):
     from newsched_amd import nsh
 
-    # --offloading extracts the bundled code objects into the working directory
-    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", os.path.abspath(nsh.HIP_LIB)],
+    # --offloading extracts the bundled code objects next to its input: run it on a copy
+    lib = tmp_path / os.path.basename(nsh.HIP_LIB)
+    shutil.copyfile(nsh.HIP_LIB, lib)
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", str(lib)],
                          capture_output=True, text=True, cwd=tmp_path)
     if out.returncode != 0:
         pytest.skip("llvm-objdump --offloading unavailable")

@@ -114,7 +114,7 @@ def test_add_mul_cc_bit_exact(torch_cuda, n):
     np.testing.assert_array_equal(host(dy), orc.mul_cc(a, b))
 
 
-# "mfma" is the default matrix-core kernel (decim 1: per-chunk scaled fp16x2, k_fir_mfma8),
+# "mfma" is the default matrix-core kernel (decim 1: per-chunk scaled fp16x2, k_fir_mfma9),
 # "mfma_x3" forces the bf16x3 six-product kernel (k_fir_mfma2), "mfma16" the 16-sample form.
 ALGOS = [("direct", nsh.FIR_DIRECT), ("mfma", nsh.FIR_MFMA), ("mfma_x3", nsh.FIR_MFMA_BF16X3),
          ("mfma16", nsh.FIR_MFMA16)]
@@ -138,7 +138,7 @@ def test_fir127_golden(torch_cuda, golden, name, algo):
     plan = nsh.FirPlan(g["taps"], 1, algo)
     assert plan.algo == algo
     if name == "mfma":
-        assert plan.kernel == "k_fir_mfma8<5>", plan.kernel
+        assert plan.kernel == "k_fir_mfma9<5>", plan.kernel
     y, hist = run_fir(torch, plan, g["x"], g["x"].size)
     ok, err, scale = orc.tol_ok(y, g["y"])
     assert ok, (name, err, scale)
@@ -295,8 +295,26 @@ def _assert_nonfinite_pattern(y, ref):
     np.testing.assert_array_equal(np.sign(y.imag[inf]), np.sign(ref.imag[inf]))
 
 
-def test_fir_mfma_nonfinite_inputs(torch_cuda):
-    """k_fir_mfma8 sends chunks holding inf/NaN (and their successors, whose halo and scale
+@pytest.fixture(params=["v9", "v8"])
+def v8_form(request, monkeypatch):
+    """Both fp16x2 kernels: k_fir_mfma9 (default: exact-path decision per chunk from the
+    reductions, exact chunks staged raw in LDS) and k_fir_mfma8 (per-sample tests, exact
+    path from global memory; NSH_FIR_MFMA_VARIANT=8)."""
+    if request.param == "v8":
+        monkeypatch.setenv("NSH_FIR_MFMA_VARIANT", "8")
+    else:
+        monkeypatch.delenv("NSH_FIR_MFMA_VARIANT", raising=False)
+    return request.param
+
+
+def _v8_plan(h, form):
+    plan = nsh.FirPlan(h, 1, nsh.FIR_MFMA)
+    assert plan.kernel == ("k_fir_mfma9<5>" if form == "v9" else "k_fir_mfma8<5>"), plan.kernel
+    return plan
+
+
+def test_fir_mfma_nonfinite_inputs(torch_cuda, v8_form):
+    """The fp16x2 kernels send chunks holding inf/NaN (and their successors, whose halo and scale
     include them) through the fp32 direct form in the same launch: the inf/NaN pattern of
     every output equals the oracle's (IEEE double), and finite outputs meet the tolerance."""
     torch = torch_cuda
@@ -306,7 +324,7 @@ def test_fir_mfma_nonfinite_inputs(torch_cuda):
     x[20_000] = np.complex64(complex(np.nan, 0.0))
     x[30_000] = np.complex64(complex(0.25, -np.inf))
     x[30_050] = np.complex64(complex(-np.inf, np.inf))
-    y, _ = run_fir(torch, nsh.FirPlan(h, 1, nsh.FIR_MFMA), x, x.size)
+    y, _ = run_fir(torch, _v8_plan(h, v8_form), x, x.size)
     ref = orc.fir_ccf(x, h)
     _assert_nonfinite_pattern(y, ref)
     fin = np.isfinite(ref.real) & np.isfinite(ref.imag)
@@ -314,7 +332,7 @@ def test_fir_mfma_nonfinite_inputs(torch_cuda):
     assert ok, (err, scale)
 
 
-def test_fir_mfma_wide_dynamic_range(torch_cuda):
+def test_fir_mfma_wide_dynamic_range(torch_cuda, v8_form):
     """One sample 2^60 above the rest: the samples sharing its chunk (and the next one)
     would flush to zero in fp16 at the spike's scale, so those chunks take the exact path.
     Outputs away from the spike are checked against the oracle on their own scale."""
@@ -322,14 +340,14 @@ def test_fir_mfma_wide_dynamic_range(torch_cuda):
     h = _firwin127()
     x = orc.synth(40_000, 21)
     x[10_000] *= np.float32(2.0 ** 60)
-    y, _ = run_fir(torch, nsh.FirPlan(h, 1, nsh.FIR_MFMA), x, x.size)
+    y, _ = run_fir(torch, _v8_plan(h, v8_form), x, x.size)
     ref = orc.fir_ccf(x, h)
     for a, b in ((0, 10_000), (10_000, 10_127), (10_127, 40_000)):
         ok, err, scale = orc.tol_ok(y[a:b], ref[a:b])
         assert ok, (a, b, err, scale)
 
 
-def test_fir_mfma_per_chunk_scale(torch_cuda):
+def test_fir_mfma_per_chunk_scale(torch_cuda, v8_form):
     """Segments at amplitudes 1e-30, 1 and 1e30 (each far outside fp16's range unscaled):
     the per-chunk power-of-two scale keeps every segment at fp32 accuracy, checked on the
     segment's own scale; chunks mixing two amplitudes take the exact path."""
@@ -339,11 +357,28 @@ def test_fir_mfma_per_chunk_scale(torch_cuda):
     x = orc.synth(3 * seg, 33)
     x[:seg] *= np.float32(1e-30)
     x[2 * seg:] *= np.float32(1e30)
-    y, _ = run_fir(torch, nsh.FirPlan(h, 1, nsh.FIR_MFMA), x, x.size)
+    y, _ = run_fir(torch, _v8_plan(h, v8_form), x, x.size)
     ref = orc.fir_ccf(x, h)
     for a, b in ((0, seg), (seg + 127, 2 * seg), (2 * seg + 127, 3 * seg)):
         ok, err, scale = orc.tol_ok(y[a:b], ref[a:b])
         assert ok, (a, b, err, scale)
+
+
+def test_fir_mfma_tiny_and_zero_chunks(torch_cuda, v8_form):
+    """All-zero chunks, an fp32-subnormal sample and a sample 2^-30 below its chunk maximum
+    (fp16-subnormal after scaling: that chunk and its successor take the exact path), and
+    a stream that ends inside a chunk: every output meets the tolerance, zeros stay zero."""
+    torch = torch_cuda
+    h = _firwin127()
+    x = orc.synth(30_001, 77)
+    x[2048:3 * 2048 + 100] = 0                       # zero chunks (and a zero halo)
+    x[9000] = np.complex64(complex(1e-40, -3e-41))  # fp32 subnormal among O(1) samples
+    x[15_000] = np.complex64(complex(2.0 ** -30, 0.0))
+    y, _ = run_fir(torch, _v8_plan(h, v8_form), x, x.size)
+    ref = orc.fir_ccf(x, h)
+    ok, err, scale = orc.tol_ok(y, ref)
+    assert ok, (err, scale)
+    assert not np.any(y[2048 + 126:3 * 2048 + 100])
 
 
 def test_fir_mfma_taps_far_below_max(torch_cuda):
@@ -355,7 +390,7 @@ def test_fir_mfma_taps_far_below_max(torch_cuda):
     h[5] = np.float32(h.max() * 2.0 ** -40)
     x = orc.synth(30_000, 4)
     plan = nsh.FirPlan(h, 1, nsh.FIR_MFMA)
-    assert plan.kernel == "k_fir_mfma8<5>", plan.kernel
+    assert plan.kernel == "k_fir_mfma9<5>", plan.kernel
     y, _ = run_fir(torch, plan, x, x.size)
     ok, err, scale = orc.tol_ok(y, orc.fir_ccf(x, h))
     assert ok, (err, scale)
@@ -364,14 +399,14 @@ def test_fir_mfma_taps_far_below_max(torch_cuda):
 def test_fir_plan_kernels():
     """Which kernel each algorithm runs (no silent fallback between the MFMA forms)."""
     h = _firwin127()
-    assert nsh.FirPlan(h, 1, nsh.FIR_MFMA).kernel == "k_fir_mfma8<5>"
-    assert nsh.FirPlan(h, 1, nsh.FIR_AUTO).kernel == "k_fir_mfma8<5>"
+    assert nsh.FirPlan(h, 1, nsh.FIR_MFMA).kernel == "k_fir_mfma9<5>"
+    assert nsh.FirPlan(h, 1, nsh.FIR_AUTO).kernel == "k_fir_mfma9<5>"
     assert nsh.FirPlan(h, 1, nsh.FIR_MFMA_BF16X3).kernel == "k_fir_mfma2<5,2>"
     assert nsh.FirPlan(h, 1, nsh.FIR_MFMA16).kernel == "k_fir_mfma5<9,1>"
     assert nsh.FirPlan(h, 1, nsh.FIR_DIRECT).kernel == "k_fir_direct<1,8>"
     assert nsh.FirPlan(h, 2, nsh.FIR_MFMA).kernel == "k_fir_mfma7<2,5>"
     for L in (1, 17, 33, 65, 97, 129, 161):
-        assert nsh.FirPlan(np.ones(L, np.float32), 1, nsh.FIR_MFMA).kernel == "k_fir_mfma8<%d>" % ((L + 30) // 32 + 1)
+        assert nsh.FirPlan(np.ones(L, np.float32), 1, nsh.FIR_MFMA).kernel == "k_fir_mfma9<%d>" % ((L + 30) // 32 + 1)
 
 
 def test_fft_golden(torch_cuda, golden):

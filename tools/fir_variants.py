@@ -1,5 +1,5 @@
 """A/B the MFMA FIR kernel variants in one process (interleaved rounds), 2^25-sample
-launches: NSH_FIR_MFMA_VARIANT 6 = v2 depth 1, 7 = v2 depth 2 (default), 20-22 = the
+launches (LOG2N): NSH_FIR_MFMA_VARIANT 0 = default (k_fir_mfma8 LEAN), 8 = k_fir_mfma8 per-sample tests, 6/7 = bf16x3 v2 depth 1/2, 20-22 = the
 16-sample form. Checks each variant against the oracle on a window and against the first
 variant over the whole output."""
 import os
@@ -13,7 +13,7 @@ import torch
 from newsched_amd import nsh
 from oracle import oracle as orc
 
-n = 1 << 25
+n = 1 << int(os.environ.get("LOG2N", "25"))
 h = ss.firwin(127, 0.2).astype(np.float32)
 x = torch.empty(n, dtype=torch.complex64, device="cuda")
 nsh.synth(x, n, 0)

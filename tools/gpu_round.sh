@@ -1,7 +1,14 @@
+#!/bin/bash
+# One GPU-box pass over everything the round's numbers come from. Usage: tools/gpu_round.sh TAG
+# (run via gpurun). Every GPU step has its own time limit; steps are chained with && so the
+# first failure ends the call.
 set -o pipefail
-mkdir -p gpurun_out/r01b
+TAG=${1:-r01}
+O=gpurun_out/$TAG
+mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/r01b/pytest_gpu.log 2>&1 && echo "pytest ok" &&
-timeout -k 10 300 python bench.py > gpurun_out/r01b/bench.json 2> gpurun_out/r01b/bench.err && echo "bench ok" &&
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r01b/prof -o bench --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu > gpurun_out/r01b/bench_under_rocprof.json 2> gpurun_out/r01b/rocprof.err && echo "rocprof ok" &&
-tools/pmc_fir.sh gpurun_out/r01b/pmc && python3 tools/pmc_summary.py gpurun_out/r01b/pmc $((1<<25)) gpurun_out/r01b/pmc_fir.json > /dev/null && echo "pmc ok"
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 && echo "pytest ok" &&
+timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && echo "smoke ok" &&
+timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err && echo "bench ok" &&
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o bench --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu > $O/bench_under_rocprof.json 2> $O/rocprof.err && echo "rocprof ok" &&
+tools/pmc_fir.sh $O/pmc && python3 tools/pmc_summary.py $O/pmc $((1<<25)) $O/pmc_fir.json > /dev/null && echo "pmc ok"

@@ -20,6 +20,18 @@ def load(d):
     return rows
 
 
+def kernel_key(name):
+    """'k_fir_mfma8<5>' from a demangled or an Itanium-mangled kernel name (rocprofv3 reports
+    either, depending on the kernel's linkage), 'k_copy_v4' for the calibration copy."""
+    m = re.search(r"(k_fir_\w+<[^>(]*>|k_copy_v4)", name)
+    if m:
+        return m.group(1).replace(" ", "")
+    m = re.search(r"\d(k_fir_[a-z0-9_]+?)I((?:L[ib]-?\d+E)+)E", name)
+    if m:
+        return "%s<%s>" % (m.group(1), ",".join(re.findall(r"L[ib](-?\d+)E", m.group(2))))
+    return None
+
+
 def main(root, n_samples, out_json):
     acc = defaultdict(lambda: defaultdict(float))
     disp = defaultdict(set)
@@ -28,11 +40,10 @@ def main(root, n_samples, out_json):
             continue
         for r in load(p):
             k = r["Kernel_Name"]
-            # key: the kernel template name, as nsh_fir_plan_kernel() reports it ("k_fir_mfma8<5>")
-            m = re.search(r"(k_fir_\w+<[^>(]*>|k_copy_v4)", k)
-            if m is None:
+            # key: the kernel template name, as nsh_fir_plan_kernel() reports it ("k_fir_mfma9<5>")
+            short = kernel_key(k)
+            if short is None:
                 continue
-            short = m.group(1).replace(" ", "")
             acc[short][r["Counter_Name"]] += float(r["Counter_Value"])
             disp[(short, r["Counter_Name"])].add(r["Dispatch_Id"])
     summ = {}
