@@ -111,7 +111,7 @@ enum nsh_fir_algo { NSH_FIR_AUTO = 0, NSH_FIR_DIRECT = 1, NSH_FIR_MFMA = 2, NSH_
 int nsh_fir_plan_create(int dev, const float* taps_host, int ntaps, int decim, int algo, void** plan);
 int nsh_fir_plan_destroy(void* plan);
 int nsh_fir_plan_algo(void* plan);          /* the algorithm AUTO resolved to */
-const char* nsh_fir_plan_kernel(void* plan); /* the kernel nsh_fir_ccf launches, e.g. "k_fir_mfma8<5>" */
+const char* nsh_fir_plan_kernel(void* plan); /* the kernel nsh_fir_ccf launches, e.g. "k_fir_mfma9<5>" */
 int nsh_fir_ccf(void* plan, const float* in, const float* hist_in, float* hist_out,
                 float* out, int64_t n_out, void* stream);
 

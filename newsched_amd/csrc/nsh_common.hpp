@@ -48,6 +48,42 @@ __device__ __forceinline__ void lds_barrier()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
+// Raw buffer resource over chunk ch of a stream of n items (8 B each), chunk = CH items:
+// [base + CH ch, + min(n - CH ch, CH) items), at least 0. Out-of-range lanes read 0 and their
+// stores are dropped, so a streaming step issues the same loads and stores for a full chunk
+// and for the stream's partial last one: no per-sample branches, and the compiler's vmcnt
+// waits count exactly. Built from wave-uniform values only (no waterfall loops).
+template <int CH>
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t chunk_rsrc(const float2* base, int64_t ch, int64_t n)
+{
+    int64_t items = n - ch * CH;
+    items = items < 0 ? 0 : (items > CH ? CH : items);
+    const uint64_t a = (uint64_t)(base + ch * CH);
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+    const int bytes = __builtin_amdgcn_readfirstlane((int)(items * 8));
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0, bytes, 0x00020000);
+}
+constexpr int AUX_NT = 2; // gfx950 cache policy bits: nt (streaming)
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef float buf_f4 __attribute__((ext_vector_type(4)));
+typedef float buf_f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float4 buf_load_f4(__amdgpu_buffer_rsrc_t r, int byte_off)
+{
+    const buf_f4 t = __builtin_bit_cast(buf_f4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, AUX_NT));
+    return make_float4(t.x, t.y, t.z, t.w);
+}
+__device__ __forceinline__ void buf_store_f2(__amdgpu_buffer_rsrc_t r, int byte_off, buf_f2 v)
+{
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, byte_off, 0, AUX_NT);
+}
+
+__device__ __forceinline__ float2 buf_load_f2(__amdgpu_buffer_rsrc_t r, int byte_off)
+{
+    const buf_f2 t = __builtin_bit_cast(buf_f2, __builtin_amdgcn_raw_buffer_load_b64(r, byte_off, 0, AUX_NT));
+    return make_float2(t.x, t.y);
+}
+
 } // namespace nsh
 
 #define NSH_CK(expr)                                                    \

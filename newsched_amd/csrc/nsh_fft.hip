@@ -148,17 +148,23 @@ __device__ __forceinline__ void fft_wave(float2 (&v)[16], float2* __restrict__ i
     for (int m = 0; m < 16; ++m) v[m] = o[m];
 }
 
-__device__ __forceinline__ void load_frame16(float2 (&v)[16], const float2* __restrict__ src)
+// Frame f of a stream of nframes frames by buffer loads/stores over that frame alone: a frame
+// past the end reads zeros and drops its stores, so the loop issues the same memory
+// instructions every iteration (no conditional prefetch) and the compiler's vmcnt waits stay
+// exact -- the next frame's loads remain in flight across this frame's transform and stores.
+__device__ __forceinline__ void load_frame16(float2 (&v)[16], const float2* __restrict__ in, int64_t f, int64_t nframes)
 {
     const int j = threadIdx.x & 63;
+    const __amdgpu_buffer_rsrc_t r = nsh::chunk_rsrc<N>(in, f, nframes * N);
 #pragma unroll
-    for (int m = 0; m < 16; ++m) v[m] = src[j + 64 * m];
+    for (int m = 0; m < 16; ++m) v[m] = nsh::buf_load_f2(r, (j + 64 * m) * 8);
 }
-__device__ __forceinline__ void store_frame16(const float2 (&v)[16], float2* __restrict__ dst)
+__device__ __forceinline__ void store_frame16(const float2 (&v)[16], float2* __restrict__ out, int64_t f, int64_t nframes)
 {
     const int j = threadIdx.x & 63;
+    const __amdgpu_buffer_rsrc_t r = nsh::chunk_rsrc<N>(out, f, nframes * N);
 #pragma unroll
-    for (int m = 0; m < 16; ++m) dst[j + 64 * m] = v[m];
+    for (int m = 0; m < 16; ++m) nsh::buf_store_f2(r, (j + 64 * m) * 8, nsh::buf_f2{ v[m].x, v[m].y });
 }
 
 constexpr int FPW = NT / 64; // frames (waves) per workgroup
@@ -176,12 +182,11 @@ __global__ __launch_bounds__(NT) void k_fft1024(const float2* __restrict__ in, f
     int64_t f = (int64_t)blockIdx.x * FPW + (threadIdx.x >> 6);
     if (f >= nframes) return;
     float2 v[16], nx[16];
-    load_frame16(v, in + f * N);
+    load_frame16(v, in, f, nframes);
     for (; f < nframes; f += stride) {
-        const int64_t fn = f + stride;
-        if (fn < nframes) load_frame16(nx, in + fn * N);
+        load_frame16(nx, in, f + stride, nframes);
         fft_wave<INV>(v, img, tw);
-        store_frame16(v, out + f * N);
+        store_frame16(v, out, f, nframes);
 #pragma unroll
         for (int m = 0; m < 16; ++m) v[m] = nx[m];
     }
@@ -203,15 +208,14 @@ __global__ __launch_bounds__(NT) void k_chan1024(const float2* __restrict__ in, 
     int64_t f = (int64_t)blockIdx.x * FPW + (threadIdx.x >> 6);
     if (f >= nframes) return;
     float2 v[16], nx[16];
-    load_frame16(v, in + f * N);
+    load_frame16(v, in, f, nframes);
     for (; f < nframes; f += stride) {
-        const int64_t fn = f + stride;
-        if (fn < nframes) load_frame16(nx, in + fn * N);
+        load_frame16(nx, in, f + stride, nframes);
         fft_wave<false>(v, img, tw);
 #pragma unroll
         for (int m = 0; m < 16; ++m) v[m] = cmul(v[m], wr[m]);
         fft_wave<true>(v, img, tw);
-        store_frame16(v, out + f * N);
+        store_frame16(v, out, f, nframes);
 #pragma unroll
         for (int m = 0; m < 16; ++m) v[m] = nx[m];
     }

@@ -53,6 +53,12 @@
 
 namespace {
 
+using nsh::AUX_NT;
+using nsh::buf_load_f4;
+using nsh::buf_store_f2;
+using nsh::chunk_rsrc;
+using nsh::u32x2;
+
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
@@ -782,36 +788,18 @@ __device__ __forceinline__ void v7_store_pair(unsigned char* buf, int r, int s, 
 }
 
 // Registers: thread t holds input samples [2D (t + 256 u'), 2D (t + 256 u') + 2D) of the
-// chunk, u' < UNITS, as D float4 each (2 samples per float4).
+// chunk, u' < UNITS, as D float4 each (2 samples per float4). Buffer loads (chunk_rsrc): the
+// streaming loop's form.
 template <int D, int QH>
-__device__ __forceinline__ void v7_load_main(float4 (&v)[4], const float2* __restrict__ in,
-                                             const float2* __restrict__ hist, int64_t ch, int64_t n_in, int L,
-                                             bool in_aligned)
+__device__ __forceinline__ void v7_load_buf(float4 (&v)[4], const float2* __restrict__ in, int64_t ch, int64_t n_in)
 {
     using G = geom7<D, QH>;
-    const int64_t g0 = ch * G::CHUNK_IN;
-    if (in_aligned && g0 + G::CHUNK_IN <= n_in) {
-        const nf4* src = reinterpret_cast<const nf4*>(in + g0);
+    const __amdgpu_buffer_rsrc_t r = chunk_rsrc<G::CHUNK_IN>(in, ch, n_in);
 #pragma unroll
-        for (int u = 0; u < G::UNITS; ++u)
+    for (int u = 0; u < G::UNITS; ++u)
 #pragma unroll
-            for (int f = 0; f < D; ++f) {
-                const nf4 t = __builtin_nontemporal_load(src + (threadIdx.x + G::NT * u) * D + f);
-                v[u * D + f] = make_float4(t.x, t.y, t.z, t.w);
-            }
-    } else {
-#pragma unroll
-        for (int u = 0; u < G::UNITS; ++u)
-#pragma unroll
-            for (int f = 0; f < D; ++f) {
-                const int64_t l = (int64_t)((threadIdx.x + G::NT * u) * D + f) * 2;
-                const float2 a = virt(in, hist, g0 + l, n_in, L);
-                const float2 b = virt(in, hist, g0 + l + 1, n_in, L);
-                v[u * D + f] = make_float4(a.x, a.y, b.x, b.y);
-            }
-    }
+        for (int f = 0; f < D; ++f) v[u * D + f] = buf_load_f4(r, ((threadIdx.x + G::NT * u) * D + f) * 16);
 }
-
 __device__ __forceinline__ float2 f4_sample(const float4& v, int which)
 {
     return which ? make_float2(v.z, v.w) : make_float2(v.x, v.y);
@@ -879,10 +867,11 @@ __device__ __forceinline__ void v7_load_store_halo(unsigned char* buf, const flo
 
 template <int D, int QH>
 __device__ __forceinline__ void v7_compute(const unsigned char* lds, const bf16x8 (&B)[D][3][QH / 2 + 1],
-                                           const bf16x4 (&T)[D][3], int64_t n_tile, int64_t n_out,
+                                           const bf16x4 (&T)[D][3], int64_t ch, int64_t n_out,
                                            float2* __restrict__ out)
 {
     using G = geom7<D, QH>;
+    const __amdgpu_buffer_rsrc_t ro = chunk_rsrc<G::CHUNK>(out, ch, n_out);
     typedef float f32x4 __attribute__((ext_vector_type(4)));
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -940,12 +929,9 @@ __device__ __forceinline__ void v7_compute(const unsigned char* lds, const bf16x
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
             const int blk = t * 8 + 2 * g + half;
-            const int64_t n = n_tile + (int64_t)wave * G::WAVE_OUT + blk * 16 + phase;
-            if (n < n_out) {
-                nf2 o = { (hi[t][2 * half] + hi_t[t][2 * half]) + (lo[t][2 * half] + lo_t[t][2 * half]),
-                          (hi[t][2 * half + 1] + hi_t[t][2 * half + 1]) + (lo[t][2 * half + 1] + lo_t[t][2 * half + 1]) };
-                __builtin_nontemporal_store(o, reinterpret_cast<nf2*>(out + n));
-            }
+            nf2 o = { (hi[t][2 * half] + hi_t[t][2 * half]) + (lo[t][2 * half] + lo_t[t][2 * half]),
+                      (hi[t][2 * half + 1] + hi_t[t][2 * half + 1]) + (lo[t][2 * half + 1] + lo_t[t][2 * half + 1]) };
+            buf_store_f2(ro, (wave * G::WAVE_OUT + blk * 16 + phase) * 8, o);
         }
     }
 }
@@ -957,8 +943,7 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma7(const float2* __restrict__
                                                      float2* __restrict__ out,
                                                      const unsigned short* __restrict__ frag,
                                                      int L,
-                                                     int64_t n_out,
-                                                     int in_aligned)
+                                                     int64_t n_out)
 {
     using G = geom7<D, QH>;
     constexpr int KS = G::KS;
@@ -992,24 +977,23 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma7(const float2* __restrict__
     const int64_t c_end = c_begin + per < nchunks ? c_begin + per : nchunks;
     if (c_begin >= c_end) return;
     const int64_t c_last = c_end - 1;
-    const bool al = in_aligned != 0;
     auto clamp = [&](int64_t x) { return x <= c_last ? x : c_last; };
 
     float4 va[G::VPT], vb[G::VPT];
     v7_load_store_halo<D, QH>(lds, in, hist_in, c_begin, n_in, L);
-    v7_load_main<D, QH>(va, in, hist_in, c_begin, n_in, L, al);
+    v7_load_buf<D, QH>(va, in, c_begin, n_in);
     v7_store_main<D, QH>(va, lds);
-    v7_load_main<D, QH>(va, in, hist_in, clamp(c_begin + 1), n_in, L, al);
-    __syncthreads();
+    v7_load_buf<D, QH>(va, in, clamp(c_begin + 1), n_in);
+    nsh::lds_barrier(); // LDS only: keep the chunk ch+2 loads in flight
 
     auto step = [&](float4 (&nxt)[G::VPT], float4 (&ld)[G::VPT], int64_t ch) {
         unsigned char* cur = lds + ((ch - c_begin) & 1) * G::BUF;
         unsigned char* nbuf = lds + (((ch - c_begin) & 1) ^ 1) * G::BUF;
-        v7_load_main<D, QH>(ld, in, hist_in, clamp(ch + 2), n_in, L, al);
+        v7_load_buf<D, QH>(ld, in, clamp(ch + 2), n_in);
         v7_copy_halo<D, QH>(cur, nbuf);
         v7_store_main<D, QH>(nxt, nbuf);
-        v7_compute<D, QH>(cur, B, T, ch * G::CHUNK, n_out, out);
-        __syncthreads();
+        v7_compute<D, QH>(cur, B, T, ch, n_out, out);
+        nsh::lds_barrier(); // LDS only: keep the chunk ch+2 loads in flight
     };
     int64_t ch = c_begin;
     for (; ch + 1 <= c_last; ch += 2) {
@@ -1035,9 +1019,8 @@ int launch_v7(const nsh_fir_plan* p, const float2* in, const float2* hin, float2
     const int wg_per_cu = (160 * 1024) / G::LDS >= 3 ? 3 : 2; // LDS-bound residency (VGPRs allow 3)
     const int64_t max_grid = (int64_t)n_cu * wg_per_cu;
     const unsigned grid = (unsigned)(nchunks < max_grid ? nchunks : max_grid);
-    const int aligned = ((uintptr_t)in % 16 == 0) ? 1 : 0;
     hipLaunchKernelGGL((k_fir_mfma7<D, QH>), dim3(grid), dim3(G::NT), G::LDS, s, in, hin, hout, out,
-                       (const unsigned short*)p->fragd_dev, p->L, n_out, aligned);
+                       (const unsigned short*)p->fragd_dev, p->L, n_out);
     NSH_CK_LAUNCH("nsh_fir_ccf(mfma decim)");
     return 0;
 }
@@ -1362,30 +1345,12 @@ __device__ __forceinline__ bool chunk_needs_exact(unsigned maxbits, unsigned mnz
     return __builtin_ldexpf(__uint_as_float(mnz1 + 1u), s) < 6.103515625e-05f; // 2^-14
 }
 
-// Raw buffer resource over chunk ch of a stream: [base + 2048 ch, + min(n - 2048 ch, 2048)
-// items), at least 0. Built from wave-uniform values only (no waterfall loops).
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t chunk_rsrc(const float2* base, int64_t ch, int64_t n)
-{
-    int64_t items = n - ch * 2048;
-    items = items < 0 ? 0 : (items > 2048 ? 2048 : items);
-    const uint64_t a = (uint64_t)(base + ch * 2048);
-    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
-    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
-    const int bytes = __builtin_amdgcn_readfirstlane((int)(items * 8));
-    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0, bytes, 0x00020000);
-}
-constexpr int AUX_NT = 2; // gfx950 cache policy bits: nt (streaming)
-typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-
 // chunk ch -> registers: lane t holds samples (2t, 2t+1) + 512 u, u < 4
 __device__ __forceinline__ void load_chunk9(float4 (&v)[4], const float2* __restrict__ in, int64_t ch, int64_t n_in)
 {
-    const __amdgpu_buffer_rsrc_t r = chunk_rsrc(in, ch, n_in);
+    const __amdgpu_buffer_rsrc_t r = chunk_rsrc<2048>(in, ch, n_in);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        const nf4 t = __builtin_bit_cast(nf4, __builtin_amdgcn_raw_buffer_load_b128(r, (threadIdx.x + 256 * u) * 16, 0, AUX_NT));
-        v[u] = make_float4(t.x, t.y, t.z, t.w);
-    }
+    for (int u = 0; u < 4; ++u) v[u] = buf_load_f4(r, (threadIdx.x + 256 * u) * 16);
 }
 
 // split without the per-sample test (k_fir_mfma9 decides per chunk)
@@ -1524,13 +1489,10 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma9(const float2* __restrict__
         z = wave_min(z);
     };
     auto store_tile = [&](int64_t ch, const nf2 (&o)[8]) {
-        const __amdgpu_buffer_rsrc_t r = chunk_rsrc(out, ch, n_out);
+        const __amdgpu_buffer_rsrc_t r = chunk_rsrc<2048>(out, ch, n_out);
         const int base = wave * TILE + phase;
 #pragma unroll
-        for (int reg = 0; reg < 8; ++reg) {
-            const int blk = (reg & 3) + 8 * (reg >> 2) + 4 * h;
-            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, o[reg]), r, (base + 32 * blk) * 8, 0, AUX_NT);
-        }
+        for (int reg = 0; reg < 8; ++reg) buf_store_f2(r, (base + 32 * ((reg & 3) + 8 * (reg >> 2) + 4 * h)) * 8, o[reg]);
     };
 
     // ---- prologue: chunk c_begin (its halo from global memory / history), +1, +2 in flight
