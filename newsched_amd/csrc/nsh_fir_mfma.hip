@@ -1579,6 +1579,285 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma9(const float2* __restrict__
     if (ch <= c_last) step(vb, vc, va, ch);
 }
 
+// ---- k_fir_mfma10: the fp16x2 split on 16-sample blocks (v_mfma_f32_16x16x32_f16) ----------
+// k_fir_mfma9's pipeline (per-chunk scale, exact chunks staged raw in LDS, buffer ops, LDS-only
+// barriers) on k_fir_mfma5's Toeplitz tiling: output n = 16 beta + i,
+// y = sum_q sum_r h[i - r + 16 q] x[16 (beta - q) + r], K = 16 QH (144 for 127 taps instead of
+// 160), a 16x16x16 MFMA for an odd last block. Rows of A are (component, block) pairs; each
+// 16-sample row is 32 B per plane (hi, lo), re and im planes 128 B apart mod 256 (k_fir_mfma5's
+// conflict-free ds_read_b128 layout with two planes instead of three).
+typedef __attribute__((ext_vector_type(4))) _Float16 f16x4;
+
+template <int QH>
+struct geom10 {
+    static constexpr int NT = 256;
+    static constexpr int CHUNK = 2048;
+    static constexpr int KS = QH / 2;
+    static constexpr int TAIL = QH % 2;
+    static constexpr int H = 16 * (QH - 1);
+    static constexpr int HR = QH - 1;
+    static constexpr int HP = H / 2;
+    static constexpr int NB = (CHUNK + H) / 16;
+    static constexpr int PLANE = NB * 32;
+    static constexpr int IM_OFF = (2 * PLANE + 255) / 256 * 256 + 128;
+    static constexpr int BUF = (IM_OFF + 2 * PLANE + 255) / 256 * 256;
+    static constexpr int STASH = HP * 16;
+    static constexpr int SLOTS = 2 * BUF + 2 * STASH;
+    static constexpr int LDS = SLOTS + 64; // u32 max[2][4], mnz[2][4]
+    static constexpr int TILES = 4;
+    static_assert((HP + 4 * NT) * 16 <= BUF, "a raw fp32 chunk + halo fits one plane buffer");
+    static_assert(HP <= NT, "halo pairs: one per thread");
+};
+
+template <int QH>
+__device__ __forceinline__ void store_pair10(const float4& v, unsigned char* buf, int s, int sc)
+{
+    using G = geom10<QH>;
+    const int off = (s >> 4) * 32 + (s & 15) * 2;
+    const float ar = __builtin_ldexpf(v.x, sc), br = __builtin_ldexpf(v.z, sc);
+    const float ai = __builtin_ldexpf(v.y, sc), bi = __builtin_ldexpf(v.w, sc);
+    const _Float16 ar0 = (_Float16)ar, br0 = (_Float16)br, ai0 = (_Float16)ai, bi0 = (_Float16)bi;
+    *reinterpret_cast<unsigned*>(buf + off) = __builtin_bit_cast(unsigned, f16x2{ ar0, br0 });
+    *reinterpret_cast<unsigned*>(buf + G::PLANE + off) =
+        __builtin_bit_cast(unsigned, f16x2{ (_Float16)(ar - (float)ar0), (_Float16)(br - (float)br0) });
+    *reinterpret_cast<unsigned*>(buf + G::IM_OFF + off) = __builtin_bit_cast(unsigned, f16x2{ ai0, bi0 });
+    *reinterpret_cast<unsigned*>(buf + G::IM_OFF + G::PLANE + off) =
+        __builtin_bit_cast(unsigned, f16x2{ (_Float16)(ai - (float)ai0), (_Float16)(bi - (float)bi0) });
+}
+
+// The wave's 4 row-tiles (8 blocks each) x (KS k-steps of 32 + an optional tail of 16), three
+// products; lane output (t, half) = block t*8 + 2g + half, sample phase.
+template <int QH>
+__device__ __forceinline__ void mfma_tile10(const unsigned char* lds, const f16x8 (&B0)[geom10<QH>::KS + 1],
+                                            const f16x8 (&B1)[geom10<QH>::KS + 1], const f16x4 (&T0), const f16x4 (&T1),
+                                            int row_base, int g, int unscale, nf2 (&o)[8])
+{
+    using G = geom10<QH>;
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+    f32x4 hi[G::TILES], lo[G::TILES], hi_t[G::TILES], lo_t[G::TILES];
+#pragma unroll
+    for (int t = 0; t < G::TILES; ++t) {
+        hi[t] = f32x4{ 0.f, 0.f, 0.f, 0.f };
+        lo[t] = f32x4{ 0.f, 0.f, 0.f, 0.f };
+        hi_t[t] = f32x4{ 0.f, 0.f, 0.f, 0.f };
+        lo_t[t] = f32x4{ 0.f, 0.f, 0.f, 0.f };
+    }
+#pragma unroll
+    for (int st = 0; st < G::KS; ++st) {
+        const int q = 2 * st + (g >> 1);
+#pragma unroll
+        for (int t = 0; t < G::TILES; ++t) {
+            const int off = row_base + t * 8 * 32 - q * 32 + (g & 1) * 16;
+            const f16x8 A0 = *reinterpret_cast<const f16x8*>(lds + off);
+            const f16x8 A1 = *reinterpret_cast<const f16x8*>(lds + off + G::PLANE);
+            hi[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0, B0[st], hi[t], 0, 0, 0);
+            lo[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0, B1[st], lo[t], 0, 0, 0);
+            lo[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1, B0[st], lo[t], 0, 0, 0);
+        }
+    }
+    // K tail in its own accumulators (16x16x32 -> dependent 16x16x16 hazard, see v5_compute)
+    if constexpr (G::TAIL) {
+#pragma unroll
+        for (int t = 0; t < G::TILES; ++t) {
+            const int off = row_base + t * 8 * 32 - (QH - 1) * 32 + g * 8;
+            const f16x4 A0 = *reinterpret_cast<const f16x4*>(lds + off);
+            const f16x4 A1 = *reinterpret_cast<const f16x4*>(lds + off + G::PLANE);
+            hi_t[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(A0, T0, hi_t[t], 0, 0, 0);
+            lo_t[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(A0, T1, lo_t[t], 0, 0, 0);
+            lo_t[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(A1, T0, lo_t[t], 0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < G::TILES; ++t)
+#pragma unroll
+        for (int half = 0; half < 2; ++half)
+            o[2 * t + half] = nf2{ __builtin_ldexpf((hi[t][2 * half] + hi_t[t][2 * half]) + (lo[t][2 * half] + lo_t[t][2 * half]), unscale),
+                                   __builtin_ldexpf((hi[t][2 * half + 1] + hi_t[t][2 * half + 1]) +
+                                                        (lo[t][2 * half + 1] + lo_t[t][2 * half + 1]), unscale) };
+}
+
+template <int QH>
+__device__ __forceinline__ void direct_tile10(const unsigned char* lds, const float* __restrict__ taps, int L, int wave, int g,
+                                              int phase, nf2 (&o)[8])
+{
+    using G = geom10<QH>;
+    const float2* raw = reinterpret_cast<const float2*>(lds);
+    for (int oi = 0; oi < 8; ++oi) {
+        const int blk = (oi >> 1) * 8 + 2 * g + (oi & 1);
+        const int j = G::H + wave * TILE + blk * 16 + phase;
+        float re = 0.f, im = 0.f;
+        for (int k = 0; k < L; ++k) {
+            const float2 x = raw[j - k];
+            re = fmaf(taps[k], x.x, re);
+            im = fmaf(taps[k], x.y, im);
+        }
+        o[oi] = nf2{ re, im };
+    }
+}
+
+template <int QH>
+__global__ __launch_bounds__(256, 2) void k_fir_mfma10(const float2* __restrict__ in,
+                                                      const float2* __restrict__ hist_in,
+                                                      float2* __restrict__ hist_out,
+                                                      float2* __restrict__ out,
+                                                      const _Float16* __restrict__ frag, // [2][KS][64] x8, [2][64] x4
+                                                      const float* __restrict__ taps,
+                                                      int L,
+                                                      int sh,
+                                                      int64_t n_out)
+{
+    using G = geom10<QH>;
+    constexpr int KS = G::KS;
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    float4* stash = reinterpret_cast<float4*>(lds + 2 * G::BUF);
+    unsigned* slot_max = reinterpret_cast<unsigned*>(lds + G::SLOTS);
+    unsigned* slot_mnz = slot_max + 8;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int64_t n_in = n_out;
+
+    if (blockIdx.x == 0) {
+        for (int j = tid; j < L - 1; j += G::NT) hist_out[j] = virt(in, hist_in, n_in - (L - 1) + j, n_in, L);
+    }
+
+    f16x8 B0[KS + 1], B1[KS + 1];
+#pragma unroll
+    for (int st = 0; st < KS; ++st) {
+        B0[st] = reinterpret_cast<const f16x8*>(frag)[(0 * KS + st) * 64 + lane];
+        B1[st] = reinterpret_cast<const f16x8*>(frag)[(1 * KS + st) * 64 + lane];
+    }
+    f16x4 T0 = {}, T1 = {};
+    if constexpr (G::TAIL) {
+        const f16x4* tf = reinterpret_cast<const f16x4*>(frag + 2 * KS * 64 * 8);
+        T0 = tf[lane];
+        T1 = tf[64 + lane];
+    }
+
+    const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
+    const int64_t per = (nchunks + gridDim.x - 1) / gridDim.x;
+    const int64_t c_begin = (int64_t)blockIdx.x * per;
+    const int64_t c_end = c_begin + per < nchunks ? c_begin + per : nchunks;
+    if (c_begin >= c_end) return;
+    const int64_t c_last = c_end - 1;
+
+    const int rho = lane & 15;
+    const int c = rho & 1, b = rho >> 1;
+    const int g = lane >> 4;
+    const int phase = lane & 15;
+    const int row_base = c * G::IM_OFF + (G::HR + wave * 32 + b) * 32;
+    const bool tail_owner = tid >= G::NT - G::HP;
+    auto clamp = [&](int64_t x) { return x <= c_last ? x : c_last; };
+    auto put_chunk = [&](unsigned char* buf, const float4& halo, const float4 (&v)[4], bool raw, int sc) {
+        if (raw) {
+            float4* r = reinterpret_cast<float4*>(buf);
+            if (G::HP > 0 && tid < G::HP) r[tid] = halo;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) r[G::HP + tid + G::NT * u] = v[u];
+        } else {
+            if (G::HP > 0 && tid < G::HP) store_pair10<QH>(halo, buf, 2 * tid, sc);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) store_pair10<QH>(v[u], buf, G::H + 2 * (tid + G::NT * u), sc);
+        }
+    };
+    auto reduce = [&](const float4 (&v)[4], unsigned& m, unsigned& z) {
+        m = 0;
+        z = ~0u;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            m = max(m, max_mag(v[u]));
+            z = min(z, min_nz1(v[u]));
+        }
+        m = wave_max(m);
+        z = wave_min(z);
+    };
+    auto store_tile = [&](int64_t ch, const nf2 (&o)[8]) {
+        const __amdgpu_buffer_rsrc_t r = chunk_rsrc<2048>(out, ch, n_out);
+        const int base = wave * TILE + phase;
+#pragma unroll
+        for (int oi = 0; oi < 8; ++oi) buf_store_f2(r, (base + ((oi >> 1) * 8 + 2 * g + (oi & 1)) * 16) * 8, o[oi]);
+    };
+
+    float4 va[4], vb[4], vc[4];
+    float4 hv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (G::HP > 0 && tid < G::HP) {
+        const int64_t gg = c_begin * G::CHUNK - G::H + 2 * tid;
+        const float2 x0 = virt(in, hist_in, gg, n_in, L), x1 = virt(in, hist_in, gg + 1, n_in, L);
+        hv = make_float4(x0.x, x0.y, x1.x, x1.y);
+    }
+    load_chunk9(va, in, c_begin, n_in);
+    {
+        unsigned m, z;
+        reduce(va, m, z);
+        m = max(m, wave_max(max_mag(hv)));
+        z = min(z, wave_min(min_nz1(hv)));
+        if (lane == 0) {
+            slot_max[wave] = m;
+            slot_mnz[wave] = z;
+        }
+    }
+    nsh::lds_barrier();
+    unsigned m_prev = max(max(slot_max[0], slot_max[1]), max(slot_max[2], slot_max[3]));
+    unsigned z_prev = min(min(slot_mnz[0], slot_mnz[1]), min(slot_mnz[2], slot_mnz[3]));
+    int s_cur = scale_of(m_prev);
+    bool ex_cur = chunk_needs_exact(m_prev, z_prev, s_cur);
+    put_chunk(lds, hv, va, ex_cur, s_cur);
+    if (G::HP > 0 && tail_owner) stash[tid - (G::NT - G::HP)] = va[3];
+    load_chunk9(va, in, clamp(c_begin + 1), n_in);
+    load_chunk9(vb, in, clamp(c_begin + 2), n_in);
+    {
+        unsigned m, z;
+        reduce(va, m, z);
+        nsh::lds_barrier();
+        if (lane == 0) {
+            slot_max[4 + wave] = m;
+            slot_mnz[4 + wave] = z;
+        }
+    }
+    nsh::lds_barrier();
+
+    auto step = [&](float4 (&nxt)[4], float4 (&nn)[4], float4 (&ld)[4], int64_t ch) {
+        const int i = (int)(ch - c_begin);
+        const int pi = i & 1, pn = pi ^ 1;
+        const unsigned char* cur = lds + pi * G::BUF;
+        unsigned char* nbuf = lds + pn * G::BUF;
+        const unsigned m_nxt = max(max(slot_max[4 * pn], slot_max[4 * pn + 1]), max(slot_max[4 * pn + 2], slot_max[4 * pn + 3]));
+        const unsigned z_nxt = min(min(slot_mnz[4 * pn], slot_mnz[4 * pn + 1]), min(slot_mnz[4 * pn + 2], slot_mnz[4 * pn + 3]));
+        const unsigned m2 = max(m_prev, m_nxt);
+        const int s_nxt = scale_of(m2);
+        const bool ex_nxt = chunk_needs_exact(m2, min(z_prev, z_nxt), s_nxt);
+        load_chunk9(ld, in, clamp(ch + 3), n_in);
+        put_chunk(nbuf, G::HP > 0 && tid < G::HP ? stash[pi * G::HP + tid] : make_float4(0.f, 0.f, 0.f, 0.f), nxt, ex_nxt, s_nxt);
+        if (G::HP > 0 && tail_owner) stash[pn * G::HP + tid - (G::NT - G::HP)] = nxt[3];
+        nf2 o[8];
+        if (ex_cur)
+            direct_tile10<QH>(cur, taps, L, wave, g, phase, o);
+        else
+            mfma_tile10<QH>(cur, B0, B1, T0, T1, row_base, g, -(s_cur + sh), o);
+        store_tile(ch, o);
+        unsigned m, z;
+        reduce(nn, m, z);
+        if (lane == 0) {
+            slot_max[4 * pi + wave] = m;
+            slot_mnz[4 * pi + wave] = z;
+        }
+        m_prev = m_nxt;
+        z_prev = z_nxt;
+        ex_cur = ex_nxt;
+        s_cur = s_nxt;
+        nsh::lds_barrier();
+    };
+    int64_t ch = c_begin;
+    for (; ch + 2 <= c_last; ch += 3) {
+        step(va, vb, vc, ch);
+        step(vb, vc, va, ch + 1);
+        step(vc, va, vb, ch + 2);
+    }
+    if (ch <= c_last) step(va, vb, vc, ch++);
+    if (ch <= c_last) step(vb, vc, va, ch);
+}
+
 // Host-side bf16 round-to-nearest-even (taps are finite).
 unsigned short bf16_rne(float f)
 {
@@ -1661,12 +1940,53 @@ int launch_v9(const nsh_fir_plan* p, const float2* in, const float2* hin, float2
     return 0;
 }
 
+template <int QH>
+int launch_v10(const nsh_fir_plan* p, const float2* in, const float2* hin, float2* hout, float2* out, int64_t n_out,
+               hipStream_t s)
+{
+    using G = geom10<QH>;
+    static bool attr_set = false;
+    if (!attr_set) {
+        NSH_CK(hipFuncSetAttribute((const void*)k_fir_mfma10<QH>, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
+        attr_set = true;
+    }
+    const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
+    int n_cu = 256;
+    (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, p->dev);
+    const int64_t max_grid = (int64_t)n_cu * 2;
+    const unsigned grid = (unsigned)(nchunks < max_grid ? nchunks : max_grid);
+    hipLaunchKernelGGL((k_fir_mfma10<QH>), dim3(grid), dim3(G::NT), G::LDS, s, in, hin, hout, out,
+                       (const _Float16*)p->frag10_dev, (const float*)p->taps_dev, p->L, p->sh8, n_out);
+    NSH_CK_LAUNCH("nsh_fir_ccf(mfma fp16x2 16-sample)");
+    return 0;
+}
+int launch_v10_qh(const nsh_fir_plan* p, const float2* in, const float2* hin, float2* hout, float2* out, int64_t n_out,
+                  hipStream_t s)
+{
+    switch (p->QH) {
+    case 1: return launch_v10<1>(p, in, hin, hout, out, n_out, s);
+    case 2: return launch_v10<2>(p, in, hin, hout, out, n_out, s);
+    case 3: return launch_v10<3>(p, in, hin, hout, out, n_out, s);
+    case 4: return launch_v10<4>(p, in, hin, hout, out, n_out, s);
+    case 5: return launch_v10<5>(p, in, hin, hout, out, n_out, s);
+    case 6: return launch_v10<6>(p, in, hin, hout, out, n_out, s);
+    case 7: return launch_v10<7>(p, in, hin, hout, out, n_out, s);
+    case 8: return launch_v10<8>(p, in, hin, hout, out, n_out, s);
+    case 9: return launch_v10<9>(p, in, hin, hout, out, n_out, s);
+    case 10: return launch_v10<10>(p, in, hin, hout, out, n_out, s);
+    default: return nsh::fail_msg("nsh_fir_ccf(mfma10): unsupported tap count");
+    }
+}
+
 // Tuning variants (selected by NSH_FIR_MFMA_VARIANT for A/B runs; default = measured best).
 template <int Q>
 int launch_q(const nsh_fir_plan* p, const float2* in, const float2* hin, float2* hout, float2* out, int64_t n_out, hipStream_t s)
 {
     if (p->frag8_dev && !p->force_x3 && p->variant != 6 && p->variant != 7)
+    {
+        if (p->variant == 10 && p->frag10_dev) return launch_v10_qh(p, in, hin, hout, out, n_out, s);
         return p->variant == 8 ? launch_v8<Q>(p, in, hin, hout, out, n_out, s) : launch_v9<Q>(p, in, hin, hout, out, n_out, s);
+    }
     switch (p->variant) {
     case 6: return launch_v2<Q, 1>(p, in, hin, hout, out, n_out, s, 2);
     case 7: return launch_v2<Q, 2>(p, in, hin, hout, out, n_out, s, 2);
@@ -1801,6 +2121,37 @@ int nsh_fir_mfma_prepare(nsh_fir_plan* p)
             NSH_CK(hipMalloc(&p->frag8_dev, f8.size() * sizeof(_Float16)));
             NSH_CK(hipMemcpy(p->frag8_dev, f8.data(), f8.size() * sizeof(_Float16), hipMemcpyHostToDevice));
         }
+        // v10: the same scaled fp16x2 taps in k_fir_mfma5's 16-sample fragment order
+        // (k-steps of 32: lane l holds B[k = 8(l >> 4) + j][col = l & 15], tap index
+        // col - (k & 15) + 16 (2 st + (k >> 4)); odd QH: a 16x16x16 tail, B[r = 4(l >> 4) + j])
+        const int QH = (p->L + 15 + 15) / 16;
+        if (QH <= 10) {
+            const int KS = QH / 2;
+            const bool tail = QH % 2;
+            std::vector<_Float16> f((size_t)2 * KS * 64 * 8 + (size_t)2 * 64 * 4, (_Float16)0.f);
+            auto put2 = [&](int t, size_t i0, size_t i1) {
+                const float hs = (t >= 0 && t < p->L) ? std::ldexp(p->taps_host[t], sh) : 0.f;
+                const _Float16 h0 = (_Float16)hs;
+                f[i0] = h0;
+                f[i1] = (_Float16)(hs - (float)h0);
+            };
+            for (int st = 0; st < KS; ++st)
+                for (int lane = 0; lane < 64; ++lane)
+                    for (int j = 0; j < 8; ++j) {
+                        const int kk = 8 * (lane >> 4) + j;
+                        put2((lane & 15) - (kk & 15) + 16 * (2 * st + (kk >> 4)), ((size_t)(0 * KS + st) * 64 + lane) * 8 + j,
+                             ((size_t)(1 * KS + st) * 64 + lane) * 8 + j);
+                    }
+            if (tail) {
+                const size_t t0 = (size_t)2 * KS * 64 * 8;
+                for (int lane = 0; lane < 64; ++lane)
+                    for (int j = 0; j < 4; ++j)
+                        put2((lane & 15) - (4 * (lane >> 4) + j) + 16 * (QH - 1), t0 + (size_t)lane * 4 + j,
+                             t0 + (size_t)(64 + lane) * 4 + j);
+            }
+            NSH_CK(hipMalloc(&p->frag10_dev, f.size() * sizeof(_Float16)));
+            NSH_CK(hipMemcpy(p->frag10_dev, f.data(), f.size() * sizeof(_Float16), hipMemcpyHostToDevice));
+        }
     }
 
     // v5: QH/2 k-steps of 32 for v_mfma_f32_16x16x32_bf16 (lane l holds B[k = 8(l >> 4) + j]
@@ -1854,7 +2205,10 @@ std::string nsh_fir_mfma_kernel_name(const nsh_fir_plan* p)
     if (p->algo == NSH_FIR_MFMA16) return t("k_fir_mfma5", p->QH, p->variant == 20 ? 2 : 1);
     if (p->D > 1) return t("k_fir_mfma7", p->D, p->QHD);
     if (p->frag8_dev && !p->force_x3 && p->variant != 6 && p->variant != 7)
+    {
+        if (p->variant == 10 && p->frag10_dev) return t("k_fir_mfma10", p->QH);
         return t(p->variant == 8 ? "k_fir_mfma8" : "k_fir_mfma9", p->Q);
+    }
     if (p->variant >= 20) return t("k_fir_mfma5", p->QH, p->variant == 20 ? 2 : 1);
     return t("k_fir_mfma2", p->Q, p->variant == 6 ? 1 : 2);
 }

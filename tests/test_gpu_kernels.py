@@ -4,6 +4,8 @@ oracle on the same seeded inputs, plus golden fixtures and size-independent prop
 Tolerances: bit-exact for copy / identity multiplies / per-stage-rounded complex
 products (same formula, no FMA); FIR and FFT within the north-star 1e-5 relative bound
 (norm-wise max|dy| <= 1e-5 max|y_ref| and per element, oracle.tol_ok)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -116,9 +118,32 @@ def test_add_mul_cc_bit_exact(torch_cuda, n):
 
 # "mfma" is the default matrix-core kernel (decim 1: per-chunk scaled fp16x2, k_fir_mfma9),
 # "mfma_x3" forces the bf16x3 six-product kernel (k_fir_mfma2), "mfma16" the 16-sample form.
+# "mfma_v8" / "mfma_v10" are the other fp16x2 kernels (NSH_FIR_MFMA_VARIANT 8: k_fir_mfma8,
+# 10: k_fir_mfma10, the 16-sample form).
 ALGOS = [("direct", nsh.FIR_DIRECT), ("mfma", nsh.FIR_MFMA), ("mfma_x3", nsh.FIR_MFMA_BF16X3),
-         ("mfma16", nsh.FIR_MFMA16)]
-MAX_TAPS = {"direct": 4096, "mfma": 161, "mfma_x3": 161, "mfma16": 145}
+         ("mfma16", nsh.FIR_MFMA16), ("mfma_v8", nsh.FIR_MFMA), ("mfma_v10", nsh.FIR_MFMA)]
+MAX_TAPS = {"direct": 4096, "mfma": 161, "mfma_x3": 161, "mfma16": 145, "mfma_v8": 161, "mfma_v10": 145}
+VARIANT = {"mfma_v8": "8", "mfma_v10": "10"}
+
+
+def make_plan(name, taps, decim, algo):
+    """FirPlan for an ALGOS entry (variants are chosen at plan creation by the env var)."""
+    v = VARIANT.get(name)
+    old = os.environ.get("NSH_FIR_MFMA_VARIANT")
+    if v:
+        os.environ["NSH_FIR_MFMA_VARIANT"] = v
+    try:
+        plan = nsh.FirPlan(taps, decim, algo)
+    finally:
+        if v:
+            if old is None:
+                del os.environ["NSH_FIR_MFMA_VARIANT"]
+            else:
+                os.environ["NSH_FIR_MFMA_VARIANT"] = old
+    if v:
+        want = "k_fir_mfma8" if v == "8" else "k_fir_mfma10"
+        assert plan.kernel.startswith(want), plan.kernel
+    return plan
 
 
 def run_fir(torch, plan, x, n_out, hist=None):
@@ -135,7 +160,7 @@ def run_fir(torch, plan, x, n_out, hist=None):
 def test_fir127_golden(torch_cuda, golden, name, algo):
     torch = torch_cuda
     g = golden("fir127.npz")
-    plan = nsh.FirPlan(g["taps"], 1, algo)
+    plan = make_plan(name, g["taps"], 1, algo)
     assert plan.algo == algo
     if name == "mfma":
         assert plan.kernel == "k_fir_mfma9<5>", plan.kernel
@@ -159,7 +184,7 @@ def test_fir_vs_oracle_shapes(torch_cuda, name, algo, ntaps, n):
     h = rng.standard_normal(ntaps).astype(np.float32) * 0.1
     x = orc.synth(n, 5 + n)
     hist = orc.synth(max(ntaps - 1, 1), 10 ** 7)[: ntaps - 1]
-    plan = nsh.FirPlan(h, 1, algo)
+    plan = make_plan(name, h, 1, algo)
     y, hout = run_fir(torch, plan, x, n, hist=hist if ntaps > 1 else None)
     y_ref, h_ref = orc.fir_ccf(x, h, hist=hist if ntaps > 1 else None, return_hist=True)
     ok, err, scale = orc.tol_ok(y, y_ref)
@@ -231,7 +256,7 @@ def test_fir_chunked_stream_equals_one_shot(torch_cuda, name, algo):
     torch = torch_cuda
     h = np.hamming(127).astype(np.float32) / 70
     x = orc.synth(300_000, 42)
-    plan = nsh.FirPlan(h, 1, algo)
+    plan = make_plan(name, h, 1, algo)
     y_all, _ = run_fir(torch, plan, x, x.size)
     hist = np.zeros(126, np.complex64)
     parts = []
@@ -252,7 +277,7 @@ def test_fir_linearity_large(torch_cuda, name, algo):
     torch = torch_cuda
     n = 1 << 24
     h = np.asarray(__import__("scipy.signal", fromlist=["firwin"]).firwin(127, 0.2), np.float32)
-    plan = nsh.FirPlan(h, 1, algo)
+    plan = make_plan(name, h, 1, algo)
     x = torch.empty(n, dtype=torch.complex64, device="cuda")
     nsh.synth(x, n, 0)
     hin = torch.zeros(126, dtype=torch.complex64, device="cuda")
@@ -295,13 +320,13 @@ def _assert_nonfinite_pattern(y, ref):
     np.testing.assert_array_equal(np.sign(y.imag[inf]), np.sign(ref.imag[inf]))
 
 
-@pytest.fixture(params=["v9", "v8"])
+@pytest.fixture(params=["v9", "v8", "v10"])
 def v8_form(request, monkeypatch):
     """Both fp16x2 kernels: k_fir_mfma9 (default: exact-path decision per chunk from the
     reductions, exact chunks staged raw in LDS) and k_fir_mfma8 (per-sample tests, exact
     path from global memory; NSH_FIR_MFMA_VARIANT=8)."""
-    if request.param == "v8":
-        monkeypatch.setenv("NSH_FIR_MFMA_VARIANT", "8")
+    if request.param in ("v8", "v10"):
+        monkeypatch.setenv("NSH_FIR_MFMA_VARIANT", request.param[1:])
     else:
         monkeypatch.delenv("NSH_FIR_MFMA_VARIANT", raising=False)
     return request.param
@@ -309,7 +334,7 @@ def v8_form(request, monkeypatch):
 
 def _v8_plan(h, form):
     plan = nsh.FirPlan(h, 1, nsh.FIR_MFMA)
-    assert plan.kernel == ("k_fir_mfma9<5>" if form == "v9" else "k_fir_mfma8<5>"), plan.kernel
+    assert plan.kernel == {"v9": "k_fir_mfma9<5>", "v8": "k_fir_mfma8<5>", "v10": "k_fir_mfma10<9>"}[form], plan.kernel
     return plan
 
 

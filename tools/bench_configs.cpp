@@ -145,7 +145,9 @@ struct gpu_fg {
     }
     double run(int steps)
     {
-        fg->run(); // warm-up
+        // warm-up to the sustained clock: the chip's power management settles after ~20
+        // back-to-back runs (tools/probe/run_series.py), as in bench.py's default warmup
+        for (int i = 0; i < 20; ++i) fg->run();
         std::vector<double> t;
         for (int i = 0; i < steps; ++i) {
             const auto t0 = clk::now();
