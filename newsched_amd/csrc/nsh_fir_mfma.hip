@@ -1003,42 +1003,6 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma7(const float2* __restrict__
     if (ch <= c_last) step(va, vb, ch);
 }
 
-template <int D, int QH>
-int launch_v7(const nsh_fir_plan* p, const float2* in, const float2* hin, float2* hout, float2* out, int64_t n_out,
-              hipStream_t s)
-{
-    using G = geom7<D, QH>;
-    static bool attr_set = false;
-    if (!attr_set) {
-        NSH_CK(hipFuncSetAttribute((const void*)k_fir_mfma7<D, QH>, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
-        attr_set = true;
-    }
-    const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
-    int n_cu = 256;
-    (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, p->dev);
-    const int wg_per_cu = (160 * 1024) / G::LDS >= 3 ? 3 : 2; // LDS-bound residency (VGPRs allow 3)
-    const int64_t max_grid = (int64_t)n_cu * wg_per_cu;
-    const unsigned grid = (unsigned)(nchunks < max_grid ? nchunks : max_grid);
-    hipLaunchKernelGGL((k_fir_mfma7<D, QH>), dim3(grid), dim3(G::NT), G::LDS, s, in, hin, hout, out,
-                       (const unsigned short*)p->fragd_dev, p->L, n_out);
-    NSH_CK_LAUNCH("nsh_fir_ccf(mfma decim)");
-    return 0;
-}
-
-template <int D>
-int launch_dec(const nsh_fir_plan* p, const float2* in, const float2* hin, float2* hout, float2* out, int64_t n_out,
-               hipStream_t s)
-{
-    switch (p->QHD) {
-    case 2: return launch_v7<D, 2>(p, in, hin, hout, out, n_out, s);
-    case 3: return launch_v7<D, 3>(p, in, hin, hout, out, n_out, s);
-    case 4: return launch_v7<D, 4>(p, in, hin, hout, out, n_out, s);
-    case 5: return launch_v7<D, 5>(p, in, hin, hout, out, n_out, s);
-    case 6: return launch_v7<D, 6>(p, in, hin, hout, out, n_out, s);
-    default: return nsh::fail_msg("nsh_fir_ccf(mfma decim): unsupported tap count");
-    }
-}
-
 // ---- v8: per-chunk scaled fp16x2 split, three products (default for decim 1) ----------------
 // Same Toeplitz GEMM, data movement and LDS row layout as v2, on v_mfma_f32_32x32x16_f16.
 // fp16 keeps 11 significant bits, so a two-term split x = x0 + x1 (both RNE) keeps 22 and
@@ -1858,6 +1822,387 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma10(const float2* __restrict_
     if (ch <= c_last) step(vb, vc, va, ch);
 }
 
+// ---- k_fir_mfma11: decimating polyphase FIR (D = 2, 4) on the fp16x2 split -----------------
+// k_fir_mfma7's polyphase Toeplitz form (phase streams z_0[i] = x[D i], z_r[i] = x[D i + D - r],
+// taps h'_0[j] = h[D j], h'_r[j] = h[D (j - 1) + r], 16-sample blocks, 16x16x32 + 16x16x16 tail)
+// with k_fir_mfma9's numerics and pipeline: two fp16 planes per component and three products
+// instead of three bf16 planes and six, per-chunk power-of-two scale, exact chunks staged raw
+// in LDS and filtered by the fp32 direct form, buffer loads/stores, LDS-only barriers. The halo
+// (the last D*H input samples of the previous chunk) is kept raw in an LDS stash and re-split
+// at each chunk's scale.
+template <int D, int QH>
+struct geom11 {
+    static constexpr int NT = 256;
+    static constexpr int CHUNK_IN = 2048;
+    static constexpr int CHUNK = CHUNK_IN / D;
+    static constexpr int TILES = 4 / D;
+    static constexpr int WAVE_OUT = TILES * 128;
+    static constexpr int KS = QH / 2;
+    static constexpr int TAIL = QH % 2;
+    static constexpr int H = 16 * (QH - 1);                    // halo samples per phase
+    static constexpr int HR = QH - 1;
+    static constexpr int NB = (CHUNK + H) / 16;
+    static constexpr int PLANE = NB * 32;
+    static constexpr int IM_OFF = (2 * PLANE + 255) / 256 * 256 + 128;
+    static constexpr int PH = (IM_OFF + 2 * PLANE + 255) / 256 * 256;
+    static constexpr int BUF = D * PH;
+    static constexpr int HP = D * H / 2;                      // halo float4 (2 input samples each)
+    static constexpr int STASH = HP * 16;
+    static constexpr int SLOTS = 2 * BUF + 2 * STASH;
+    static constexpr int LDS = SLOTS + 64;                     // u32 max[2][4], mnz[2][4]
+    static constexpr int UNITS = 4 / D;                        // units of 2D samples per thread
+    static constexpr int PER_PHASE = 2 * KS * 64 * 8 + 2 * 64 * 4; // fp16 tap elements
+    static_assert(D == 2 || D == 4, "D");
+    static_assert((HP + 1024) * 16 <= BUF, "a raw fp32 chunk + halo fits one plane buffer");
+    static_assert(HP <= NT && H / 2 <= NT, "halo: one float4 per thread");
+};
+
+template <int D, int QH>
+__device__ __forceinline__ void store_pair11(unsigned char* buf, int r, int s, float a_re, float b_re, float a_im,
+                                             float b_im, int sc)
+{
+    using G = geom11<D, QH>;
+    unsigned char* ph = buf + r * G::PH;
+    const int off = (s >> 4) * 32 + (s & 15) * 2;
+    const float ar = __builtin_ldexpf(a_re, sc), br = __builtin_ldexpf(b_re, sc);
+    const float ai = __builtin_ldexpf(a_im, sc), bi = __builtin_ldexpf(b_im, sc);
+    const _Float16 ar0 = (_Float16)ar, br0 = (_Float16)br, ai0 = (_Float16)ai, bi0 = (_Float16)bi;
+    *reinterpret_cast<unsigned*>(ph + off) = __builtin_bit_cast(unsigned, f16x2{ ar0, br0 });
+    *reinterpret_cast<unsigned*>(ph + G::PLANE + off) =
+        __builtin_bit_cast(unsigned, f16x2{ (_Float16)(ar - (float)ar0), (_Float16)(br - (float)br0) });
+    *reinterpret_cast<unsigned*>(ph + G::IM_OFF + off) = __builtin_bit_cast(unsigned, f16x2{ ai0, bi0 });
+    *reinterpret_cast<unsigned*>(ph + G::IM_OFF + G::PLANE + off) =
+        __builtin_bit_cast(unsigned, f16x2{ (_Float16)(ai - (float)ai0), (_Float16)(bi - (float)bi0) });
+}
+
+template <int D, int QH>
+__global__ __launch_bounds__(256, 2) void k_fir_mfma11(const float2* __restrict__ in,
+                                                      const float2* __restrict__ hist_in,
+                                                      float2* __restrict__ hist_out,
+                                                      float2* __restrict__ out,
+                                                      const _Float16* __restrict__ frag, // per phase: [2][KS][64] x8, [2][64] x4
+                                                      const float* __restrict__ taps,
+                                                      int L,
+                                                      int sh,
+                                                      int64_t n_out)
+{
+    using G = geom11<D, QH>;
+    constexpr int KS = G::KS;
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    float4* stash = reinterpret_cast<float4*>(lds + 2 * G::BUF); // [2][HP] raw halo sources
+    unsigned* slot_max = reinterpret_cast<unsigned*>(lds + G::SLOTS);
+    unsigned* slot_mnz = slot_max + 8;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int64_t n_in = n_out * D;
+
+    if (blockIdx.x == 0) {
+        for (int j = tid; j < L - 1; j += G::NT) hist_out[j] = virt(in, hist_in, n_in - (L - 1) + j, n_in, L);
+    }
+
+    f16x8 B0[D][KS + 1], B1[D][KS + 1];
+    f16x4 T0[D], T1[D];
+#pragma unroll
+    for (int r = 0; r < D; ++r) {
+        const _Float16* fr = frag + (size_t)r * G::PER_PHASE;
+#pragma unroll
+        for (int st = 0; st < KS; ++st) {
+            B0[r][st] = reinterpret_cast<const f16x8*>(fr)[(0 * KS + st) * 64 + lane];
+            B1[r][st] = reinterpret_cast<const f16x8*>(fr)[(1 * KS + st) * 64 + lane];
+        }
+        const f16x4* tf = reinterpret_cast<const f16x4*>(fr + 2 * KS * 64 * 8);
+        T0[r] = tf[lane];
+        T1[r] = tf[64 + lane];
+    }
+
+    const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
+    const int64_t per = (nchunks + gridDim.x - 1) / gridDim.x;
+    const int64_t c_begin = (int64_t)blockIdx.x * per;
+    const int64_t c_end = c_begin + per < nchunks ? c_begin + per : nchunks;
+    if (c_begin >= c_end) return;
+    const int64_t c_last = c_end - 1;
+
+    const int rho = lane & 15;
+    const int c = rho & 1, b = rho >> 1;
+    const int g = lane >> 4;
+    const int phase = lane & 15;
+    const int row_base = c * G::IM_OFF + (G::HR + wave * (G::WAVE_OUT / 16) + b) * 32;
+    const bool tail_owner = tid >= G::NT - G::H / 2; // holds the chunk's last D*H samples (last unit)
+    auto clamp = [&](int64_t x) { return x <= c_last ? x : c_last; };
+    auto load = [&](float4 (&v)[4], int64_t ch) {
+        const __amdgpu_buffer_rsrc_t r = chunk_rsrc<G::CHUNK_IN>(in, ch, n_in);
+#pragma unroll
+        for (int u = 0; u < G::UNITS; ++u)
+#pragma unroll
+            for (int f = 0; f < D; ++f) v[u * D + f] = buf_load_f4(r, ((tid + G::NT * u) * D + f) * 16);
+    };
+    auto stash_tail = [&](float4* st, const float4 (&v)[4]) {
+        if (tail_owner) {
+#pragma unroll
+            for (int f = 0; f < D; ++f) st[(tid - (G::NT - G::H / 2)) * D + f] = v[(G::UNITS - 1) * D + f];
+        }
+    };
+    // chunk -> buffer: raw fp32 (halo float4 [0, HP), chunk float4 HP + j) or split phase planes
+    auto put_chunk = [&](unsigned char* buf, const float4* hsrc, const float4 (&v)[4], bool raw, int sc) {
+        if (raw) {
+            float4* rb = reinterpret_cast<float4*>(buf);
+            if (tid < G::HP) rb[tid] = hsrc[tid];
+#pragma unroll
+            for (int u = 0; u < G::UNITS; ++u)
+#pragma unroll
+                for (int f = 0; f < D; ++f) rb[G::HP + (tid + G::NT * u) * D + f] = v[u * D + f];
+            return;
+        }
+        if (tid < D * (G::H / 2)) { // halo: phase r, pair pi from the raw halo samples
+            const int r = tid / (G::H / 2), pi = tid % (G::H / 2);
+            const int sr = r == 0 ? 0 : D - r;
+            const int pa = D * (2 * pi) + sr, pb = D * (2 * pi + 1) + sr;
+            const float2 a = f4_sample(hsrc[pa >> 1], pa & 1), bb = f4_sample(hsrc[pb >> 1], pb & 1);
+            store_pair11<D, QH>(buf, r, 2 * pi, a.x, bb.x, a.y, bb.y, sc);
+        }
+#pragma unroll
+        for (int u = 0; u < G::UNITS; ++u) {
+            const int i0 = 2 * (tid + G::NT * u);
+#pragma unroll
+            for (int r = 0; r < D; ++r) {
+                const int sr = r == 0 ? 0 : D - r;
+                const int la = sr, lb = D + sr;
+                const float2 a = f4_sample(v[u * D + la / 2], la & 1);
+                const float2 bb = f4_sample(v[u * D + lb / 2], lb & 1);
+                store_pair11<D, QH>(buf, r, G::H + i0, a.x, bb.x, a.y, bb.y, sc);
+            }
+        }
+    };
+    auto reduce = [&](const float4 (&v)[4], unsigned& m, unsigned& z) {
+        m = 0;
+        z = ~0u;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            m = max(m, max_mag(v[u]));
+            z = min(z, min_nz1(v[u]));
+        }
+        m = wave_max(m);
+        z = wave_min(z);
+    };
+    auto mfma_tile = [&](const unsigned char* cur, int unscale, nf2 (&o)[2 * G::TILES]) {
+        f32x4 hi[G::TILES], lo[G::TILES], hi_t[G::TILES], lo_t[G::TILES];
+#pragma unroll
+        for (int t = 0; t < G::TILES; ++t) {
+            hi[t] = f32x4{ 0.f, 0.f, 0.f, 0.f };
+            lo[t] = f32x4{ 0.f, 0.f, 0.f, 0.f };
+            hi_t[t] = f32x4{ 0.f, 0.f, 0.f, 0.f };
+            lo_t[t] = f32x4{ 0.f, 0.f, 0.f, 0.f };
+        }
+#pragma unroll
+        for (int r = 0; r < D; ++r) {
+            const unsigned char* ph = cur + r * G::PH;
+#pragma unroll
+            for (int st = 0; st < KS; ++st) {
+                const int q = 2 * st + (g >> 1);
+#pragma unroll
+                for (int t = 0; t < G::TILES; ++t) {
+                    const int off = row_base + t * 8 * 32 - q * 32 + (g & 1) * 16;
+                    const f16x8 A0 = *reinterpret_cast<const f16x8*>(ph + off);
+                    const f16x8 A1 = *reinterpret_cast<const f16x8*>(ph + off + G::PLANE);
+                    hi[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0, B0[r][st], hi[t], 0, 0, 0);
+                    lo[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0, B1[r][st], lo[t], 0, 0, 0);
+                    lo[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1, B0[r][st], lo[t], 0, 0, 0);
+                }
+            }
+            if constexpr (G::TAIL) { // separate accumulators: see v5_compute
+#pragma unroll
+                for (int t = 0; t < G::TILES; ++t) {
+                    const int off = row_base + t * 8 * 32 - (QH - 1) * 32 + g * 8;
+                    const f16x4 A0 = *reinterpret_cast<const f16x4*>(ph + off);
+                    const f16x4 A1 = *reinterpret_cast<const f16x4*>(ph + off + G::PLANE);
+                    hi_t[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(A0, T0[r], hi_t[t], 0, 0, 0);
+                    lo_t[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(A0, T1[r], lo_t[t], 0, 0, 0);
+                    lo_t[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(A1, T0[r], lo_t[t], 0, 0, 0);
+                }
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < G::TILES; ++t)
+#pragma unroll
+            for (int half = 0; half < 2; ++half)
+                o[2 * t + half] = nf2{ __builtin_ldexpf((hi[t][2 * half] + hi_t[t][2 * half]) + (lo[t][2 * half] + lo_t[t][2 * half]), unscale),
+                                       __builtin_ldexpf((hi[t][2 * half + 1] + hi_t[t][2 * half + 1]) +
+                                                            (lo[t][2 * half + 1] + lo_t[t][2 * half + 1]), unscale) };
+    };
+    // exact path: y[m] = sum_k h[k] x[D m - k] from the raw chunk (float2 index D H + D m - k)
+    auto direct_tile = [&](const unsigned char* cur, nf2 (&o)[2 * G::TILES]) {
+        const float2* raw = reinterpret_cast<const float2*>(cur);
+        for (int oi = 0; oi < 2 * G::TILES; ++oi) {
+            const int blk = (oi >> 1) * 8 + 2 * g + (oi & 1);
+            const int j = D * G::H + D * (wave * G::WAVE_OUT + blk * 16 + phase);
+            float re = 0.f, im = 0.f;
+            for (int k = 0; k < L; ++k) {
+                const float2 x = raw[j - k];
+                re = fmaf(taps[k], x.x, re);
+                im = fmaf(taps[k], x.y, im);
+            }
+            o[oi] = nf2{ re, im };
+        }
+    };
+    auto store_tile = [&](int64_t ch, const nf2 (&o)[2 * G::TILES]) {
+        const __amdgpu_buffer_rsrc_t r = chunk_rsrc<G::CHUNK>(out, ch, n_out);
+#pragma unroll
+        for (int oi = 0; oi < 2 * G::TILES; ++oi)
+            buf_store_f2(r, (wave * G::WAVE_OUT + ((oi >> 1) * 8 + 2 * g + (oi & 1)) * 16 + phase) * 8, o[oi]);
+    };
+
+    // ---- prologue: chunk c_begin's halo (global memory / history) into stash[1] (free until
+    // step 0 writes it), the chunk itself; chunks +1, +2 in flight
+    float4 va[4], vb[4], vc[4];
+    float4 hv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (tid < G::HP) {
+        const int64_t gg = c_begin * G::CHUNK_IN - 2 * G::HP + 2 * tid;
+        const float2 x0 = virt(in, hist_in, gg, n_in, L), x1 = virt(in, hist_in, gg + 1, n_in, L);
+        hv = make_float4(x0.x, x0.y, x1.x, x1.y);
+        stash[G::HP + tid] = hv;
+    }
+    load(va, c_begin);
+    {
+        unsigned m, z;
+        reduce(va, m, z);
+        m = max(m, wave_max(max_mag(hv)));
+        z = min(z, wave_min(min_nz1(hv)));
+        if (lane == 0) {
+            slot_max[wave] = m;
+            slot_mnz[wave] = z;
+        }
+    }
+    nsh::lds_barrier();
+    unsigned m_prev = max(max(slot_max[0], slot_max[1]), max(slot_max[2], slot_max[3]));
+    unsigned z_prev = min(min(slot_mnz[0], slot_mnz[1]), min(slot_mnz[2], slot_mnz[3]));
+    int s_cur = scale_of(m_prev);
+    bool ex_cur = chunk_needs_exact(m_prev, z_prev, s_cur);
+    put_chunk(lds, stash + G::HP, va, ex_cur, s_cur);
+    stash_tail(stash, va);
+    load(va, clamp(c_begin + 1));
+    load(vb, clamp(c_begin + 2));
+    {
+        unsigned m, z;
+        reduce(va, m, z);
+        nsh::lds_barrier(); // slots [0..3] and stash[1] read above
+        if (lane == 0) {
+            slot_max[4 + wave] = m;
+            slot_mnz[4 + wave] = z;
+        }
+    }
+    nsh::lds_barrier();
+
+    auto step = [&](float4 (&nxt)[4], float4 (&nn)[4], float4 (&ld)[4], int64_t ch) {
+        const int i = (int)(ch - c_begin);
+        const int pi = i & 1, pn = pi ^ 1;
+        const unsigned char* cur = lds + pi * G::BUF;
+        unsigned char* nbuf = lds + pn * G::BUF;
+        const unsigned m_nxt = max(max(slot_max[4 * pn], slot_max[4 * pn + 1]), max(slot_max[4 * pn + 2], slot_max[4 * pn + 3]));
+        const unsigned z_nxt = min(min(slot_mnz[4 * pn], slot_mnz[4 * pn + 1]), min(slot_mnz[4 * pn + 2], slot_mnz[4 * pn + 3]));
+        const unsigned m2 = max(m_prev, m_nxt);
+        const int s_nxt = scale_of(m2);
+        const bool ex_nxt = chunk_needs_exact(m2, min(z_prev, z_nxt), s_nxt);
+        load(ld, clamp(ch + 3));
+        put_chunk(nbuf, stash + pi * G::HP, nxt, ex_nxt, s_nxt);
+        stash_tail(stash + pn * G::HP, nxt);
+        nf2 o[2 * G::TILES];
+        if (ex_cur)
+            direct_tile(cur, o);
+        else
+            mfma_tile(cur, -(s_cur + sh), o);
+        store_tile(ch, o);
+        unsigned m, z;
+        reduce(nn, m, z);
+        if (lane == 0) {
+            slot_max[4 * pi + wave] = m;
+            slot_mnz[4 * pi + wave] = z;
+        }
+        m_prev = m_nxt;
+        z_prev = z_nxt;
+        ex_cur = ex_nxt;
+        s_cur = s_nxt;
+        nsh::lds_barrier();
+    };
+    int64_t ch = c_begin;
+    for (; ch + 2 <= c_last; ch += 3) {
+        step(va, vb, vc, ch);
+        step(vb, vc, va, ch + 1);
+        step(vc, va, vb, ch + 2);
+    }
+    if (ch <= c_last) step(va, vb, vc, ch++);
+    if (ch <= c_last) step(vb, vc, va, ch);
+}
+
+template <int D, int QH>
+int launch_v7(const nsh_fir_plan* p, const float2* in, const float2* hin, float2* hout, float2* out, int64_t n_out,
+              hipStream_t s)
+{
+    using G = geom7<D, QH>;
+    static bool attr_set = false;
+    if (!attr_set) {
+        NSH_CK(hipFuncSetAttribute((const void*)k_fir_mfma7<D, QH>, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
+        attr_set = true;
+    }
+    const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
+    int n_cu = 256;
+    (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, p->dev);
+    const int wg_per_cu = (160 * 1024) / G::LDS >= 3 ? 3 : 2; // LDS-bound residency (VGPRs allow 3)
+    const int64_t max_grid = (int64_t)n_cu * wg_per_cu;
+    const unsigned grid = (unsigned)(nchunks < max_grid ? nchunks : max_grid);
+    hipLaunchKernelGGL((k_fir_mfma7<D, QH>), dim3(grid), dim3(G::NT), G::LDS, s, in, hin, hout, out,
+                       (const unsigned short*)p->fragd_dev, p->L, n_out);
+    NSH_CK_LAUNCH("nsh_fir_ccf(mfma decim)");
+    return 0;
+}
+
+template <int D, int QH>
+int launch_v11(const nsh_fir_plan* p, const float2* in, const float2* hin, float2* hout, float2* out, int64_t n_out,
+               hipStream_t s)
+{
+    using G = geom11<D, QH>;
+    static bool attr_set = false;
+    if (!attr_set) {
+        NSH_CK(hipFuncSetAttribute((const void*)k_fir_mfma11<D, QH>, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
+        attr_set = true;
+    }
+    const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
+    int n_cu = 256;
+    (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, p->dev);
+    const int64_t max_grid = (int64_t)n_cu * 2;
+    const unsigned grid = (unsigned)(nchunks < max_grid ? nchunks : max_grid);
+    hipLaunchKernelGGL((k_fir_mfma11<D, QH>), dim3(grid), dim3(G::NT), G::LDS, s, in, hin, hout, out,
+                       (const _Float16*)p->fragd8_dev, (const float*)p->taps_dev, p->L, p->sh8, n_out);
+    NSH_CK_LAUNCH("nsh_fir_ccf(mfma decim fp16x2)");
+    return 0;
+}
+
+template <int D>
+int launch_dec(const nsh_fir_plan* p, const float2* in, const float2* hin, float2* hout, float2* out, int64_t n_out,
+               hipStream_t s)
+{
+    if (p->fragd8_dev && p->variant != 7) {
+        switch (p->QHD) {
+        case 2: return launch_v11<D, 2>(p, in, hin, hout, out, n_out, s);
+        case 3: return launch_v11<D, 3>(p, in, hin, hout, out, n_out, s);
+        case 4: return launch_v11<D, 4>(p, in, hin, hout, out, n_out, s);
+        case 5: return launch_v11<D, 5>(p, in, hin, hout, out, n_out, s);
+        case 6: return launch_v11<D, 6>(p, in, hin, hout, out, n_out, s);
+        default: return nsh::fail_msg("nsh_fir_ccf(mfma decim): unsupported tap count");
+        }
+    }
+    switch (p->QHD) {
+    case 2: return launch_v7<D, 2>(p, in, hin, hout, out, n_out, s);
+    case 3: return launch_v7<D, 3>(p, in, hin, hout, out, n_out, s);
+    case 4: return launch_v7<D, 4>(p, in, hin, hout, out, n_out, s);
+    case 5: return launch_v7<D, 5>(p, in, hin, hout, out, n_out, s);
+    case 6: return launch_v7<D, 6>(p, in, hin, hout, out, n_out, s);
+    default: return nsh::fail_msg("nsh_fir_ccf(mfma decim): unsupported tap count");
+    }
+}
+
 // Host-side bf16 round-to-nearest-even (taps are finite).
 unsigned short bf16_rne(float f)
 {
@@ -2058,6 +2403,46 @@ int nsh_fir_mfma_prepare_decim(nsh_fir_plan* p)
     }
     NSH_CK(hipMalloc(&p->fragd_dev, f.size() * sizeof(unsigned short)));
     NSH_CK(hipMemcpy(p->fragd_dev, f.data(), f.size() * sizeof(unsigned short), hipMemcpyHostToDevice));
+
+    // k_fir_mfma11: the same polyphase taps scaled by 2^sh8 (max |h| * 2^sh8 in [2^14, 2^15),
+    // as for decim 1) and split into two fp16 terms; per phase [2][KS][64] x8 then [2][64] x4
+    {
+        unsigned maxbits = 0;
+        for (float t : p->taps_host) {
+            unsigned u;
+            std::memcpy(&u, &t, 4);
+            maxbits = std::max(maxbits, u & 0x7fffffffu);
+        }
+        const int sh = 141 - (int)(maxbits >> 23);
+        p->sh8 = sh;
+        const size_t pp = (size_t)2 * KS * 64 * 8 + (size_t)2 * 64 * 4;
+        std::vector<_Float16> f8((size_t)D * pp, (_Float16)0.f);
+        auto put2 = [&](float hv, size_t i0, size_t i1) {
+            const float hs = std::ldexp(hv, sh);
+            const _Float16 h0 = (_Float16)hs;
+            f8[i0] = h0;
+            f8[i1] = (_Float16)(hs - (float)h0);
+        };
+        for (int r = 0; r < D; ++r) {
+            const size_t base = (size_t)r * pp;
+            for (int st = 0; st < KS; ++st)
+                for (int lane = 0; lane < 64; ++lane)
+                    for (int j = 0; j < 8; ++j) {
+                        const int kk = 8 * (lane >> 4) + j;
+                        put2(tap(r, (lane & 15) - (kk & 15) + 16 * (2 * st + (kk >> 4))),
+                             base + (((size_t)0 * KS + st) * 64 + lane) * 8 + j, base + (((size_t)1 * KS + st) * 64 + lane) * 8 + j);
+                    }
+            if (tail) {
+                const size_t t0 = base + (size_t)2 * KS * 64 * 8;
+                for (int lane = 0; lane < 64; ++lane)
+                    for (int j = 0; j < 4; ++j)
+                        put2(tap(r, (lane & 15) - (4 * (lane >> 4) + j) + 16 * (QH - 1)), t0 + (size_t)lane * 4 + j,
+                             t0 + (size_t)(64 + lane) * 4 + j);
+            }
+        }
+        NSH_CK(hipMalloc(&p->fragd8_dev, f8.size() * sizeof(_Float16)));
+        NSH_CK(hipMemcpy(p->fragd8_dev, f8.data(), f8.size() * sizeof(_Float16), hipMemcpyHostToDevice));
+    }
     return 0;
 }
 
@@ -2203,7 +2588,7 @@ std::string nsh_fir_mfma_kernel_name(const nsh_fir_plan* p)
         return std::string(k) + "<" + std::to_string(a) + (b >= 0 ? "," + std::to_string(b) : std::string()) + ">";
     };
     if (p->algo == NSH_FIR_MFMA16) return t("k_fir_mfma5", p->QH, p->variant == 20 ? 2 : 1);
-    if (p->D > 1) return t("k_fir_mfma7", p->D, p->QHD);
+    if (p->D > 1) return t(p->fragd8_dev && p->variant != 7 ? "k_fir_mfma11" : "k_fir_mfma7", p->D, p->QHD);
     if (p->frag8_dev && !p->force_x3 && p->variant != 6 && p->variant != 7)
     {
         if (p->variant == 10 && p->frag10_dev) return t("k_fir_mfma10", p->QH);

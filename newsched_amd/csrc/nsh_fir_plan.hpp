@@ -25,6 +25,7 @@ struct nsh_fir_plan {
     // [phase][part(3)][kstep][lane][8] + [phase][part][lane][4] tail, bf16.
     int QHD = 0;
     void* fragd_dev = nullptr;
+    void* fragd8_dev = nullptr; // fp16x2 polyphase fragments (k_fir_mfma11), taps scaled by 2^sh8
     // scaled fp16x2 form (decim 1, default): taps * 2^sh8 split into two fp16 terms,
     // [part(2)][kstep(S)][lane(64)][8]; null when the taps' range does not allow it.
     void* frag8_dev = nullptr;

@@ -207,18 +207,36 @@ def test_fir_decim_vs_oracle(torch_cuda, decim):
         np.testing.assert_array_equal(hout, h_ref)
 
 
+@pytest.fixture(params=["v11", "v7"])
+def dec_form(request, monkeypatch):
+    """Both polyphase MFMA kernels: k_fir_mfma11 (default: fp16x2, per-chunk scale, exact
+    path) and k_fir_mfma7 (bf16x3 six products; NSH_FIR_MFMA_VARIANT=7)."""
+    if request.param == "v7":
+        monkeypatch.setenv("NSH_FIR_MFMA_VARIANT", "7")
+    else:
+        monkeypatch.delenv("NSH_FIR_MFMA_VARIANT", raising=False)
+    return request.param
+
+
+def _dec_plan(h, decim, form):
+    plan = nsh.FirPlan(h, decim, nsh.FIR_MFMA)
+    assert plan.algo == nsh.FIR_MFMA
+    want = "k_fir_mfma11<" if form == "v11" else "k_fir_mfma7<"
+    assert plan.kernel.startswith(want), plan.kernel
+    return plan
+
+
 @pytest.mark.parametrize("decim", [2, 4])
 @pytest.mark.parametrize("ntaps", [1, 2, 15, 16, 17, 33, 64, 127, 128, 160])
 @pytest.mark.parametrize("n_out", [1, 100, 1023, 1024, 1025, 33333])
-def test_fir_decim_mfma_vs_oracle(torch_cuda, decim, ntaps, n_out):
-    """Polyphase MFMA form (k_fir_mfma7): every phase/halo/tail shape against the oracle."""
+def test_fir_decim_mfma_vs_oracle(torch_cuda, dec_form, decim, ntaps, n_out):
+    """Polyphase MFMA forms: every phase/halo/tail shape against the oracle."""
     torch = torch_cuda
     rng = np.random.default_rng(ntaps * 7919 + n_out * decim)
     h = rng.standard_normal(ntaps).astype(np.float32) * 0.1
     x = orc.synth(n_out * decim, 11 + n_out)
     hist = orc.synth(max(ntaps - 1, 1), 5 * 10 ** 6)[: ntaps - 1]
-    plan = nsh.FirPlan(h, decim, nsh.FIR_MFMA)
-    assert plan.algo == nsh.FIR_MFMA
+    plan = _dec_plan(h, decim, dec_form)
     y, hout = run_fir(torch, plan, x, n_out, hist=hist if ntaps > 1 else None)
     y_ref, h_ref = orc.fir_ccf(x, h, decim=decim, hist=hist if ntaps > 1 else None, return_hist=True)
     ok, err, scale = orc.tol_ok(y, y_ref)
@@ -231,6 +249,36 @@ def test_fir_decim_auto_picks_mfma(torch_cuda):
     assert nsh.FirPlan(h, 2).algo == nsh.FIR_MFMA
     assert nsh.FirPlan(h, 4).algo == nsh.FIR_MFMA
     assert nsh.FirPlan(h, 8).algo == nsh.FIR_DIRECT
+
+
+@pytest.mark.parametrize("decim", [2, 4])
+def test_fir_decim_mfma_edge_values(torch_cuda, dec_form, decim):
+    """inf/NaN (pattern equal to the oracle's), a 2^60 spike, segments at 1e-30 / 1e30, zero
+    chunks and an fp32-subnormal sample through the polyphase kernels; each region checked on
+    its own scale. The fp16x2 form sends the chunks that need it through the exact path."""
+    torch = torch_cuda
+    h = _firwin127()
+    n_out = 30_000
+    x = orc.synth(n_out * decim, 40 + decim)
+    seg = len(x) // 4
+    x[:seg] *= np.float32(1e-30)
+    x[3 * seg:] *= np.float32(1e30)
+    if dec_form == "v11":  # the bf16x3 form has no exact path: finite inputs only
+        x[seg + 5000] = np.complex64(complex(np.inf, 0.5))
+        x[seg + 9000] = np.complex64(complex(np.nan, 0.0))
+    x[2 * seg + 100] *= np.float32(2.0 ** 60)
+    x[2 * seg + 6000:2 * seg + 10_000] = 0
+    x[2 * seg + 12_000] = np.complex64(complex(1e-40, 0.0))
+    y, _ = run_fir(torch, _dec_plan(h, decim, dec_form), x, n_out)
+    ref = orc.fir_ccf(x, h, decim=decim)
+    _assert_nonfinite_pattern(y, ref)
+    before = lambda i: (i + decim - 1) // decim  # outputs [0, before(i)) do not see input i
+    after = lambda i: (i + 126) // decim + 1     # outputs from after(i) on no longer see it
+    regions = [(0, before(seg)), (after(seg), before(seg + 5000)), (after(seg + 9000), before(2 * seg + 100)),
+               (after(2 * seg + 100), before(3 * seg)), (after(3 * seg), n_out)]
+    for a, b in regions:
+        ok, err, scale = orc.tol_ok(y[a:b], ref[a:b])
+        assert ok, (decim, a, b, err, scale)
 
 
 def test_fir_decim2_golden_chain(torch_cuda, golden):
@@ -429,7 +477,8 @@ def test_fir_plan_kernels():
     assert nsh.FirPlan(h, 1, nsh.FIR_MFMA_BF16X3).kernel == "k_fir_mfma2<5,2>"
     assert nsh.FirPlan(h, 1, nsh.FIR_MFMA16).kernel == "k_fir_mfma5<9,1>"
     assert nsh.FirPlan(h, 1, nsh.FIR_DIRECT).kernel == "k_fir_direct<1,8>"
-    assert nsh.FirPlan(h, 2, nsh.FIR_MFMA).kernel == "k_fir_mfma7<2,5>"
+    assert nsh.FirPlan(h, 2, nsh.FIR_MFMA).kernel == "k_fir_mfma11<2,5>"
+    assert nsh.FirPlan(h, 4, nsh.FIR_MFMA).kernel == "k_fir_mfma11<4,3>"
     for L in (1, 17, 33, 65, 97, 129, 161):
         assert nsh.FirPlan(np.ones(L, np.float32), 1, nsh.FIR_MFMA).kernel == "k_fir_mfma9<%d>" % ((L + 30) // 32 + 1)
 
