@@ -84,13 +84,19 @@ def main():
 
     import torch
 
-    torch.cuda.set_device(local)
+    # one process per GPU; more ranks than GPUs (a rehearsal on a 1-GPU box) share devices
+    device = local % max(torch.cuda.device_count(), 1)
+    torch.cuda.set_device(device)
     dist = None
+    backend = os.environ.get("NSH_BENCH_BACKEND", "nccl")  # nccl = RCCL; gloo only for rehearsals
     if world > 1:
         import torch.distributed as dist
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group(backend="nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group(backend=backend)
 
     from newsched_amd import nsh, nsr
     from oracle import oracle as orc  # checker only: tail parity + CPU-baseline inputs
@@ -100,7 +106,7 @@ def main():
     n = 1 << a.log2n
     taps = firwin127()
     first = rank * n  # this rank's time shard
-    fb = nsr.FirBench(taps, n, device=local, algo=algo, first_index=first, out_buf_bytes=a.out_buf_mib << 20)
+    fb = nsr.FirBench(taps, n, device=device, algo=algo, first_index=first, out_buf_bytes=a.out_buf_mib << 20)
 
     def barrier():
         if dist is not None:
@@ -122,7 +128,7 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     st = fb.stats()
@@ -141,6 +147,10 @@ def main():
     xw = orc.synth(m + taps.size - 1, lo)
     y_ref = orc.fir_ccf(xw[taps.size - 1:], taps, hist=xw[: taps.size - 1])
     ok, err, scale = orc.tol_ok(y, y_ref)
+    if dist is not None:  # every rank's shard tail must pass; report the worst error
+        r = torch.tensor([0.0 if ok else 1.0, err], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
+        dist.all_reduce(r, op=dist.ReduceOp.MAX)
+        ok, err = r[0].item() == 0.0, float(r[1].item())
 
     value = world * n * a.steps / elapsed / 1e6  # MSamples/s, whole job
     out = {
@@ -179,7 +189,7 @@ def main():
             "algorithmic_bytes_per_launch": int(BYTES_PER_SAMPLE * per_launch_samples),
             "kernel_gflops": round(FLOP_PER_SAMPLE * per_launch_samples / (avg_launch_ms * 1e-3) / 1e9, 1),
         },
-        "parity": {"check": "last 4096 outputs of the last step vs oracle (double accumulation)",
+        "parity": {"check": "last 4096 outputs of the last step vs oracle (double accumulation), every rank",
                    "max_abs_err": err, "scale": scale, "ok": bool(ok)},
     }
     tr = load_pmc_traffic(kernel, per_launch_samples)
