@@ -88,6 +88,10 @@ int nsh_mul_const_ff(const float* in, float* out, int64_t n, float k, void* stre
 int nsh_mul_const_chain_cc(const float* in, float* out, int64_t n, const float* k_host, int m, void* stream);
 int nsh_add_cc(const float* a, const float* b, float* out, int64_t n, void* stream);
 int nsh_mul_cc(const float* a, const float* b, float* out, int64_t n, void* stream);
+/* multiply_const_vcc: items of vlen complex samples, y[i][j] = x[i][j] * k[j], k_dev a device
+ * array of vlen (re,im) pairs (GNU Radio's vector-constant multiply; the reference has only the
+ * scalar multiply_const<T> over n_items*vlen, blocklib/blocks/lib/multiply_const.cpp:33-46). */
+int nsh_mul_const_vcc(const float* in, float* out, const float* k_dev, int vlen, int64_t nitems, void* stream);
 
 /* Counter-based synthetic stream: x[i] = (u(2i), u(2i+1)),
  * u(j) = 24-bit uniform in [-1,1) from splitmix64(seed ^ j), j counted from first_index*2. */

@@ -19,6 +19,8 @@ public:
     }
     fft_vcc(size_t fft_size, bool forward);
     work_return_code_t work(std::vector<block_work_input>& in, std::vector<block_work_output>& out) override;
+    bool forward() const { return _forward; }
+    size_t fft_size() const { return 1024; }
 
 private:
     bool _forward;
@@ -36,6 +38,7 @@ public:
         return p;
     }
     explicit channelizer_vcc(const std::vector<gr_complex>& w);
+    const std::vector<gr_complex>& w() const { return _w; }
     ~channelizer_vcc() override;
     bool start() override;
     work_return_code_t work(std::vector<block_work_input>& in, std::vector<block_work_output>& out) override;

@@ -72,5 +72,31 @@ private:
     std::vector<gr_complex> d_ks;
     size_t d_vlen;
 };
+
+// y[i][j] = x[i][j] * k[j] on items of vlen = k.size() complex samples (GNU Radio's
+// multiply_const_vcc; the reference has only the scalar multiply_const<T>). Not an
+// elementwise_cc stage (its constant depends on the position in the item); scheduler_hip
+// fuses fft_vcc -> multiply_const_vcc -> fft_vcc(inverse) into one channelizer_vcc launch.
+class multiply_const_vcc : public sync_block
+{
+public:
+    using sptr = std::shared_ptr<multiply_const_vcc>;
+    static sptr make(const std::vector<gr_complex>& k)
+    {
+        auto p = std::make_shared<multiply_const_vcc>(k);
+        p->add_port(port<gr_complex>::make("input", port_direction_t::INPUT, std::vector<size_t>{ k.size() }));
+        p->add_port(port<gr_complex>::make("output", port_direction_t::OUTPUT, std::vector<size_t>{ k.size() }));
+        return p;
+    }
+    explicit multiply_const_vcc(const std::vector<gr_complex>& k);
+    ~multiply_const_vcc() override;
+    bool start() override;
+    work_return_code_t work(std::vector<block_work_input>& in, std::vector<block_work_output>& out) override;
+    const std::vector<gr_complex>& k() const { return d_k; }
+
+private:
+    std::vector<gr_complex> d_k;
+    void* d_kdev = nullptr;
+};
 } // namespace hip
 } // namespace gr

@@ -48,6 +48,33 @@ work_return_code_t multiply_const<float>::work(std::vector<block_work_input>& in
 template class multiply_const<gr_complex>;
 template class multiply_const<float>;
 
+multiply_const_vcc::multiply_const_vcc(const std::vector<gr_complex>& k) : sync_block("multiply_const_vcc (hip)"), d_k(k)
+{
+    if (k.empty()) throw std::invalid_argument("hip::multiply_const_vcc: k must not be empty");
+}
+multiply_const_vcc::~multiply_const_vcc()
+{
+    if (d_kdev) nsh_free(d_kdev);
+}
+bool multiply_const_vcc::start()
+{
+    if (!d_kdev) { // the constant lives on the device of the thread that runs the block
+        check(nsh_malloc(current_device(), d_k.size() * sizeof(gr_complex), &d_kdev), "hip::multiply_const_vcc");
+        check(nsh_memcpy_async(d_kdev, d_k.data(), d_k.size() * sizeof(gr_complex), NSH_H2D, current_stream()),
+              "hip::multiply_const_vcc");
+        check(nsh_stream_sync(current_stream()), "hip::multiply_const_vcc");
+    }
+    return sync_block::start();
+}
+work_return_code_t multiply_const_vcc::work(std::vector<block_work_input>& in, std::vector<block_work_output>& out)
+{
+    check(nsh_mul_const_vcc((const float*)in[0].buffer->read_ptr(), (float*)out[0].buffer->write_ptr(),
+                            (const float*)d_kdev, (int)d_k.size(), out[0].n_items, current_stream()),
+          "hip::multiply_const_vcc");
+    out[0].n_produced = out[0].n_items;
+    return work_return_code_t::WORK_OK;
+}
+
 work_return_code_t multiply_const_chain_cc::work(std::vector<block_work_input>& in, std::vector<block_work_output>& out)
 {
     std::vector<float> k;

@@ -173,6 +173,19 @@ int launch_map_c(const float* in, float* out, int64_t n, Op op, hipStream_t s, c
 }
 
 // Binary complex maps (add_cc, multiply_cc).
+// y[i] = x[i] * k[i mod vlen] (multiply_const_vcc); cmul's rounding, as fft -> w -> ifft in
+// k_chan1024, so the scheduler's channelizer fusion is bit-identical to the separate blocks.
+template <bool POW2>
+__global__ __launch_bounds__(kBlock) void k_mulc_vec(const float2* __restrict__ in, float2* __restrict__ out,
+                                                     const float2* __restrict__ k, int vlen, int64_t n)
+{
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+        const int j = POW2 ? (int)(i & (int64_t)(vlen - 1)) : (int)(i % vlen);
+        out[i] = cmul(in[i], k[j]);
+    }
+}
+
 template <int OP>
 __device__ __forceinline__ float2 bin(float2 a, float2 b)
 {
@@ -345,6 +358,23 @@ int nsh_add_cc(const float* a, const float* b, float* out, int64_t n, void* stre
 int nsh_mul_cc(const float* a, const float* b, float* out, int64_t n, void* stream)
 {
     return launch_bin<1>(a, b, out, n, nsh::S(stream), "nsh_mul_cc");
+}
+
+int nsh_mul_const_vcc(const float* in, float* out, const float* k_dev, int vlen, int64_t nitems, void* stream)
+{
+    if (vlen <= 0 || nitems < 0) return nsh::fail_msg("nsh_mul_const_vcc: bad vlen or item count");
+    const int64_t n = nitems * (int64_t)vlen;
+    if (n == 0) return 0;
+    hipStream_t s = nsh::S(stream);
+    const unsigned grid = nsh::stream_grid(n, kBlock);
+    if ((vlen & (vlen - 1)) == 0)
+        hipLaunchKernelGGL(k_mulc_vec<true>, dim3(grid), dim3(kBlock), 0, s, (const float2*)in, (float2*)out,
+                           (const float2*)k_dev, vlen, n);
+    else
+        hipLaunchKernelGGL(k_mulc_vec<false>, dim3(grid), dim3(kBlock), 0, s, (const float2*)in, (float2*)out,
+                           (const float2*)k_dev, vlen, n);
+    NSH_CK_LAUNCH("nsh_mul_const_vcc");
+    return 0;
 }
 
 int nsh_synth_cf32(float* out, int64_t n, uint64_t first_index, uint64_t seed, void* stream)

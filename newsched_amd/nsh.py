@@ -53,6 +53,7 @@ SIGNATURES = {
     "nsh_mul_const_chain_cc": (_i, [_vp, _vp, _i64, C.POINTER(_f), _i, _vp]),
     "nsh_add_cc": (_i, [_vp, _vp, _vp, _i64, _vp]),
     "nsh_mul_cc": (_i, [_vp, _vp, _vp, _i64, _vp]),
+    "nsh_mul_const_vcc": (_i, [_vp, _vp, _vp, _i, _i64, _vp]),
     "nsh_synth_cf32": (_i, [_vp, _i64, _u64, _u64, _vp]),
     "nsh_fir_plan_create": (_i, [_i, C.POINTER(_f), _i, _i, _i, C.POINTER(_vp)]),
     "nsh_fir_plan_destroy": (_i, [_vp]),
@@ -131,6 +132,11 @@ def add_cc(a, b, y, n: int, stream=None):
 
 def mul_cc(a, b, y, n: int, stream=None):
     check(lib().nsh_mul_cc(ptr(a), ptr(b), ptr(y), n, stream_ptr(stream)), "nsh_mul_cc")
+
+
+def mul_const_vcc(x, y, k, vlen: int, nitems: int, stream=None):
+    """y[i][j] = x[i][j] * k[j] over nitems items of vlen samples (k: device, vlen complex)."""
+    check(lib().nsh_mul_const_vcc(ptr(x), ptr(y), ptr(k), vlen, nitems, stream_ptr(stream)), "nsh_mul_const_vcc")
 
 
 def synth(y, n: int, first_index: int = 0, seed: int = 0x6E736368, stream=None):

@@ -42,5 +42,11 @@ constexpr size_t max_fused_stages = 16;
 // of their output port and carry no custom buffer or a hip_buffer of type D2D.
 fusion_result fuse_elementwise_cc(flat_graph_sptr fg);
 
+// Channelizer pass: fft_vcc(forward, 1024) -> multiply_const_vcc(w, 1024) -> fft_vcc(inverse,
+// 1024), linked as above (single D2D edges, same tag policy), becomes ONE channelizer_vcc(w):
+// the spectrum stays in registers (one HBM pass instead of three) and, with the same butterfly
+// and product rounding in k_chan1024 as in the three kernels, the output is bit-identical.
+fusion_result fuse_channelizer(flat_graph_sptr fg);
+
 } // namespace hip
 } // namespace gr

@@ -1,4 +1,5 @@
 // Elementwise-chain fusion pass for scheduler_hip (see gnuradio/hip_fusion.hpp).
+#include <gnuradio/blocklib/hip/fft.hpp>
 #include <gnuradio/blocklib/hip/multiply_const.hpp>
 #include <gnuradio/hip_buffer.hpp>
 #include <gnuradio/hip_fusion.hpp>
@@ -23,6 +24,58 @@ bool device_to_device(const edge_sptr& e)
     return p && p->buffer_type() == hip_buffer_type::D2D;
 }
 
+} // namespace
+
+namespace {
+// Replace each chain (a path of blocks joined by single edges) by one block with the head's
+// input port and the tail's output port; shared by the passes.
+flat_graph_sptr rewrite_chains(flat_graph_sptr fg, const std::vector<std::vector<block_sptr>>& chains,
+                               const std::vector<block_sptr>& fused)
+{
+    auto as_block = [](const node_sptr& n) { return std::dynamic_pointer_cast<block>(n); };
+    std::map<block*, std::pair<size_t, block_sptr>> owner;
+    for (size_t i = 0; i < chains.size(); ++i)
+        for (auto& b : chains[i]) owner[b.get()] = { i, fused[i] };
+    auto g = std::make_shared<flat_graph>();
+    for (auto& e : fg->edges()) {
+        auto s = as_block(e->src().node());
+        auto d = as_block(e->dst().node());
+        auto so = s ? owner.find(s.get()) : owner.end();
+        auto dn = d ? owner.find(d.get()) : owner.end();
+        if (so == owner.end() && dn == owner.end()) {
+            g->edges().push_back(e);
+            continue;
+        }
+        e->src().port()->disconnect(e->dst().port());
+        e->dst().port()->disconnect(e->src().port());
+        if (so != owner.end() && dn != owner.end() && so->second.first == dn->second.first) continue; // interior
+        auto src = so == owner.end() ? e->src()
+                                     : node_endpoint(so->second.second, so->second.second->output_stream_ports()[0]);
+        auto dst = dn == owner.end() ? e->dst()
+                                     : node_endpoint(dn->second.second, dn->second.second->input_stream_ports()[0]);
+        auto ne = g->connect(src, dst);
+        if (e->has_custom_buffer()) ne->set_custom_buffer(e->buffer_factory(), e->buf_properties());
+    }
+    auto move_links = [](const port_sptr& from, const port_sptr& to) {
+        for (auto& peer : from->connected_ports()) {
+            peer->disconnect(from);
+            from->disconnect(peer);
+            peer->connect(to);
+            to->connect(peer);
+        }
+    };
+    for (size_t i = 0; i < chains.size(); ++i) {
+        move_links(chains[i].front()->input_stream_ports()[0], fused[i]->input_stream_ports()[0]);
+        move_links(chains[i].back()->output_stream_ports()[0], fused[i]->output_stream_ports()[0]);
+    }
+    for (auto& o : fg->orphan_nodes()) g->add_orphan_node(o);
+    for (auto& f : fused) {
+        bool linked = false;
+        for (auto& e : g->edges()) linked = linked || e->src().node() == f || e->dst().node() == f;
+        if (!linked) g->add_orphan_node(f);
+    }
+    return g;
+}
 } // namespace
 
 fusion_result fuse_elementwise_cc(flat_graph_sptr fg)
@@ -95,10 +148,6 @@ fusion_result fuse_elementwise_cc(flat_graph_sptr fg)
     }
     if (chains.empty()) return r;
 
-    // Rewrite. Every edge touching a chain member is interior to its chain (dropped), into a
-    // chain head, or out of a chain tail; the latter two are re-made on the fused block
-    // (both ends when one segment of a split chain feeds the next).
-    std::map<block*, std::pair<size_t, block_sptr>> owner; // member -> (chain index, fused block)
     for (size_t i = 0; i < chains.size(); ++i) {
         auto& c = chains[i];
         std::vector<gr_complex> ks;
@@ -107,51 +156,60 @@ fusion_result fuse_elementwise_cc(flat_graph_sptr fg)
         auto f = multiply_const_chain_cc::make(ks, vlen);
         f->set_tag_propagation_policy(c.front()->tag_propagation_policy());
         f->set_alias("fused(" + c.front()->alias() + ".." + c.back()->alias() + ")");
-        for (auto& b : c) owner[b.get()] = { i, f };
         r.fused.push_back(f);
     }
-    auto g = std::make_shared<flat_graph>();
-    for (auto& e : fg->edges()) {
-        auto s = as_block(e->src().node());
-        auto d = as_block(e->dst().node());
-        auto so = s ? owner.find(s.get()) : owner.end();
-        auto dn = d ? owner.find(d.get()) : owner.end();
-        if (so == owner.end() && dn == owner.end()) {
-            g->edges().push_back(e);
-            continue;
-        }
-        e->src().port()->disconnect(e->dst().port());
-        e->dst().port()->disconnect(e->src().port());
-        if (so != owner.end() && dn != owner.end() && so->second.first == dn->second.first) continue; // interior
-        auto src = so == owner.end() ? e->src()
-                                     : node_endpoint(so->second.second, so->second.second->output_stream_ports()[0]);
-        auto dst = dn == owner.end() ? e->dst()
-                                     : node_endpoint(dn->second.second, dn->second.second->input_stream_ports()[0]);
-        auto ne = g->connect(src, dst);
-        if (e->has_custom_buffer()) ne->set_custom_buffer(e->buffer_factory(), e->buf_properties());
-    }
-    // Links that are not edges of this partition (an in-process domain crossing keeps the
-    // original cross-domain port pair connected for notifications) move to the fused block.
-    auto move_links = [](const port_sptr& from, const port_sptr& to) {
-        for (auto& peer : from->connected_ports()) {
-            peer->disconnect(from);
-            from->disconnect(peer);
-            peer->connect(to);
-            to->connect(peer);
-        }
-    };
-    for (size_t i = 0; i < chains.size(); ++i) {
-        move_links(chains[i].front()->input_stream_ports()[0], r.fused[i]->input_stream_ports()[0]);
-        move_links(chains[i].back()->output_stream_ports()[0], r.fused[i]->output_stream_ports()[0]);
-    }
-    for (auto& o : fg->orphan_nodes()) g->add_orphan_node(o);
-    for (auto& f : r.fused) {
-        bool linked = false;
-        for (auto& e : g->edges()) linked = linked || e->src().node() == f || e->dst().node() == f;
-        if (!linked) g->add_orphan_node(f);
-    }
+    // Every edge touching a chain member is interior to its chain (dropped), into a chain
+    // head, or out of a chain tail; the latter two are re-made on the fused block (both ends
+    // when one segment of a split chain feeds the next). Links that are not edges of this
+    // partition (an in-process domain crossing keeps the original cross-domain port pair
+    // connected for notifications) move to the fused block.
+    auto g = rewrite_chains(fg, chains, r.fused);
     r.chains = std::move(chains);
     r.graph = g;
+    return r;
+}
+
+
+fusion_result fuse_channelizer(flat_graph_sptr fg)
+{
+    fusion_result r;
+    r.graph = fg;
+    auto as_block = [](const node_sptr& n) { return std::dynamic_pointer_cast<block>(n); };
+    // the single out-edge of b's single output port, if it goes to a block, else null
+    std::map<block*, std::vector<edge_sptr>> outs;
+    std::map<block*, int> ins;
+    for (auto& e : fg->edges()) {
+        if (auto s = as_block(e->src().node())) outs[s.get()].push_back(e);
+        if (auto d = as_block(e->dst().node())) ins[d.get()]++;
+    }
+    auto next = [&](const block_sptr& b) -> block_sptr {
+        auto it = outs.find(b.get());
+        if (it == outs.end() || it->second.size() != 1 || b->output_stream_ports().size() != 1) return nullptr;
+        auto e = it->second[0];
+        auto d = as_block(e->dst().node());
+        if (!d || !device_to_device(e) || ins[d.get()] != 1 || d->input_stream_ports().size() != 1) return nullptr;
+        if (d->tag_propagation_policy() != b->tag_propagation_policy()) return nullptr;
+        return d;
+    };
+    std::set<block*> used;
+    for (auto& b : fg->calc_used_blocks()) {
+        auto f1 = std::dynamic_pointer_cast<fft_vcc>(b);
+        if (!f1 || !f1->forward() || used.count(b.get())) continue;
+        auto m = std::dynamic_pointer_cast<multiply_const_vcc>(next(b));
+        if (!m || m->k().size() != 1024) continue;
+        auto f2 = std::dynamic_pointer_cast<fft_vcc>(next(m));
+        if (!f2 || f2->forward() || used.count(f2.get())) continue;
+        auto c = channelizer_vcc::make(m->k());
+        c->set_tag_propagation_policy(b->tag_propagation_policy());
+        c->set_alias("fused(" + b->alias() + ".." + f2->alias() + ")");
+        r.chains.push_back({ b, m, f2 });
+        r.fused.push_back(c);
+        used.insert(b.get());
+        used.insert(m.get());
+        used.insert(f2.get());
+    }
+    if (r.fused.empty()) return r;
+    r.graph = rewrite_chains(fg, r.chains, r.fused);
     return r;
 }
 

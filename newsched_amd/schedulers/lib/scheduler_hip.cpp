@@ -41,6 +41,10 @@ void scheduler_hip::initialize(flat_graph_sptr fg, flowgraph_monitor_sptr fgmon,
     release_fused();
     if (_fusion) {
         _plan = hip::fuse_elementwise_cc(fg);
+        auto ch = hip::fuse_channelizer(_plan.graph);
+        _plan.graph = ch.graph;
+        _plan.fused.insert(_plan.fused.end(), ch.fused.begin(), ch.fused.end());
+        _plan.chains.insert(_plan.chains.end(), ch.chains.begin(), ch.chains.end());
         fg = _plan.graph;
     }
     scheduler_mt::initialize(fg, fgmon, nbr);

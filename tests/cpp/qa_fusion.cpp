@@ -9,6 +9,7 @@
 #include <gnuradio/blocklib/blocks/vector_source.hpp>
 #include <gnuradio/blocklib/hip/arith.hpp>
 #include <gnuradio/blocklib/hip/copy.hpp>
+#include <gnuradio/blocklib/hip/fft.hpp>
 #include <gnuradio/blocklib/hip/multiply_const.hpp>
 #include <gnuradio/flowgraph.hpp>
 #include <gnuradio/hip_buffer.hpp>
@@ -176,4 +177,68 @@ TEST(Fusion, LongChainsSplitAtStageLimit)
     // the fused blocks form one path src -> F0 -> F1 -> F2 -> snk
     EXPECT_TRUE(r.graph->edges().size() == 4u);
     EXPECT_TRUE(r.graph->calc_used_blocks().size() == 5u);
+}
+
+static std::vector<gr_complex> W1024()
+{
+    std::vector<gr_complex> w(1024);
+    for (int b = 0; b < 1024; ++b) w[b] = gr_complex(1.0f / (1 + b), 0.5f);
+    return w;
+}
+
+// src -[H2D]-> fft -> w -> ifft -[D2H]-> sink becomes src -> channelizer(w) -> sink
+TEST(Fusion, ChannelizerFromBlocks)
+{
+    auto src = blocks::vector_source_c::make(std::vector<gr_complex>(2048), false, 1024);
+    auto f1 = hip::fft_vcc::make(1024, true);
+    auto m = hip::multiply_const_vcc::make(W1024());
+    auto f2 = hip::fft_vcc::make(1024, false);
+    auto snk = blocks::null_sink::make(1024 * sizeof(gr_complex));
+    auto fg = flowgraph::make();
+    fg->connect(src, 0, f1, 0)->set_custom_buffer(HIP_BUFFER_ARGS_H2D);
+    fg->connect(f1, 0, m, 0);
+    fg->connect(m, 0, f2, 0)->set_custom_buffer(HIP_BUFFER_ARGS_D2D);
+    fg->connect(f2, 0, snk, 0)->set_custom_buffer(HIP_BUFFER_ARGS_D2H);
+    auto r = hip::fuse_channelizer(flat(fg));
+    ASSERT_TRUE(r.fused.size() == 1u);
+    auto c = std::dynamic_pointer_cast<hip::channelizer_vcc>(r.fused[0]);
+    ASSERT_TRUE(c != nullptr);
+    EXPECT_TRUE(c->w() == W1024());
+    EXPECT_TRUE(r.chains[0].size() == 3u && r.chains[0][0] == f1 && r.chains[0][2] == f2);
+    auto& e = r.graph->edges();
+    ASSERT_TRUE(e.size() == 2u);
+    EXPECT_TRUE(e[0]->src().node() == src && e[0]->dst().port() == c->input_stream_ports()[0]);
+    EXPECT_TRUE(e[1]->src().port() == c->output_stream_ports()[0] && e[1]->dst().node() == snk);
+    auto p0 = std::dynamic_pointer_cast<hip_buffer_properties>(e[0]->buf_properties());
+    auto p1 = std::dynamic_pointer_cast<hip_buffer_properties>(e[1]->buf_properties());
+    EXPECT_TRUE(p0 && p0->buffer_type() == hip_buffer_type::H2D);
+    EXPECT_TRUE(p1 && p1->buffer_type() == hip_buffer_type::D2H);
+    EXPECT_TRUE(connected(src->output_stream_ports()[0], c->input_stream_ports()[0]));
+    EXPECT_TRUE(connected(snk->input_stream_ports()[0], c->output_stream_ports()[0]));
+    EXPECT_TRUE(r.graph->calc_used_blocks().size() == 3u);
+}
+
+// Not the pattern: two forward transforms, a host-visible interior edge, a fan-out of the
+// spectrum, an ifft first.
+TEST(Fusion, ChannelizerBoundaries)
+{
+    auto run = [](int variant) {
+        auto src = blocks::vector_source_c::make(std::vector<gr_complex>(2048), false, 1024);
+        auto f1 = hip::fft_vcc::make(1024, variant != 3);
+        auto m = hip::multiply_const_vcc::make(W1024());
+        auto f2 = hip::fft_vcc::make(1024, variant == 0);
+        auto snk = blocks::null_sink::make(1024 * sizeof(gr_complex));
+        auto fg = flowgraph::make();
+        fg->connect(src, 0, f1, 0);
+        auto e1 = fg->connect(f1, 0, m, 0);
+        if (variant == 1) e1->set_custom_buffer(HIP_BUFFER_ARGS_D2H);
+        fg->connect(m, 0, f2, 0);
+        fg->connect(f2, 0, snk, 0);
+        if (variant == 2) fg->connect(f1, 0, blocks::null_sink::make(1024 * sizeof(gr_complex)), 0);
+        return hip::fuse_channelizer(flat(fg)).fused.size();
+    };
+    EXPECT_TRUE(run(0) == 0u); // fft -> w -> fft (both forward)
+    EXPECT_TRUE(run(1) == 0u); // spectrum crosses to the host
+    EXPECT_TRUE(run(2) == 0u); // spectrum fans out
+    EXPECT_TRUE(run(3) == 0u); // ifft -> w -> fft
 }

@@ -244,6 +244,46 @@ TEST(HipDomain, ChannelizerC4)
     EXPECT_TRUE(close_normwise(got, yr));
 }
 
+// C4 as separate blocks: fft_vcc -> multiply_const_vcc(w) -> fft_vcc(inverse). scheduler_hip
+// fuses the three into one channelizer launch; fused, unfused (three kernels, two interior
+// HBM edges) and the channelizer_vcc block must agree bit for bit.
+TEST(HipDomain, ChannelizerFromBlocksFused)
+{
+    const size_t frames = 300, n = frames * 1024;
+    std::vector<gr_complex> w(1024);
+    for (int b = 0; b < 1024; ++b) w[b] = gr_complex((1.0f + 0.5f * std::cos(2 * (float)M_PI * b / 1024)) / 1024.0f, 0.25f / (1 + b));
+    auto run = [&](int how) { // 0: blocks fused, 1: blocks unfused, 2: channelizer_vcc
+        auto src = hip::synth_source::make(0, n, 0x6E736368, 1024);
+        auto snk = blocks::vector_sink_c::make(1024, frames);
+        auto fg = flowgraph::make();
+        if (how == 2) {
+            auto ch = hip::channelizer_vcc::make(w);
+            fg->connect(src, 0, ch, 0);
+            fg->connect(ch, 0, snk, 0)->set_custom_buffer(HIP_BUFFER_ARGS_D2H);
+        } else {
+            auto f1 = hip::fft_vcc::make(1024, true);
+            auto m = hip::multiply_const_vcc::make(w);
+            auto f2 = hip::fft_vcc::make(1024, false);
+            fg->connect(src, 0, f1, 0);
+            fg->connect(f1, 0, m, 0);
+            fg->connect(m, 0, f2, 0);
+            fg->connect(f2, 0, snk, 0)->set_custom_buffer(HIP_BUFFER_ARGS_D2H);
+        }
+        auto sched = schedulers::scheduler_hip::make("hip", 0, 1u << 20);
+        sched->set_fusion(how != 1);
+        fg->set_scheduler(sched);
+        fg->validate();
+        const size_t nfused = sched->fusion_plan().fused.size();
+        EXPECT_TRUE(nfused == (how == 0 ? 1u : 0u));
+        fg->run();
+        return snk->data();
+    };
+    const auto yf = run(0), yu = run(1), yc = run(2);
+    ASSERT_TRUE(yf.size() == n && yu.size() == n && yc.size() == n);
+    EXPECT_TRUE(yf == yu);
+    EXPECT_TRUE(yf == yc);
+}
+
 TEST(HipDomain, DecimatingChainC5)
 {
     const size_t n = 1u << 20;

@@ -47,6 +47,7 @@ def test_tags_through_device_edges():
 
 
 def test_fusion_pass_graph_rewrite():
-    """scheduler_hip's elementwise-fusion pass as host logic (no device touched)."""
+    """scheduler_hip's fusion passes (elementwise chains, fft -> w -> ifft channelizer) as host
+    logic (no device touched)."""
     out = run("qa_fusion", 120)
-    assert "4 test(s), 0 failure(s)" in out
+    assert "6 test(s), 0 failure(s)" in out

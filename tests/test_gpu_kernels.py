@@ -116,6 +116,19 @@ def test_add_mul_cc_bit_exact(torch_cuda, n):
     np.testing.assert_array_equal(host(dy), orc.mul_cc(a, b))
 
 
+@pytest.mark.parametrize("vlen,nitems", [(1024, 37), (1, 1000), (3, 777), (1024, 0)])
+def test_mul_const_vcc_bitexact(torch_cuda, vlen, nitems):
+    """multiply_const_vcc: x[i][j] * k[j], each product rounded as the oracle's mul_cc."""
+    torch = torch_cuda
+    x = orc.synth(max(nitems * vlen, 1), 91)[: nitems * vlen]
+    k = orc.synth(vlen, 92)
+    dx, dk = dev(torch, x), dev(torch, k)
+    dy = torch.zeros(max(nitems * vlen, 1), dtype=torch.complex64, device="cuda")
+    nsh.mul_const_vcc(dx, dy, dk, vlen, nitems)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(host(dy)[: nitems * vlen], orc.mul_cc(x, np.tile(k, nitems)))
+
+
 # "mfma" is the default matrix-core kernel (decim 1: per-chunk scaled fp16x2, k_fir_mfma9),
 # "mfma_x3" forces the bf16x3 six-product kernel (k_fir_mfma2), "mfma16" the 16-sample form.
 # "mfma_v8" / "mfma_v10" are the other fp16x2 kernels (NSH_FIR_MFMA_VARIANT 8: k_fir_mfma8,
