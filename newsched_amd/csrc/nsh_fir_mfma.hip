@@ -2171,7 +2171,7 @@ int launch_v11(const nsh_fir_plan* p, const float2* in, const float2* hin, float
     const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
     int n_cu = 256;
     (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, p->dev);
-    const int64_t max_grid = (int64_t)n_cu * 2;
+    const int64_t max_grid = (int64_t)n_cu * 2; // launch_v9's longer grids measured 4-7 % slower here
     const unsigned grid = (unsigned)(nchunks < max_grid ? nchunks : max_grid);
     hipLaunchKernelGGL((k_fir_mfma11<D, QH>), dim3(grid), dim3(G::NT), G::LDS, s, in, hin, hout, out,
                        (const _Float16*)p->fragd8_dev, (const float*)p->taps_dev, p->L, p->sh8, n_out);
@@ -2277,7 +2277,15 @@ int launch_v9(const nsh_fir_plan* p, const float2* in, const float2* hin, float2
     const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
     int n_cu = 256;
     (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, p->dev);
-    const int64_t max_grid = (int64_t)n_cu * 2;
+    // Workgroups over the whole launch (2 resident per CU at a time): about 32 chunks each, at
+    // least 2 and at most 16 per CU. Long streams then walk in shorter contiguous ranges, which
+    // keeps the window of addresses in flight compact: at 2^28 samples 16 per CU runs 807 us vs
+    // 855 with 2 (tools/fir_variants.py, same process); at 2^25-2^27 the rule changes nothing.
+    int64_t max_grid = (int64_t)n_cu * 2;
+    if (p->wg_per_cu > 0)
+        max_grid = (int64_t)n_cu * p->wg_per_cu; // NSH_FIR_WG_PER_CU (A/B)
+    else if (nchunks / 32 > max_grid)
+        max_grid = std::min<int64_t>(nchunks / 32, (int64_t)n_cu * 16);
     const unsigned grid = (unsigned)(nchunks < max_grid ? nchunks : max_grid);
     hipLaunchKernelGGL((k_fir_mfma9<Q>), dim3(grid), dim3(G::NT), G::LDS, s, in, hin, hout, out,
                        (const f16x8*)p->frag8_dev, (const float*)p->taps_dev, p->L, p->sh8, n_out);
@@ -2449,6 +2457,10 @@ int nsh_fir_mfma_prepare_decim(nsh_fir_plan* p)
 int nsh_fir_mfma_prepare(nsh_fir_plan* p)
 {
     if (const char* v = std::getenv("NSH_FIR_MFMA_VARIANT")) p->variant = std::atoi(v);
+    if (const char* v = std::getenv("NSH_FIR_WG_PER_CU")) { // A/B only
+        const int w = std::atoi(v);
+        if (w >= 1 && w <= 64) p->wg_per_cu = w;
+    }
     if (p->D > 1) return nsh_fir_mfma_prepare_decim(p);
     const int Q = (p->L + 30) / 32 + 1;
     const int S = 2 * Q;

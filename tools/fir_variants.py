@@ -21,9 +21,14 @@ y = torch.empty_like(x)
 hin = torch.zeros(126, dtype=torch.complex64, device="cuda")
 hout = torch.zeros_like(hin)
 plans = {}
-for v in [int(t) for t in os.environ.get("VARIANTS", "6,7,21").split(",")]:
-    os.environ["NSH_FIR_MFMA_VARIANT"] = str(v)
-    plans[v] = nsh.FirPlan(h, 1, nsh.FIR_MFMA)
+# VARIANTS entries: "v" or "v:g" (g = NSH_FIR_WG_PER_CU for that plan)
+for spec in os.environ.get("VARIANTS", "6,7,21").split(","):
+    v, _, g = spec.partition(":")
+    os.environ["NSH_FIR_MFMA_VARIANT"] = v
+    if g:
+        os.environ["NSH_FIR_WG_PER_CU"] = g
+    plans[spec] = nsh.FirPlan(h, 1, nsh.FIR_MFMA)
+    os.environ.pop("NSH_FIR_WG_PER_CU", None)
 os.environ.pop("NSH_FIR_MFMA_VARIANT")
 xs = x[:20000].cpu().numpy()
 ref = orc.fir_ccf(xs, h)
