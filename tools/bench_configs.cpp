@@ -22,6 +22,7 @@
 #include <gnuradio/blocklib/hip/fft.hpp>
 #include <gnuradio/blocklib/hip/fir_filter_ccf.hpp>
 #include <gnuradio/blocklib/hip/multiply_const.hpp>
+#include <gnuradio/domain_adapter_direct.hpp>
 #include <gnuradio/flowgraph.hpp>
 #include <gnuradio/hip_buffer.hpp>
 #include <gnuradio/hip_context.hpp>
@@ -333,6 +334,45 @@ int main(int argc, char** argv)
              ", \"hbm_bytes_per_input_sample\": 8.5, \"achieved_GBs\": " + num(gbs) + ", \"hbm_frac\": " + num(gbs / hbm, 4) +
              ", \"parity_tail_rel_err\": " + num(rel_err(y, r), 9) + ", \"cpu_baseline\": {\"value\": " + num(nc / cs / 1e6, 2) +
              ", \"unit\": \"MSamples/s (input)\", \"sample\": \"2^24 samples, vector_source->head->4x blocks::fir_filter_ccf(decim 2)->null_sink, scheduler_mt thread per block\"}}");
+    }
+    // ---- C3 with host endpoints: the PCIe-inclusive rate (not the metric: bench.py's input is
+    // resident). vector_source(repeat) -> head -[H2D]-> hip::fir_filter_ccf -[D2H]-> null_sink,
+    // host blocks in a scheduler_mt domain (thread per block), the FIR in scheduler_hip.
+    {
+        const int64_t nh = (int64_t)1 << 26;
+        const auto h = lowpass(127, 0.1); // firwin(127, 0.2)
+        auto run = [&](size_t buf) {
+            auto src = blocks::vector_source_c::make(synth(1 << 20), true);
+            auto head = blocks::head::make(sizeof(gr_complex), (size_t)nh);
+            auto fir = hip::fir_filter_ccf::make(h, 1);
+            auto snk = blocks::null_sink::make(sizeof(gr_complex));
+            auto fg = flowgraph::make();
+            fg->connect(src, 0, head, 0);
+            fg->connect(head, 0, fir, 0)->set_custom_buffer(HIP_BUFFER_ARGS_H2D);
+            fg->connect(fir, 0, snk, 0)->set_custom_buffer(HIP_BUFFER_ARGS_D2H);
+            auto cpu = schedulers::scheduler_mt::make("cpu", (unsigned)buf);
+            auto gpu = schedulers::scheduler_hip::make("gpu", 0, buf);
+            fg->add_scheduler(cpu);
+            fg->add_scheduler(gpu);
+            auto da = domain_adapter_direct_conf::make(buffer_preference_t::DOWNSTREAM);
+            domain_conf_vec dc{ domain_conf(cpu, { src, head, snk }, da), domain_conf(gpu, { fir }, da) };
+            fg->partition(dc);
+            fg->run(); // warm-up
+            std::vector<double> t;
+            for (int i = 0; i < 5; ++i) {
+                const auto t0 = clk::now();
+                fg->run();
+                t.push_back(std::chrono::duration<double>(clk::now() - t0).count());
+            }
+            return median(t);
+        };
+        for (size_t buf : { (size_t)16 << 20, (size_t)64 << 20 }) {
+            const double s = run(buf);
+            emit("{\"config\": \"C3-host\", \"variant\": \"vector_source -> head -[H2D]-> hip::fir_filter_ccf -[D2H]-> null_sink, " +
+                 std::to_string(buf >> 20) + " MiB buffers (PCIe-inclusive; not the metric)\", \"value\": " + num(nh / s / 1e6) +
+                 ", \"unit\": \"MSamples/s\", \"ms_per_run\": " + num(s * 1e3, 3) + ", \"pcie_GBs_each_way\": " +
+                 num(8.0 * nh / s / 1e9, 2) + "}");
+        }
     }
     return 0;
 }
