@@ -192,32 +192,32 @@ __global__ __launch_bounds__(NT) void k_fft1024(const float2* __restrict__ in, f
     }
 }
 
-__global__ __launch_bounds__(NT) void k_chan1024(const float2* __restrict__ in, float2* __restrict__ out, int64_t nframes,
-                                                 const float2* __restrict__ tw_g, const float2* __restrict__ w)
+// No register prefetch of the next frame here (unlike k_fft1024): without it and with the
+// weights in LDS the kernel fits 168 VGPRs, i.e. 3 workgroups (12 waves) per CU, and that
+// occupancy hides the load latency better: 816 vs 858 us per 2^28 samples
+// (tools/probe/fft_ab.py history in DESIGN.md section 4).
+__global__ __launch_bounds__(NT, 2) void k_chan1024(const float2* __restrict__ in, float2* __restrict__ out, int64_t nframes,
+                                                    const float2* __restrict__ tw_g, const float2* __restrict__ w)
 {
     __shared__ float2 tw[N];
+    __shared__ float2 wl[N];
     __shared__ float2 img_all[FPW * WLDS];
-    for (int t = threadIdx.x; t < N; t += NT) tw[t] = tw_g[t];
+    for (int t = threadIdx.x; t < N; t += NT) {
+        tw[t] = tw_g[t];
+        wl[t] = w[t];
+    }
     __syncthreads();
     float2* img = img_all + (threadIdx.x >> 6) * WLDS;
     const int j = threadIdx.x & 63;
-    float2 wr[16]; // this lane's spectral weights W[j + 64 m]
-#pragma unroll
-    for (int m = 0; m < 16; ++m) wr[m] = w[j + 64 * m];
     const int64_t stride = (int64_t)gridDim.x * FPW;
-    int64_t f = (int64_t)blockIdx.x * FPW + (threadIdx.x >> 6);
-    if (f >= nframes) return;
-    float2 v[16], nx[16];
-    load_frame16(v, in, f, nframes);
-    for (; f < nframes; f += stride) {
-        load_frame16(nx, in, f + stride, nframes);
+    float2 v[16];
+    for (int64_t f = (int64_t)blockIdx.x * FPW + (threadIdx.x >> 6); f < nframes; f += stride) {
+        load_frame16(v, in, f, nframes);
         fft_wave<false>(v, img, tw);
 #pragma unroll
-        for (int m = 0; m < 16; ++m) v[m] = cmul(v[m], wr[m]);
+        for (int m = 0; m < 16; ++m) v[m] = cmul(v[m], wl[j + 64 * m]);
         fft_wave<true>(v, img, tw);
         store_frame16(v, out, f, nframes);
-#pragma unroll
-        for (int m = 0; m < 16; ++m) v[m] = nx[m];
     }
 }
 
