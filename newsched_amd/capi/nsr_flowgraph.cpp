@@ -99,6 +99,7 @@ int nsr_fir_bench_create(int dev, const float* taps, int ntaps, int algo, int64_
         b->fg->connect(b->fir, 0, snk, 0); // scheduler default: hip_buffer D2D
         b->sched = schedulers::scheduler_hip::make("hip" + std::to_string(dev), dev, out_buf_bytes);
         b->fg->set_scheduler(b->sched);
+        b->fg->set_wait_spin_us(5000); // one run is ~1 ms: poll for its end instead of sleeping
         b->fg->validate();
 
         auto in_ring = std::dynamic_pointer_cast<hip_buffer>(b->sched->buffers()->get_input_buffer(b->fir->input_stream_ports()[0]));

@@ -9,6 +9,7 @@
 // reports to its scheduler, which sends FLUSHED here once all its threads have. wait()
 // returns when every scheduler has flushed -- no fixed sleep anywhere.
 #pragma once
+#include <atomic>
 #include <condition_variable>
 #include <cstdint>
 #include <exception>
@@ -56,6 +57,9 @@ public:
     void start();                                    // arm for a new run
     void stop() { push_message(fg_monitor_message(fg_monitor_message_t::KILL, 0, 0)); }
     void wait();                                     // block until all flushed (or killed)
+    // wait() first polls for this long (us) before sleeping: the caller's thread is idle
+    // anyway, and a futex wake-up after the last scheduler flushed costs several us per run
+    void set_wait_spin_us(int us) { _wait_spin_us = us; }
     bool run_complete();
     void report_error(std::exception_ptr e);         // a worker thread failed
     std::exception_ptr error();
@@ -69,6 +73,8 @@ private:
     std::condition_variable _cv;
     std::map<int64_t, bool> _flushed;
     bool _killed = false;
+    std::atomic<bool> _complete{ false };
+    int _wait_spin_us = 0;
     uint64_t _done_blocks = 0;
     std::exception_ptr _error;
 };

@@ -5,6 +5,7 @@
 #include <gnuradio/graph_utils.hpp>
 
 #include <algorithm>
+#include <chrono>
 
 namespace gr {
 
@@ -18,6 +19,7 @@ void flowgraph_monitor::push_message(fg_monitor_message msg)
     case fg_monitor_message_t::KILL: _killed = true; break;
     default: break;
     }
+    if (_killed || run_complete()) _complete.store(true, std::memory_order_release);
     _cv.notify_all();
 }
 
@@ -26,6 +28,7 @@ void flowgraph_monitor::start()
     std::lock_guard<std::mutex> g(_m);
     _flushed.clear();
     _killed = false;
+    _complete.store(false, std::memory_order_release);
     _done_blocks = 0;
     _error = nullptr;
 }
@@ -39,6 +42,11 @@ bool flowgraph_monitor::run_complete()
 
 void flowgraph_monitor::wait()
 {
+    if (_wait_spin_us > 0) {
+        const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(_wait_spin_us);
+        while (!_complete.load(std::memory_order_acquire) && std::chrono::steady_clock::now() < until)
+            __builtin_ia32_pause();
+    }
     std::unique_lock<std::mutex> l(_m);
     _cv.wait(l, [this] { return _killed || run_complete(); });
 }
@@ -125,6 +133,7 @@ void flowgraph::partition(std::vector<domain_conf>& confs)
                                       }),
                        d_schedulers.end());
     d_fgmon = std::make_shared<flowgraph_monitor>(d_schedulers);
+    d_fgmon->set_wait_spin_us(d_wait_spin_us);
     auto parts = graph_utils::partition(base(), d_schedulers, confs);
     d_flat_subgraphs.clear();
     for (auto& p : parts) {
@@ -138,6 +147,7 @@ void flowgraph::validate()
 {
     if (d_schedulers.empty()) throw std::runtime_error("flowgraph::validate: no scheduler specified");
     d_fgmon = std::make_shared<flowgraph_monitor>(d_schedulers);
+    d_fgmon->set_wait_spin_us(d_wait_spin_us);
     d_flat_graph = flat_graph::make_flat(base());
     for (auto& s : d_schedulers) s->initialize(d_flat_graph, d_fgmon);
 }

@@ -65,6 +65,9 @@ thread_hooks scheduler_hip::hooks_for_group(const block_group_properties&)
     void* s = _stream;
     h.on_thread_start = [dev, s] { hip::bind_thread(dev, s); };
     h.on_flush = [s] { hip::check(nsh_stream_sync(s), "scheduler_hip: flush"); };
+    // one thread per GPU partition: spinning briefly on its queue takes the futex wake-up out
+    // of each run's start (the notification arrives within microseconds of the last one)
+    h.queue_spin_us = 200;
     return h;
 }
 

@@ -75,7 +75,7 @@ void thread_wrapper::thread_body(thread_wrapper* top)
     while (!top->d_thread_stopped) {
         scheduler_message_sptr msg;
         bool do_work = false;
-        bool got = blocking ? top->msgq.pop(msg) : top->msgq.try_pop(msg);
+        bool got = blocking ? top->msgq.pop(msg, top->_hooks.queue_spin_us) : top->msgq.try_pop(msg);
         while (got) {
             if (msg->type() == scheduler_message_t::SCHEDULER_ACTION) {
                 switch (std::static_pointer_cast<scheduler_action>(msg)->action()) {
