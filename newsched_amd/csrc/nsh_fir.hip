@@ -211,7 +211,6 @@ int nsh_fir_plan_destroy(void* plan)
     if (p->frag_dev) (void)hipFree(p->frag_dev);
     if (p->frag16_dev) (void)hipFree(p->frag16_dev);
     if (p->frag8_dev) (void)hipFree(p->frag8_dev);
-    if (p->frag10_dev) (void)hipFree(p->frag10_dev);
     if (p->fragd_dev) (void)hipFree(p->fragd_dev);
     if (p->fragd8_dev) (void)hipFree(p->fragd8_dev);
     delete p;

@@ -1003,8 +1003,8 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma7(const float2* __restrict__
     if (ch <= c_last) step(va, vb, ch);
 }
 
-// ---- v8: per-chunk scaled fp16x2 split, three products (default for decim 1) ----------------
-// Same Toeplitz GEMM, data movement and LDS row layout as v2, on v_mfma_f32_32x32x16_f16.
+// ---- fp16x2: per-chunk scaled split, three products (default for decim 1) -------------------
+// Same Toeplitz GEMM and LDS row layout as v2, on v_mfma_f32_32x32x16_f16.
 // fp16 keeps 11 significant bits, so a two-term split x = x0 + x1 (both RNE) keeps 22 and
 // three products x0h0 + x0h1 + x1h0 suffice (dropped x1h1 <= 2^-22 |xh|), where bf16 needs
 // three terms and six products: half the matrix work, which is what bounds v2 (DESIGN.md
@@ -1056,227 +1056,11 @@ __device__ __forceinline__ unsigned wave_max(unsigned v)
     for (int o = 32; o > 0; o >>= 1) v = max(v, (unsigned)__shfl_xor((int)v, o));
     return v;
 }
-// a scaled sample needs the exact path: non-finite, or nonzero below fp16's normal range
-__device__ __forceinline__ bool needs_exact(float xs)
-{
-    const unsigned m = mag(xs);
-    return m >= 0x7f800000u || (m != 0u && m < 0x38800000u);
-}
-
-// Split two consecutive samples (a, b) of one component, scaled by 2^s, into packed fp16
-// pairs (high terms, low terms).
-__device__ __forceinline__ void split16_pair(float a, float b, int s, unsigned& p0, unsigned& p1, bool& exact)
-{
-    const float as = __builtin_ldexpf(a, s), bs = __builtin_ldexpf(b, s);
-    const _Float16 a0 = (_Float16)as, b0 = (_Float16)bs;
-    const _Float16 a1 = (_Float16)(as - (float)a0), b1 = (_Float16)(bs - (float)b0);
-    p0 = __builtin_bit_cast(unsigned, f16x2{ a0, b0 });
-    p1 = __builtin_bit_cast(unsigned, f16x2{ a1, b1 });
-    exact = exact || needs_exact(as) || needs_exact(bs);
-}
-
-// One float4 (samples s, s+1 of both components) -> the four planes at local sample s.
-template <int Q>
-__device__ __forceinline__ void store_pair8(const float4& v, unsigned char* buf, int s, int sc, bool& exact)
-{
-    using G = geom8<Q>;
-    const int off = (s >> 5) * 80 + (s & 31) * 2;
-    unsigned r0, r1, i0, i1;
-    split16_pair(v.x, v.z, sc, r0, r1, exact);
-    split16_pair(v.y, v.w, sc, i0, i1, exact);
-    *reinterpret_cast<unsigned*>(buf + 0 * G::PLANE + off) = r0;
-    *reinterpret_cast<unsigned*>(buf + 1 * G::PLANE + off) = r1;
-    *reinterpret_cast<unsigned*>(buf + 2 * G::PLANE + off) = i0;
-    *reinterpret_cast<unsigned*>(buf + 3 * G::PLANE + off) = i1;
-}
-
-template <int Q>
-__device__ __forceinline__ void compute_tile8(const unsigned char* lds, const f16x8 (&B0)[2 * Q],
-                                              const f16x8 (&B1)[2 * Q], int a_base, int64_t n_tile, int h,
-                                              int phase, int64_t n_out, int unscale, float2* __restrict__ out)
-{
-    using G = geom8<Q>;
-    f32x16 acc_hi = {};
-    f32x16 acc_lo = {};
-#pragma unroll
-    for (int st = 0; st < 2 * Q; ++st) {
-        const int off = a_base - (st >> 1) * 80 + 32 * (st & 1);
-        const f16x8 A0 = *reinterpret_cast<const f16x8*>(lds + off);
-        const f16x8 A1 = *reinterpret_cast<const f16x8*>(lds + off + G::PLANE);
-        acc_hi = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, B0[st], acc_hi, 0, 0, 0);
-        acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, B1[st], acc_lo, 0, 0, 0);
-        acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, B0[st], acc_lo, 0, 0, 0);
-    }
-#pragma unroll
-    for (int reg = 0; reg < 8; ++reg) {
-        const int blk = (reg & 3) + 8 * (reg >> 2) + 4 * h;
-        const int64_t n = n_tile + 32 * blk + phase;
-        if (n < n_out) {
-            nf2 o = { __builtin_ldexpf(acc_hi[reg] + acc_lo[reg], unscale),
-                      __builtin_ldexpf(acc_hi[reg + 8] + acc_lo[reg + 8], unscale) };
-            __builtin_nontemporal_store(o, reinterpret_cast<nf2*>(out + n));
-        }
-    }
-}
-
-// The exact path for one chunk: fp32 direct form, outputs tid, tid + 256, ...
-__device__ __noinline__ void direct_chunk(const float2* __restrict__ in, const float2* __restrict__ hist,
-                                          const float* __restrict__ taps, int L, int64_t ch, int64_t n_out,
-                                          float2* __restrict__ out)
-{
-    for (int j = threadIdx.x; j < 2048; j += blockDim.x) {
-        const int64_t n = ch * 2048 + j;
-        if (n >= n_out) break;
-        float re = 0.f, im = 0.f;
-        for (int k = 0; k < L; ++k) {
-            const float2 x = virt(in, hist, n - k, n_out, L);
-            re = fmaf(taps[k], x.x, re);
-            im = fmaf(taps[k], x.y, im);
-        }
-        out[n] = make_float2(re, im);
-    }
-}
-
-template <int Q>
-__global__ __launch_bounds__(256, 2) void k_fir_mfma8(const float2* __restrict__ in,
-                                                     const float2* __restrict__ hist_in,
-                                                     float2* __restrict__ hist_out,
-                                                     float2* __restrict__ out,
-                                                     const f16x8* __restrict__ frag, // [2][S][64]
-                                                     const float* __restrict__ taps,
-                                                     int L,
-                                                     int sh,
-                                                     int64_t n_out,
-                                                     int in_aligned)
-{
-    using G = geom8<Q>;
-    constexpr int S = G::S;
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    float4* stash = reinterpret_cast<float4*>(lds + 2 * G::BUF); // [2][HP]
-    unsigned* slot_max = reinterpret_cast<unsigned*>(lds + G::SLOTS);
-    unsigned* slot_exact = slot_max + 8;
-
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = tid >> 6;
-    const int64_t n_in = n_out;
-
-    if (blockIdx.x == 0) {
-        for (int j = tid; j < L - 1; j += G::NT) hist_out[j] = virt(in, hist_in, n_in - (L - 1) + j, n_in, L);
-    }
-
-    f16x8 B0[S], B1[S];
-#pragma unroll
-    for (int st = 0; st < S; ++st) {
-        B0[st] = frag[(0 * S + st) * 64 + lane];
-        B1[st] = frag[(1 * S + st) * 64 + lane];
-    }
-
-    const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
-    const int64_t per = (nchunks + gridDim.x - 1) / gridDim.x;
-    const int64_t c_begin = (int64_t)blockIdx.x * per;
-    const int64_t c_end = c_begin + per < nchunks ? c_begin + per : nchunks;
-    if (c_begin >= c_end) return;
-    const int64_t c_last = c_end - 1;
-
-    const int rho = lane & 31;
-    const int b = rho & 15;
-    const int c = rho >> 4;
-    const int h = lane >> 5;
-    const int a_base = c * 2 * G::PLANE + ((Q - 1) + 16 * wave + b) * 80 + 16 * h;
-    const int phase = lane & 31;
-    const bool al = in_aligned != 0;
-    const bool tail_owner = tid >= G::NT - G::HP; // holds the chunk's last H samples in v[3]
-    auto clamp = [&](int64_t x) { return x <= c_last ? x : c_last; };
-
-    // ---- prologue: chunk c_begin (its halo from global memory), chunks +1, +2 in flight
-    float4 va[G::VPT], vb[G::VPT], vc[G::VPT];
-    float4 hv = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (G::HP > 0 && tid < G::HP) {
-        const int64_t g = c_begin * G::CHUNK - G::H + 2 * tid;
-        const float2 x0 = virt(in, hist_in, g, n_in, L), x1 = virt(in, hist_in, g + 1, n_in, L);
-        hv = make_float4(x0.x, x0.y, x1.x, x1.y);
-    }
-    load_main<Q>(va, in, hist_in, c_begin, n_in, L, al);
-    {
-        unsigned m = max_mag(hv);
-#pragma unroll
-        for (int u = 0; u < G::VPT; ++u) m = max(m, max_mag(va[u]));
-        m = wave_max(m);
-        if (lane == 0) slot_max[wave] = m;
-    }
-    __syncthreads();
-    unsigned m_prev = max(max(slot_max[0], slot_max[1]), max(slot_max[2], slot_max[3]));
-    int s_cur = scale_of(m_prev);
-    bool ex = false;
-    if (G::HP > 0 && tid < G::HP) store_pair8<Q>(hv, lds, 2 * tid, s_cur, ex);
-#pragma unroll
-    for (int u = 0; u < G::VPT; ++u) store_pair8<Q>(va[u], lds, G::H + 2 * (tid + G::NT * u), s_cur, ex);
-    if (G::HP > 0 && tail_owner) stash[tid - (G::NT - G::HP)] = va[G::VPT - 1];
-    load_main<Q>(va, in, hist_in, clamp(c_begin + 1), n_in, L, al);
-    load_main<Q>(vb, in, hist_in, clamp(c_begin + 2), n_in, L, al);
-    {
-        unsigned m = 0;
-#pragma unroll
-        for (int u = 0; u < G::VPT; ++u) m = max(m, max_mag(va[u]));
-        m = wave_max(m);
-        const bool any_ex = __any(ex);
-        __syncthreads(); // everyone has read slot_max[0..3] above
-        if (lane == 0) {
-            slot_max[4 + wave] = m;   // chunk 1 -> parity 1
-            slot_exact[wave] = any_ex; // chunk 0 -> parity 0
-        }
-    }
-    __syncthreads();
-
-    // step i (chunk ch = c_begin + i): nxt = chunk ch+1 (split into the other buffer now),
-    // nn = chunk ch+2 (its maximum is published for the next step), ld receives ch+3.
-    auto step = [&](float4 (&nxt)[G::VPT], float4 (&nn)[G::VPT], float4 (&ld)[G::VPT], int64_t ch) {
-        const int i = (int)(ch - c_begin);
-        const int pi = i & 1, pn = pi ^ 1;
-        unsigned char* cur = lds + pi * G::BUF;
-        unsigned char* nbuf = lds + pn * G::BUF;
-        const bool exact_cur = (slot_exact[4 * pi] | slot_exact[4 * pi + 1] | slot_exact[4 * pi + 2] |
-                                slot_exact[4 * pi + 3]) != 0u;
-        const unsigned m_nxt = max(max(slot_max[4 * pn], slot_max[4 * pn + 1]), max(slot_max[4 * pn + 2], slot_max[4 * pn + 3]));
-        const int s_nxt = scale_of(max(m_prev, m_nxt));
-        load_main<Q>(ld, in, hist_in, clamp(ch + 3), n_in, L, al);
-        bool ex2 = false;
-        if (G::HP > 0 && tid < G::HP) store_pair8<Q>(stash[pi * G::HP + tid], nbuf, 2 * tid, s_nxt, ex2);
-#pragma unroll
-        for (int u = 0; u < G::VPT; ++u) store_pair8<Q>(nxt[u], nbuf, G::H + 2 * (tid + G::NT * u), s_nxt, ex2);
-        if (G::HP > 0 && tail_owner) stash[pn * G::HP + tid - (G::NT - G::HP)] = nxt[G::VPT - 1];
-        if (exact_cur)
-            direct_chunk(in, hist_in, taps, L, ch, n_out, out);
-        else
-            compute_tile8<Q>(cur, B0, B1, a_base, ch * G::CHUNK + (int64_t)wave * TILE, h, phase, n_out, -(s_cur + sh), out);
-        unsigned m = 0;
-#pragma unroll
-        for (int u = 0; u < G::VPT; ++u) m = max(m, max_mag(nn[u]));
-        m = wave_max(m);
-        const bool any_ex = __any(ex2);
-        if (lane == 0) {
-            slot_max[4 * pi + wave] = m;       // chunk ch+2 has this step's parity
-            slot_exact[4 * pn + wave] = any_ex; // chunk ch+1
-        }
-        m_prev = m_nxt;
-        s_cur = s_nxt;
-        __syncthreads();
-    };
-    int64_t ch = c_begin;
-    for (; ch + 2 <= c_last; ch += 3) {
-        step(va, vb, vc, ch);
-        step(vb, vc, va, ch + 1);
-        step(vc, va, vb, ch + 2);
-    }
-    if (ch <= c_last) step(va, vb, vc, ch++);
-    if (ch <= c_last) step(vb, vc, va, ch);
-}
-
-// ---- k_fir_mfma9: the fp16x2 form of k_fir_mfma8 with an exactly counted memory pipeline ----
-// Same GEMM, LDS planes, per-chunk scale and exact-path rule as k_fir_mfma8. What changes is
-// how the step's memory traffic is ordered, which k_fir_mfma8 lost twice over (its .s waits
-// vmcnt(0) once per step, i.e. for the prefetch of chunk ch+3 issued at the top of that step):
+// ---- k_fir_mfma9: the fp16x2 kernel with an exactly counted memory pipeline ----------------
+// Its first form (k_fir_mfma8, removed; bit-identical outputs) tested each
+// sample for the exact path in the split, used __syncthreads() and read the exact path's inputs
+// from global memory -- its .s waited vmcnt(0) once per step, i.e. for the prefetch of chunk
+// ch+3 issued at the top of that step. Here:
 //  * barriers order LDS only (nsh::lds_barrier); __syncthreads() is a fence on global memory too;
 //  * every step issues exactly 4 buffer loads (chunk ch+3) and 8 buffer stores per lane on a
 //    per-chunk resource: out-of-range lanes read 0 and drop their store, so the stream's
@@ -1285,8 +1069,9 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma8(const float2* __restrict__
 //    as raw fp32 (instead of fp16 planes) one step ahead, and the direct form reads it there,
 //    producing the same 8 outputs per lane the MFMA tile does, stored by the same 8 stores;
 //  * the exact-path decision is per chunk, from the chunk maximum (non-finite) and minimum
-//    nonzero magnitude (fp16-subnormal after scaling) reduced alongside the scale: the same
-//    rule k_fir_mfma8 applies per sample, with the halo test widened to its whole source chunk.
+//    nonzero magnitude (fp16-subnormal after scaling) reduced alongside the scale: a nonzero
+//    sample more than 2^28 below the chunk maximum, or a non-finite one, sends the chunk to the
+//    fp32 direct form; the halo test covers its whole source chunk (conservative).
 
 __device__ __forceinline__ unsigned wave_min(unsigned v)
 {
@@ -1300,7 +1085,7 @@ __device__ __forceinline__ unsigned min_nz1(const float4& v)
 {
     return min(min(mag(v.x) - 1u, mag(v.y) - 1u), min(mag(v.z) - 1u, mag(v.w) - 1u));
 }
-// needs_exact() over a whole chunk: non-finite iff its largest magnitude is; a nonzero sample
+// The exact-path rule over a whole chunk: non-finite iff its largest magnitude is; a nonzero sample
 // scales below fp16's normal range iff its smallest nonzero one does (ldexp is exact, monotonic)
 __device__ __forceinline__ bool chunk_needs_exact(unsigned maxbits, unsigned mnz1, int s)
 {
@@ -1334,7 +1119,8 @@ __device__ __forceinline__ void store_pair9(const float4& v, unsigned char* buf,
         __builtin_bit_cast(unsigned, f16x2{ (_Float16)(ai - (float)ai0), (_Float16)(bi - (float)bi0) });
 }
 
-// MFMA tile (as compute_tile8) -> the lane's 8 outputs, unscaled
+// MFMA tile -> the lane's 8 outputs, unscaled (lane holds phase rho of blocks (reg & 3) +
+// 8 (reg >> 2) + 4 h: rows 0-7 re, 8-15 im)
 template <int Q>
 __device__ __forceinline__ void mfma_tile9(const unsigned char* lds, const f16x8 (&B0)[2 * Q], const f16x8 (&B1)[2 * Q],
                                            int a_base, int unscale, nf2 (&o)[8])
@@ -1358,7 +1144,7 @@ __device__ __forceinline__ void mfma_tile9(const unsigned char* lds, const f16x8
 }
 
 // The exact path on a raw fp32 chunk in LDS (local sample j at float2 index j, halo first):
-// the lane's 8 outputs by the fp32 direct form, in direct_chunk's order.
+// the lane's 8 outputs by the fp32 direct form (taps in order, fmaf).
 template <int Q>
 __device__ __forceinline__ void direct_tile9(const unsigned char* lds, const float* __restrict__ taps, int L, int wave, int h,
                                              int phase, nf2 (&o)[8])
@@ -1543,284 +1329,7 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma9(const float2* __restrict__
     if (ch <= c_last) step(vb, vc, va, ch);
 }
 
-// ---- k_fir_mfma10: the fp16x2 split on 16-sample blocks (v_mfma_f32_16x16x32_f16) ----------
-// k_fir_mfma9's pipeline (per-chunk scale, exact chunks staged raw in LDS, buffer ops, LDS-only
-// barriers) on k_fir_mfma5's Toeplitz tiling: output n = 16 beta + i,
-// y = sum_q sum_r h[i - r + 16 q] x[16 (beta - q) + r], K = 16 QH (144 for 127 taps instead of
-// 160), a 16x16x16 MFMA for an odd last block. Rows of A are (component, block) pairs; each
-// 16-sample row is 32 B per plane (hi, lo), re and im planes 128 B apart mod 256 (k_fir_mfma5's
-// conflict-free ds_read_b128 layout with two planes instead of three).
 typedef __attribute__((ext_vector_type(4))) _Float16 f16x4;
-
-template <int QH>
-struct geom10 {
-    static constexpr int NT = 256;
-    static constexpr int CHUNK = 2048;
-    static constexpr int KS = QH / 2;
-    static constexpr int TAIL = QH % 2;
-    static constexpr int H = 16 * (QH - 1);
-    static constexpr int HR = QH - 1;
-    static constexpr int HP = H / 2;
-    static constexpr int NB = (CHUNK + H) / 16;
-    static constexpr int PLANE = NB * 32;
-    static constexpr int IM_OFF = (2 * PLANE + 255) / 256 * 256 + 128;
-    static constexpr int BUF = (IM_OFF + 2 * PLANE + 255) / 256 * 256;
-    static constexpr int STASH = HP * 16;
-    static constexpr int SLOTS = 2 * BUF + 2 * STASH;
-    static constexpr int LDS = SLOTS + 64; // u32 max[2][4], mnz[2][4]
-    static constexpr int TILES = 4;
-    static_assert((HP + 4 * NT) * 16 <= BUF, "a raw fp32 chunk + halo fits one plane buffer");
-    static_assert(HP <= NT, "halo pairs: one per thread");
-};
-
-template <int QH>
-__device__ __forceinline__ void store_pair10(const float4& v, unsigned char* buf, int s, int sc)
-{
-    using G = geom10<QH>;
-    const int off = (s >> 4) * 32 + (s & 15) * 2;
-    const float ar = __builtin_ldexpf(v.x, sc), br = __builtin_ldexpf(v.z, sc);
-    const float ai = __builtin_ldexpf(v.y, sc), bi = __builtin_ldexpf(v.w, sc);
-    const _Float16 ar0 = (_Float16)ar, br0 = (_Float16)br, ai0 = (_Float16)ai, bi0 = (_Float16)bi;
-    *reinterpret_cast<unsigned*>(buf + off) = __builtin_bit_cast(unsigned, f16x2{ ar0, br0 });
-    *reinterpret_cast<unsigned*>(buf + G::PLANE + off) =
-        __builtin_bit_cast(unsigned, f16x2{ (_Float16)(ar - (float)ar0), (_Float16)(br - (float)br0) });
-    *reinterpret_cast<unsigned*>(buf + G::IM_OFF + off) = __builtin_bit_cast(unsigned, f16x2{ ai0, bi0 });
-    *reinterpret_cast<unsigned*>(buf + G::IM_OFF + G::PLANE + off) =
-        __builtin_bit_cast(unsigned, f16x2{ (_Float16)(ai - (float)ai0), (_Float16)(bi - (float)bi0) });
-}
-
-// The wave's 4 row-tiles (8 blocks each) x (KS k-steps of 32 + an optional tail of 16), three
-// products; lane output (t, half) = block t*8 + 2g + half, sample phase.
-template <int QH>
-__device__ __forceinline__ void mfma_tile10(const unsigned char* lds, const f16x8 (&B0)[geom10<QH>::KS + 1],
-                                            const f16x8 (&B1)[geom10<QH>::KS + 1], const f16x4 (&T0), const f16x4 (&T1),
-                                            int row_base, int g, int unscale, nf2 (&o)[8])
-{
-    using G = geom10<QH>;
-    typedef float f32x4 __attribute__((ext_vector_type(4)));
-    f32x4 hi[G::TILES], lo[G::TILES], hi_t[G::TILES], lo_t[G::TILES];
-#pragma unroll
-    for (int t = 0; t < G::TILES; ++t) {
-        hi[t] = f32x4{ 0.f, 0.f, 0.f, 0.f };
-        lo[t] = f32x4{ 0.f, 0.f, 0.f, 0.f };
-        hi_t[t] = f32x4{ 0.f, 0.f, 0.f, 0.f };
-        lo_t[t] = f32x4{ 0.f, 0.f, 0.f, 0.f };
-    }
-#pragma unroll
-    for (int st = 0; st < G::KS; ++st) {
-        const int q = 2 * st + (g >> 1);
-#pragma unroll
-        for (int t = 0; t < G::TILES; ++t) {
-            const int off = row_base + t * 8 * 32 - q * 32 + (g & 1) * 16;
-            const f16x8 A0 = *reinterpret_cast<const f16x8*>(lds + off);
-            const f16x8 A1 = *reinterpret_cast<const f16x8*>(lds + off + G::PLANE);
-            hi[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0, B0[st], hi[t], 0, 0, 0);
-            lo[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0, B1[st], lo[t], 0, 0, 0);
-            lo[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1, B0[st], lo[t], 0, 0, 0);
-        }
-    }
-    // K tail in its own accumulators (16x16x32 -> dependent 16x16x16 hazard, see v5_compute)
-    if constexpr (G::TAIL) {
-#pragma unroll
-        for (int t = 0; t < G::TILES; ++t) {
-            const int off = row_base + t * 8 * 32 - (QH - 1) * 32 + g * 8;
-            const f16x4 A0 = *reinterpret_cast<const f16x4*>(lds + off);
-            const f16x4 A1 = *reinterpret_cast<const f16x4*>(lds + off + G::PLANE);
-            hi_t[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(A0, T0, hi_t[t], 0, 0, 0);
-            lo_t[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(A0, T1, lo_t[t], 0, 0, 0);
-            lo_t[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(A1, T0, lo_t[t], 0, 0, 0);
-        }
-    }
-#pragma unroll
-    for (int t = 0; t < G::TILES; ++t)
-#pragma unroll
-        for (int half = 0; half < 2; ++half)
-            o[2 * t + half] = nf2{ __builtin_ldexpf((hi[t][2 * half] + hi_t[t][2 * half]) + (lo[t][2 * half] + lo_t[t][2 * half]), unscale),
-                                   __builtin_ldexpf((hi[t][2 * half + 1] + hi_t[t][2 * half + 1]) +
-                                                        (lo[t][2 * half + 1] + lo_t[t][2 * half + 1]), unscale) };
-}
-
-template <int QH>
-__device__ __forceinline__ void direct_tile10(const unsigned char* lds, const float* __restrict__ taps, int L, int wave, int g,
-                                              int phase, nf2 (&o)[8])
-{
-    using G = geom10<QH>;
-    const float2* raw = reinterpret_cast<const float2*>(lds);
-    for (int oi = 0; oi < 8; ++oi) {
-        const int blk = (oi >> 1) * 8 + 2 * g + (oi & 1);
-        const int j = G::H + wave * TILE + blk * 16 + phase;
-        float re = 0.f, im = 0.f;
-        for (int k = 0; k < L; ++k) {
-            const float2 x = raw[j - k];
-            re = fmaf(taps[k], x.x, re);
-            im = fmaf(taps[k], x.y, im);
-        }
-        o[oi] = nf2{ re, im };
-    }
-}
-
-template <int QH>
-__global__ __launch_bounds__(256, 2) void k_fir_mfma10(const float2* __restrict__ in,
-                                                      const float2* __restrict__ hist_in,
-                                                      float2* __restrict__ hist_out,
-                                                      float2* __restrict__ out,
-                                                      const _Float16* __restrict__ frag, // [2][KS][64] x8, [2][64] x4
-                                                      const float* __restrict__ taps,
-                                                      int L,
-                                                      int sh,
-                                                      int64_t n_out)
-{
-    using G = geom10<QH>;
-    constexpr int KS = G::KS;
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    float4* stash = reinterpret_cast<float4*>(lds + 2 * G::BUF);
-    unsigned* slot_max = reinterpret_cast<unsigned*>(lds + G::SLOTS);
-    unsigned* slot_mnz = slot_max + 8;
-
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = tid >> 6;
-    const int64_t n_in = n_out;
-
-    if (blockIdx.x == 0) {
-        for (int j = tid; j < L - 1; j += G::NT) hist_out[j] = virt(in, hist_in, n_in - (L - 1) + j, n_in, L);
-    }
-
-    f16x8 B0[KS + 1], B1[KS + 1];
-#pragma unroll
-    for (int st = 0; st < KS; ++st) {
-        B0[st] = reinterpret_cast<const f16x8*>(frag)[(0 * KS + st) * 64 + lane];
-        B1[st] = reinterpret_cast<const f16x8*>(frag)[(1 * KS + st) * 64 + lane];
-    }
-    f16x4 T0 = {}, T1 = {};
-    if constexpr (G::TAIL) {
-        const f16x4* tf = reinterpret_cast<const f16x4*>(frag + 2 * KS * 64 * 8);
-        T0 = tf[lane];
-        T1 = tf[64 + lane];
-    }
-
-    const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
-    const int64_t per = (nchunks + gridDim.x - 1) / gridDim.x;
-    const int64_t c_begin = (int64_t)blockIdx.x * per;
-    const int64_t c_end = c_begin + per < nchunks ? c_begin + per : nchunks;
-    if (c_begin >= c_end) return;
-    const int64_t c_last = c_end - 1;
-
-    const int rho = lane & 15;
-    const int c = rho & 1, b = rho >> 1;
-    const int g = lane >> 4;
-    const int phase = lane & 15;
-    const int row_base = c * G::IM_OFF + (G::HR + wave * 32 + b) * 32;
-    const bool tail_owner = tid >= G::NT - G::HP;
-    auto clamp = [&](int64_t x) { return x <= c_last ? x : c_last; };
-    auto put_chunk = [&](unsigned char* buf, const float4& halo, const float4 (&v)[4], bool raw, int sc) {
-        if (raw) {
-            float4* r = reinterpret_cast<float4*>(buf);
-            if (G::HP > 0 && tid < G::HP) r[tid] = halo;
-#pragma unroll
-            for (int u = 0; u < 4; ++u) r[G::HP + tid + G::NT * u] = v[u];
-        } else {
-            if (G::HP > 0 && tid < G::HP) store_pair10<QH>(halo, buf, 2 * tid, sc);
-#pragma unroll
-            for (int u = 0; u < 4; ++u) store_pair10<QH>(v[u], buf, G::H + 2 * (tid + G::NT * u), sc);
-        }
-    };
-    auto reduce = [&](const float4 (&v)[4], unsigned& m, unsigned& z) {
-        m = 0;
-        z = ~0u;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            m = max(m, max_mag(v[u]));
-            z = min(z, min_nz1(v[u]));
-        }
-        m = wave_max(m);
-        z = wave_min(z);
-    };
-    auto store_tile = [&](int64_t ch, const nf2 (&o)[8]) {
-        const __amdgpu_buffer_rsrc_t r = chunk_rsrc<2048>(out, ch, n_out);
-        const int base = wave * TILE + phase;
-#pragma unroll
-        for (int oi = 0; oi < 8; ++oi) buf_store_f2(r, (base + ((oi >> 1) * 8 + 2 * g + (oi & 1)) * 16) * 8, o[oi]);
-    };
-
-    float4 va[4], vb[4], vc[4];
-    float4 hv = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (G::HP > 0 && tid < G::HP) {
-        const int64_t gg = c_begin * G::CHUNK - G::H + 2 * tid;
-        const float2 x0 = virt(in, hist_in, gg, n_in, L), x1 = virt(in, hist_in, gg + 1, n_in, L);
-        hv = make_float4(x0.x, x0.y, x1.x, x1.y);
-    }
-    load_chunk9(va, in, c_begin, n_in);
-    {
-        unsigned m, z;
-        reduce(va, m, z);
-        m = max(m, wave_max(max_mag(hv)));
-        z = min(z, wave_min(min_nz1(hv)));
-        if (lane == 0) {
-            slot_max[wave] = m;
-            slot_mnz[wave] = z;
-        }
-    }
-    nsh::lds_barrier();
-    unsigned m_prev = max(max(slot_max[0], slot_max[1]), max(slot_max[2], slot_max[3]));
-    unsigned z_prev = min(min(slot_mnz[0], slot_mnz[1]), min(slot_mnz[2], slot_mnz[3]));
-    int s_cur = scale_of(m_prev);
-    bool ex_cur = chunk_needs_exact(m_prev, z_prev, s_cur);
-    put_chunk(lds, hv, va, ex_cur, s_cur);
-    if (G::HP > 0 && tail_owner) stash[tid - (G::NT - G::HP)] = va[3];
-    load_chunk9(va, in, clamp(c_begin + 1), n_in);
-    load_chunk9(vb, in, clamp(c_begin + 2), n_in);
-    {
-        unsigned m, z;
-        reduce(va, m, z);
-        nsh::lds_barrier();
-        if (lane == 0) {
-            slot_max[4 + wave] = m;
-            slot_mnz[4 + wave] = z;
-        }
-    }
-    nsh::lds_barrier();
-
-    auto step = [&](float4 (&nxt)[4], float4 (&nn)[4], float4 (&ld)[4], int64_t ch) {
-        const int i = (int)(ch - c_begin);
-        const int pi = i & 1, pn = pi ^ 1;
-        const unsigned char* cur = lds + pi * G::BUF;
-        unsigned char* nbuf = lds + pn * G::BUF;
-        const unsigned m_nxt = max(max(slot_max[4 * pn], slot_max[4 * pn + 1]), max(slot_max[4 * pn + 2], slot_max[4 * pn + 3]));
-        const unsigned z_nxt = min(min(slot_mnz[4 * pn], slot_mnz[4 * pn + 1]), min(slot_mnz[4 * pn + 2], slot_mnz[4 * pn + 3]));
-        const unsigned m2 = max(m_prev, m_nxt);
-        const int s_nxt = scale_of(m2);
-        const bool ex_nxt = chunk_needs_exact(m2, min(z_prev, z_nxt), s_nxt);
-        load_chunk9(ld, in, clamp(ch + 3), n_in);
-        put_chunk(nbuf, G::HP > 0 && tid < G::HP ? stash[pi * G::HP + tid] : make_float4(0.f, 0.f, 0.f, 0.f), nxt, ex_nxt, s_nxt);
-        if (G::HP > 0 && tail_owner) stash[pn * G::HP + tid - (G::NT - G::HP)] = nxt[3];
-        nf2 o[8];
-        if (ex_cur)
-            direct_tile10<QH>(cur, taps, L, wave, g, phase, o);
-        else
-            mfma_tile10<QH>(cur, B0, B1, T0, T1, row_base, g, -(s_cur + sh), o);
-        store_tile(ch, o);
-        unsigned m, z;
-        reduce(nn, m, z);
-        if (lane == 0) {
-            slot_max[4 * pi + wave] = m;
-            slot_mnz[4 * pi + wave] = z;
-        }
-        m_prev = m_nxt;
-        z_prev = z_nxt;
-        ex_cur = ex_nxt;
-        s_cur = s_nxt;
-        nsh::lds_barrier();
-    };
-    int64_t ch = c_begin;
-    for (; ch + 2 <= c_last; ch += 3) {
-        step(va, vb, vc, ch);
-        step(vb, vc, va, ch + 1);
-        step(vc, va, vb, ch + 2);
-    }
-    if (ch <= c_last) step(va, vb, vc, ch++);
-    if (ch <= c_last) step(vb, vc, va, ch);
-}
 
 // ---- k_fir_mfma11: decimating polyphase FIR (D = 2, 4) on the fp16x2 split -----------------
 // k_fir_mfma7's polyphase Toeplitz form (phase streams z_0[i] = x[D i], z_r[i] = x[D i + D - r],
@@ -2242,27 +1751,6 @@ int launch_v2(const nsh_fir_plan* p, const float2* in, const float2* hin, float2
     return 0;
 }
 
-template <int Q>
-int launch_v8(const nsh_fir_plan* p, const float2* in, const float2* hin, float2* hout, float2* out, int64_t n_out,
-              hipStream_t s)
-{
-    using G = geom8<Q>;
-    static bool attr_set = false;
-    if (!attr_set) {
-        NSH_CK(hipFuncSetAttribute((const void*)k_fir_mfma8<Q>, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
-        attr_set = true;
-    }
-    const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
-    int n_cu = 256;
-    (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, p->dev);
-    const int64_t max_grid = (int64_t)n_cu * 2;
-    const unsigned grid = (unsigned)(nchunks < max_grid ? nchunks : max_grid);
-    const int aligned = ((uintptr_t)in % 16 == 0) ? 1 : 0;
-    hipLaunchKernelGGL((k_fir_mfma8<Q>), dim3(grid), dim3(G::NT), G::LDS, s, in, hin, hout, out,
-                       (const f16x8*)p->frag8_dev, (const float*)p->taps_dev, p->L, p->sh8, n_out, aligned);
-    NSH_CK_LAUNCH("nsh_fir_ccf(mfma fp16x2)");
-    return 0;
-}
 
 template <int Q>
 int launch_v9(const nsh_fir_plan* p, const float2* in, const float2* hin, float2* hout, float2* out, int64_t n_out,
@@ -2293,53 +1781,13 @@ int launch_v9(const nsh_fir_plan* p, const float2* in, const float2* hin, float2
     return 0;
 }
 
-template <int QH>
-int launch_v10(const nsh_fir_plan* p, const float2* in, const float2* hin, float2* hout, float2* out, int64_t n_out,
-               hipStream_t s)
-{
-    using G = geom10<QH>;
-    static bool attr_set = false;
-    if (!attr_set) {
-        NSH_CK(hipFuncSetAttribute((const void*)k_fir_mfma10<QH>, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
-        attr_set = true;
-    }
-    const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
-    int n_cu = 256;
-    (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, p->dev);
-    const int64_t max_grid = (int64_t)n_cu * 2;
-    const unsigned grid = (unsigned)(nchunks < max_grid ? nchunks : max_grid);
-    hipLaunchKernelGGL((k_fir_mfma10<QH>), dim3(grid), dim3(G::NT), G::LDS, s, in, hin, hout, out,
-                       (const _Float16*)p->frag10_dev, (const float*)p->taps_dev, p->L, p->sh8, n_out);
-    NSH_CK_LAUNCH("nsh_fir_ccf(mfma fp16x2 16-sample)");
-    return 0;
-}
-int launch_v10_qh(const nsh_fir_plan* p, const float2* in, const float2* hin, float2* hout, float2* out, int64_t n_out,
-                  hipStream_t s)
-{
-    switch (p->QH) {
-    case 1: return launch_v10<1>(p, in, hin, hout, out, n_out, s);
-    case 2: return launch_v10<2>(p, in, hin, hout, out, n_out, s);
-    case 3: return launch_v10<3>(p, in, hin, hout, out, n_out, s);
-    case 4: return launch_v10<4>(p, in, hin, hout, out, n_out, s);
-    case 5: return launch_v10<5>(p, in, hin, hout, out, n_out, s);
-    case 6: return launch_v10<6>(p, in, hin, hout, out, n_out, s);
-    case 7: return launch_v10<7>(p, in, hin, hout, out, n_out, s);
-    case 8: return launch_v10<8>(p, in, hin, hout, out, n_out, s);
-    case 9: return launch_v10<9>(p, in, hin, hout, out, n_out, s);
-    case 10: return launch_v10<10>(p, in, hin, hout, out, n_out, s);
-    default: return nsh::fail_msg("nsh_fir_ccf(mfma10): unsupported tap count");
-    }
-}
 
 // Tuning variants (selected by NSH_FIR_MFMA_VARIANT for A/B runs; default = measured best).
 template <int Q>
 int launch_q(const nsh_fir_plan* p, const float2* in, const float2* hin, float2* hout, float2* out, int64_t n_out, hipStream_t s)
 {
     if (p->frag8_dev && !p->force_x3 && p->variant != 6 && p->variant != 7)
-    {
-        if (p->variant == 10 && p->frag10_dev) return launch_v10_qh(p, in, hin, hout, out, n_out, s);
-        return p->variant == 8 ? launch_v8<Q>(p, in, hin, hout, out, n_out, s) : launch_v9<Q>(p, in, hin, hout, out, n_out, s);
-    }
+        return launch_v9<Q>(p, in, hin, hout, out, n_out, s);
     switch (p->variant) {
     case 6: return launch_v2<Q, 1>(p, in, hin, hout, out, n_out, s, 2);
     case 7: return launch_v2<Q, 2>(p, in, hin, hout, out, n_out, s, 2);
@@ -2487,7 +1935,7 @@ int nsh_fir_mfma_prepare(nsh_fir_plan* p)
     NSH_CK(hipMalloc(&p->frag_dev, frag.size() * sizeof(unsigned short)));
     NSH_CK(hipMemcpy(p->frag_dev, frag.data(), frag.size() * sizeof(unsigned short), hipMemcpyHostToDevice));
 
-    // v8: taps scaled by 2^sh8 (max |h| * 2^sh8 in [2^14, 2^15)), split into two fp16 terms
+    // fp16x2 (k_fir_mfma9): taps scaled by 2^sh8 (max |h| * 2^sh8 in [2^14, 2^15)), split into two fp16 terms
     // (RNE), same lane order as v2. A tap far below the largest (e.g. firwin's ~1e-18 taps
     // at the sinc zeros) lands in fp16's subnormal range or flushes: it is then exact to
     // 2^-39 of the largest tap, which moves an output by at most 2^-39 max|h| sum|x|, far
@@ -2517,37 +1965,6 @@ int nsh_fir_mfma_prepare(nsh_fir_plan* p)
             p->sh8 = sh;
             NSH_CK(hipMalloc(&p->frag8_dev, f8.size() * sizeof(_Float16)));
             NSH_CK(hipMemcpy(p->frag8_dev, f8.data(), f8.size() * sizeof(_Float16), hipMemcpyHostToDevice));
-        }
-        // v10: the same scaled fp16x2 taps in k_fir_mfma5's 16-sample fragment order
-        // (k-steps of 32: lane l holds B[k = 8(l >> 4) + j][col = l & 15], tap index
-        // col - (k & 15) + 16 (2 st + (k >> 4)); odd QH: a 16x16x16 tail, B[r = 4(l >> 4) + j])
-        const int QH = (p->L + 15 + 15) / 16;
-        if (QH <= 10) {
-            const int KS = QH / 2;
-            const bool tail = QH % 2;
-            std::vector<_Float16> f((size_t)2 * KS * 64 * 8 + (size_t)2 * 64 * 4, (_Float16)0.f);
-            auto put2 = [&](int t, size_t i0, size_t i1) {
-                const float hs = (t >= 0 && t < p->L) ? std::ldexp(p->taps_host[t], sh) : 0.f;
-                const _Float16 h0 = (_Float16)hs;
-                f[i0] = h0;
-                f[i1] = (_Float16)(hs - (float)h0);
-            };
-            for (int st = 0; st < KS; ++st)
-                for (int lane = 0; lane < 64; ++lane)
-                    for (int j = 0; j < 8; ++j) {
-                        const int kk = 8 * (lane >> 4) + j;
-                        put2((lane & 15) - (kk & 15) + 16 * (2 * st + (kk >> 4)), ((size_t)(0 * KS + st) * 64 + lane) * 8 + j,
-                             ((size_t)(1 * KS + st) * 64 + lane) * 8 + j);
-                    }
-            if (tail) {
-                const size_t t0 = (size_t)2 * KS * 64 * 8;
-                for (int lane = 0; lane < 64; ++lane)
-                    for (int j = 0; j < 4; ++j)
-                        put2((lane & 15) - (4 * (lane >> 4) + j) + 16 * (QH - 1), t0 + (size_t)lane * 4 + j,
-                             t0 + (size_t)(64 + lane) * 4 + j);
-            }
-            NSH_CK(hipMalloc(&p->frag10_dev, f.size() * sizeof(_Float16)));
-            NSH_CK(hipMemcpy(p->frag10_dev, f.data(), f.size() * sizeof(_Float16), hipMemcpyHostToDevice));
         }
     }
 
@@ -2601,11 +2018,7 @@ std::string nsh_fir_mfma_kernel_name(const nsh_fir_plan* p)
     };
     if (p->algo == NSH_FIR_MFMA16) return t("k_fir_mfma5", p->QH, p->variant == 20 ? 2 : 1);
     if (p->D > 1) return t(p->fragd8_dev && p->variant != 7 ? "k_fir_mfma11" : "k_fir_mfma7", p->D, p->QHD);
-    if (p->frag8_dev && !p->force_x3 && p->variant != 6 && p->variant != 7)
-    {
-        if (p->variant == 10 && p->frag10_dev) return t("k_fir_mfma10", p->QH);
-        return t(p->variant == 8 ? "k_fir_mfma8" : "k_fir_mfma9", p->Q);
-    }
+    if (p->frag8_dev && !p->force_x3 && p->variant != 6 && p->variant != 7) return t("k_fir_mfma9", p->Q);
     if (p->variant >= 20) return t("k_fir_mfma5", p->QH, p->variant == 20 ? 2 : 1);
     return t("k_fir_mfma2", p->Q, p->variant == 6 ? 1 : 2);
 }

@@ -29,7 +29,6 @@ struct nsh_fir_plan {
     // scaled fp16x2 form (decim 1, default): taps * 2^sh8 split into two fp16 terms,
     // [part(2)][kstep(S)][lane(64)][8]; null when the taps' range does not allow it.
     void* frag8_dev = nullptr;
-    void* frag10_dev = nullptr; // fp16x2, 16-sample blocks (k_fir_mfma10): [2][QH/2][64] x8 + [2][64] x4
     int sh8 = 0;
     bool force_x3 = false; // NSH_FIR_MFMA_BF16X3: always the bf16x3 six-product kernel
     int variant = 0;      // MFMA kernel tuning variant (0 = default)

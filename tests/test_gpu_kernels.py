@@ -131,12 +131,10 @@ def test_mul_const_vcc_bitexact(torch_cuda, vlen, nitems):
 
 # "mfma" is the default matrix-core kernel (decim 1: per-chunk scaled fp16x2, k_fir_mfma9),
 # "mfma_x3" forces the bf16x3 six-product kernel (k_fir_mfma2), "mfma16" the 16-sample form.
-# "mfma_v8" / "mfma_v10" are the other fp16x2 kernels (NSH_FIR_MFMA_VARIANT 8: k_fir_mfma8,
-# 10: k_fir_mfma10, the 16-sample form).
 ALGOS = [("direct", nsh.FIR_DIRECT), ("mfma", nsh.FIR_MFMA), ("mfma_x3", nsh.FIR_MFMA_BF16X3),
-         ("mfma16", nsh.FIR_MFMA16), ("mfma_v8", nsh.FIR_MFMA), ("mfma_v10", nsh.FIR_MFMA)]
-MAX_TAPS = {"direct": 4096, "mfma": 161, "mfma_x3": 161, "mfma16": 145, "mfma_v8": 161, "mfma_v10": 145}
-VARIANT = {"mfma_v8": "8", "mfma_v10": "10"}
+         ("mfma16", nsh.FIR_MFMA16)]
+MAX_TAPS = {"direct": 4096, "mfma": 161, "mfma_x3": 161, "mfma16": 145}
+VARIANT = {}  # name -> NSH_FIR_MFMA_VARIANT for tuning variants under test (none at present)
 
 
 def make_plan(name, taps, decim, algo):
@@ -153,9 +151,6 @@ def make_plan(name, taps, decim, algo):
                 del os.environ["NSH_FIR_MFMA_VARIANT"]
             else:
                 os.environ["NSH_FIR_MFMA_VARIANT"] = old
-    if v:
-        want = "k_fir_mfma8" if v == "8" else "k_fir_mfma10"
-        assert plan.kernel.startswith(want), plan.kernel
     return plan
 
 
@@ -381,21 +376,16 @@ def _assert_nonfinite_pattern(y, ref):
     np.testing.assert_array_equal(np.sign(y.imag[inf]), np.sign(ref.imag[inf]))
 
 
-@pytest.fixture(params=["v9", "v8", "v10"])
-def v8_form(request, monkeypatch):
-    """Both fp16x2 kernels: k_fir_mfma9 (default: exact-path decision per chunk from the
-    reductions, exact chunks staged raw in LDS) and k_fir_mfma8 (per-sample tests, exact
-    path from global memory; NSH_FIR_MFMA_VARIANT=8)."""
-    if request.param in ("v8", "v10"):
-        monkeypatch.setenv("NSH_FIR_MFMA_VARIANT", request.param[1:])
-    else:
-        monkeypatch.delenv("NSH_FIR_MFMA_VARIANT", raising=False)
-    return request.param
+@pytest.fixture
+def v8_form(monkeypatch):
+    """The fp16x2 kernel (k_fir_mfma9, default): no tuning variant set."""
+    monkeypatch.delenv("NSH_FIR_MFMA_VARIANT", raising=False)
+    return "v9"
 
 
 def _v8_plan(h, form):
     plan = nsh.FirPlan(h, 1, nsh.FIR_MFMA)
-    assert plan.kernel == {"v9": "k_fir_mfma9<5>", "v8": "k_fir_mfma8<5>", "v10": "k_fir_mfma10<9>"}[form], plan.kernel
+    assert plan.kernel == "k_fir_mfma9<5>", plan.kernel
     return plan
 
 
