@@ -10,6 +10,6 @@ export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 && echo "pytest ok" &&
 timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && echo "smoke ok" &&
 timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err && echo "bench ok" &&
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o bench --output-format csv -- python3 bench.py --steps 50 --warmup 20 --no-cpu > $O/bench_under_rocprof.json 2> $O/rocprof.err && echo "rocprof ok" &&
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o bench --output-format csv -- python3 bench.py > $O/bench_under_rocprof.json 2> $O/rocprof.err && echo "rocprof ok" &&
 tools/pmc_fir.sh $O/pmc && python3 tools/pmc_summary.py $O/pmc $((1<<25)) $O/pmc_fir.json > /dev/null && echo "pmc ok" &&
 timeout -k 10 400 build/tools/bench_configs 28 30 > $O/configs.jsonl 2> $O/configs.err && echo "configs ok"
