@@ -1097,6 +1097,10 @@ __device__ __forceinline__ bool chunk_needs_exact(unsigned maxbits, unsigned mnz
 // chunk ch -> registers: lane t holds samples (2t, 2t+1) + 512 u, u < 4
 __device__ __forceinline__ void load_chunk9(float4 (&v)[4], const float2* __restrict__ in, int64_t ch, int64_t n_in)
 {
+#if NSH_FIR_ABLATE & 1024 // timing only: no global loads
+    for (int u = 0; u < 4; ++u) v[u] = make_float4((float)ch, (float)u, (float)threadIdx.x, 1.f);
+    return;
+#endif
     const __amdgpu_buffer_rsrc_t r = chunk_rsrc<2048>(in, ch, n_in);
 #pragma unroll
     for (int u = 0; u < 4; ++u) v[u] = buf_load_f4(r, (threadIdx.x + 256 * u) * 16);
@@ -1108,6 +1112,13 @@ __device__ __forceinline__ void store_pair9(const float4& v, unsigned char* buf,
 {
     using G = geom8<Q>;
     const int off = (s >> 5) * 80 + (s & 31) * 2;
+#if NSH_FIR_ABLATE & 512 // timing only: the split's LDS writes without its conversion VALU
+    *reinterpret_cast<unsigned*>(buf + 0 * G::PLANE + off) = __float_as_uint(v.x);
+    *reinterpret_cast<unsigned*>(buf + 1 * G::PLANE + off) = __float_as_uint(v.y);
+    *reinterpret_cast<unsigned*>(buf + 2 * G::PLANE + off) = __float_as_uint(v.z);
+    *reinterpret_cast<unsigned*>(buf + 3 * G::PLANE + off) = __float_as_uint(v.w);
+    return;
+#endif
     const float ar = __builtin_ldexpf(v.x, sc), br = __builtin_ldexpf(v.z, sc);
     const float ai = __builtin_ldexpf(v.y, sc), bi = __builtin_ldexpf(v.w, sc);
     const _Float16 ar0 = (_Float16)ar, br0 = (_Float16)br, ai0 = (_Float16)ai, bi0 = (_Float16)bi;
@@ -1133,6 +1144,10 @@ __device__ __forceinline__ void mfma_tile9(const unsigned char* lds, const f16x8
         const int off = a_base - (st >> 1) * 80 + 32 * (st & 1);
         const f16x8 A0 = *reinterpret_cast<const f16x8*>(lds + off);
         const f16x8 A1 = *reinterpret_cast<const f16x8*>(lds + off + G::PLANE);
+#if NSH_FIR_ABLATE & 256 // timing only: A-fragment reads kept, no matrix work
+        acc_hi[st & 15] += (float)A0[0] + (float)A1[1];
+        continue;
+#endif
         acc_hi = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, B0[st], acc_hi, 0, 0, 0);
         acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, B1[st], acc_lo, 0, 0, 0);
         acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, B0[st], acc_lo, 0, 0, 0);
@@ -1241,6 +1256,12 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma9(const float2* __restrict__
     auto store_tile = [&](int64_t ch, const nf2 (&o)[8]) {
         const __amdgpu_buffer_rsrc_t r = chunk_rsrc<2048>(out, ch, n_out);
         const int base = wave * TILE + phase;
+#if NSH_FIR_ABLATE & 2048 // timing only: one store per lane per chunk (keeps the results live)
+        nf2 acc = o[0];
+        for (int reg = 1; reg < 8; ++reg) acc += o[reg];
+        if (acc.x == 1.2345e-30f) buf_store_f2(r, base * 8, acc);
+        return;
+#endif
 #pragma unroll
         for (int reg = 0; reg < 8; ++reg) buf_store_f2(r, (base + 32 * ((reg & 3) + 8 * (reg >> 2) + 4 * h)) * 8, o[reg]);
     };
