@@ -119,6 +119,18 @@ const char* nsh_fir_plan_kernel(void* plan); /* the kernel nsh_fir_ccf launches,
 int nsh_fir_ccf(void* plan, const float* in, const float* hist_in, float* hist_out,
                 float* out, int64_t n_out, void* stream);
 
+/* Two decimate-by-2 FIRs in one pass (the fused form of fir_filter_ccf(h1, 2) ->
+ * fir_filter_ccf(h2, 2), what scheduler_hip's fusion pass turns such a pair into; replaces
+ * two nsh_fir_ccf calls): y1[i] = sum_k h1[k] x[2i - k], y2[m] = sum_k h2[k] y1[2m - k].
+ * plan1/plan2 are decim-2 NSH_FIR_MFMA (or AUTO-resolved MFMA) plans on the same device;
+ * in = 4 n_out samples; hist1 = ntaps1-1 x samples, hist2 = ntaps2-1 y1 samples, each an
+ * in/out pair as for nsh_fir_ccf (no aliasing). Outputs within the fp16x2 MFMA tolerance of
+ * the two-call chain (stage 1's outputs are not rounded through HBM: they are the same fp32
+ * values). nsh_fir_cascade2_supported returns 1 when the pair qualifies. */
+int nsh_fir_cascade2_supported(void* plan1, void* plan2);
+int nsh_fir_cascade2_ccf(void* plan1, void* plan2, const float* in, const float* hist1_in, float* hist1_out,
+                         const float* hist2_in, float* hist2_out, float* out, int64_t n_out, void* stream);
+
 /* ---- FFT (fft_vcc, 1024-point, unnormalised both ways) ------------------------------
  * frames of 1024 complex samples; inverse=1 computes sum_k X[k] e^{+2 pi i kn/1024}
  * (= 1024 * numpy.fft.ifft). nsh_channelizer1024 fuses fft -> multiply by w[1024]

@@ -234,4 +234,24 @@ int nsh_fir_ccf(void* plan, const float* in, const float* hist_in, float* hist_o
     return run_direct(p, (const float2*)in, (const float2*)hist_in, (float2*)hist_out, (float2*)out, n_out, s);
 }
 
+int nsh_fir_cascade2_supported(void* plan1, void* plan2)
+{
+    return nsh_fir_cascade2_ok(static_cast<nsh_fir_plan*>(plan1), static_cast<nsh_fir_plan*>(plan2)) ? 1 : 0;
+}
+
+int nsh_fir_cascade2_ccf(void* plan1, void* plan2, const float* in, const float* hist1_in, float* hist1_out,
+                         const float* hist2_in, float* hist2_out, float* out, int64_t n_out, void* stream)
+{
+    auto* p1 = static_cast<nsh_fir_plan*>(plan1);
+    auto* p2 = static_cast<nsh_fir_plan*>(plan2);
+    if (!nsh_fir_cascade2_ok(p1, p2))
+        return nsh::fail_msg("nsh_fir_cascade2_ccf: plans must be decim-2 fp16x2 MFMA plans (3 <= ceil((ntaps/2+1)/16)+1 <= 6) on one device");
+    if (n_out <= 0) return 0;
+    if (n_out > ((int64_t)1 << 40)) return nsh::fail_msg("nsh_fir_cascade2_ccf: n_out too large");
+    if (hist1_in == hist1_out || hist2_in == hist2_out)
+        return nsh::fail_msg("nsh_fir_cascade2_ccf: hist_out must not alias hist_in");
+    return nsh_fir_cascade2_run(p1, p2, (const float2*)in, (const float2*)hist1_in, (float2*)hist1_out,
+                                (const float2*)hist2_in, (float2*)hist2_out, (float2*)out, n_out, nsh::S(stream));
+}
+
 } // extern "C"

@@ -1050,12 +1050,23 @@ __device__ __forceinline__ unsigned max_mag(const float4& v)
 }
 // scale exponent: max magnitude (bit pattern) * 2^s in [2^14, 2^15) (zero/subnormal: 2^141)
 __device__ __forceinline__ int scale_of(unsigned maxbits) { return 141 - (int)(maxbits >> 23); }
-__device__ __forceinline__ unsigned wave_max(unsigned v)
+// Wave-wide max / min, uniform result: DPP within each 16-lane row (quad_perm xor 1, xor 2,
+// row_ror 4, 8: VALU, no LDS) then the four row results by v_readlane. The __shfl_xor form
+// was six dependent ds_bpermute round trips through the LDS unit per reduction.
+template <bool MAX>
+__device__ __forceinline__ unsigned wave_red(unsigned v)
 {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = max(v, (unsigned)__shfl_xor((int)v, o));
-    return v;
+    constexpr int id = MAX ? 0 : -1;
+    auto op = [](unsigned a, unsigned b) { return MAX ? max(a, b) : min(a, b); };
+    v = op(v, (unsigned)__builtin_amdgcn_update_dpp(id, (int)v, 0xB1, 0xf, 0xf, false));  // quad_perm [1,0,3,2]
+    v = op(v, (unsigned)__builtin_amdgcn_update_dpp(id, (int)v, 0x4E, 0xf, 0xf, false));  // quad_perm [2,3,0,1]
+    v = op(v, (unsigned)__builtin_amdgcn_update_dpp(id, (int)v, 0x124, 0xf, 0xf, false)); // row_ror:4
+    v = op(v, (unsigned)__builtin_amdgcn_update_dpp(id, (int)v, 0x128, 0xf, 0xf, false)); // row_ror:8
+    const unsigned a = (unsigned)__builtin_amdgcn_readlane((int)v, 0), b = (unsigned)__builtin_amdgcn_readlane((int)v, 16);
+    const unsigned c = (unsigned)__builtin_amdgcn_readlane((int)v, 32), d = (unsigned)__builtin_amdgcn_readlane((int)v, 48);
+    return op(op(a, b), op(c, d));
 }
+__device__ __forceinline__ unsigned wave_max(unsigned v) { return wave_red<true>(v); }
 // ---- k_fir_mfma9: the fp16x2 kernel with an exactly counted memory pipeline ----------------
 // Its first form (k_fir_mfma8, removed; bit-identical outputs) tested each
 // sample for the exact path in the split, used __syncthreads() and read the exact path's inputs
@@ -1073,12 +1084,7 @@ __device__ __forceinline__ unsigned wave_max(unsigned v)
 //    sample more than 2^28 below the chunk maximum, or a non-finite one, sends the chunk to the
 //    fp32 direct form; the halo test covers its whole source chunk (conservative).
 
-__device__ __forceinline__ unsigned wave_min(unsigned v)
-{
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = min(v, (unsigned)__shfl_xor((int)v, o));
-    return v;
-}
+__device__ __forceinline__ unsigned wave_min(unsigned v) { return wave_red<false>(v); }
 // min over components of (magnitude bits - 1): zero maps to 0xffffffff, so the chunk minimum
 // is (smallest nonzero magnitude - 1), or ~0u for an all-zero chunk
 __device__ __forceinline__ unsigned min_nz1(const float4& v)
@@ -1387,11 +1393,10 @@ struct geom11 {
     static_assert(HP <= NT && H / 2 <= NT, "halo: one float4 per thread");
 };
 
-template <int D, int QH>
-__device__ __forceinline__ void store_pair11(unsigned char* buf, int r, int s, float a_re, float b_re, float a_im,
+template <class G>
+__device__ __forceinline__ void store_pair_g(unsigned char* buf, int r, int s, float a_re, float b_re, float a_im,
                                              float b_im, int sc)
 {
-    using G = geom11<D, QH>;
     unsigned char* ph = buf + r * G::PH;
     const int off = (s >> 4) * 32 + (s & 15) * 2;
     const float ar = __builtin_ldexpf(a_re, sc), br = __builtin_ldexpf(b_re, sc);
@@ -1403,6 +1408,12 @@ __device__ __forceinline__ void store_pair11(unsigned char* buf, int r, int s, f
     *reinterpret_cast<unsigned*>(ph + G::IM_OFF + off) = __builtin_bit_cast(unsigned, f16x2{ ai0, bi0 });
     *reinterpret_cast<unsigned*>(ph + G::IM_OFF + G::PLANE + off) =
         __builtin_bit_cast(unsigned, f16x2{ (_Float16)(ai - (float)ai0), (_Float16)(bi - (float)bi0) });
+}
+template <int D, int QH>
+__device__ __forceinline__ void store_pair11(unsigned char* buf, int r, int s, float a_re, float b_re, float a_im,
+                                             float b_im, int sc)
+{
+    store_pair_g<geom11<D, QH>>(buf, r, s, a_re, b_re, a_im, b_im, sc);
 }
 
 template <int D, int QH>
@@ -1730,6 +1741,486 @@ int launch_dec(const nsh_fir_plan* p, const float2* in, const float2* hin, float
     case 5: return launch_v7<D, 5>(p, in, hin, hout, out, n_out, s);
     case 6: return launch_v7<D, 6>(p, in, hin, hout, out, n_out, s);
     default: return nsh::fail_msg("nsh_fir_ccf(mfma decim): unsupported tap count");
+    }
+}
+
+// ---- k_fir_casc2: two decimate-by-2 FIRs fused, stage 1's outputs kept in LDS ---------------
+// y1 = fir(h1, 2) x, y2 = fir(h2, 2) y1 in one launch: each step runs k_fir_mfma11<2, QH1>'s
+// step on input chunk ch (2048 x -> 1024 y1), writes the 1024 y1 raw (fp32) into one half of
+// an LDS ring R instead of global memory, then filters that y1 chunk with stage 2 (k_fir_mfma11's
+// numerics over 1024-sample chunks: 512 y2 per step, one 16x16 tile per wave): per-chunk scale
+// from the y1 chunk's maximum and its predecessor's, fp16x2 split from R into stage-2 planes (or
+// raw when the chunk needs the exact path), MFMA, store. HBM per input sample: 8 B in + 0.5 B
+// out, against 8 + 4 + 4 + 2 for the two kernels apart. The stage-2 halo (2 H2 y1 samples) is the
+// tail of R's other half; a workgroup's first y1 chunk gets it from the fp32 direct form over
+// its x window (or from the y1 history at the stream start). Stage-2 taps live in LDS (the
+// stage-1 B fragments already fill the VGPR budget). Two LDS barriers per step: after y1 is in R,
+// after the stage-2 planes are.
+template <int QH>
+struct geomc2 {
+    static constexpr int NT = 256;
+    static constexpr int CHUNK_IN = 1024;
+    static constexpr int CHUNK = 512;
+    static constexpr int WAVE_OUT = 128;
+    static constexpr int KS = QH / 2;
+    static constexpr int TAIL = QH % 2;
+    static constexpr int H = 16 * (QH - 1);                    // halo samples per phase
+    static constexpr int HR = QH - 1;
+    static constexpr int NB = (CHUNK + H) / 16;
+    static constexpr int PLANE = NB * 32;
+    static constexpr int IM_OFF = (2 * PLANE + 255) / 256 * 256 + 128;
+    static constexpr int PH = (IM_OFF + 2 * PLANE + 255) / 256 * 256;
+    static constexpr int BUF = 2 * PH;
+    static constexpr int PER_PHASE = 2 * KS * 64 * 8 + 2 * 64 * 4; // fp16 tap elements
+    static_assert((2 * H + CHUNK_IN) * 8 <= BUF, "a raw fp32 y1 chunk + halo fits the plane buffer");
+    static_assert(H / 2 <= NT, "halo pairs: one per thread");
+};
+template <int QH1, int QH2>
+struct geomcasc {
+    using G1 = geom11<2, QH1>;
+    using G2 = geomc2<QH2>;
+    static constexpr int R = G1::SLOTS + 64;                   // float2 [2][1024]
+    static constexpr int P2 = R + 2 * 1024 * 8;
+    static constexpr int F2 = P2 + G2::BUF;                    // stage-2 fragments, 2 phases
+    static constexpr int S2 = F2 + 2 * G2::PER_PHASE * 2;      // u32 max[4], mnz[4]
+    static constexpr int LDS = S2 + 32;
+    static_assert(2 * LDS <= 160 * 1024, "two workgroups per CU");
+    static_assert(2 * G2::H >= 2 * 16 && 2 * G2::H <= 1024, "halo");
+};
+
+template <int QH1, int QH2>
+__global__ __launch_bounds__(256, 2) void k_fir_casc2(const float2* __restrict__ in,
+                                                     const float2* __restrict__ hist1_in,
+                                                     float2* __restrict__ hist1_out,
+                                                     const float2* __restrict__ hist2_in,
+                                                     float2* __restrict__ hist2_out,
+                                                     float2* __restrict__ out,
+                                                     const _Float16* __restrict__ frag1,
+                                                     const float* __restrict__ taps1, int L1, int sh1,
+                                                     const _Float16* __restrict__ frag2,
+                                                     const float* __restrict__ taps2, int L2, int sh2,
+                                                     int64_t n_out)
+{
+    constexpr int D = 2;
+    using C = geomcasc<QH1, QH2>;
+    using G = geom11<D, QH1>;
+    using G2 = geomc2<QH2>;
+    constexpr int KS = G::KS;
+    constexpr int KS2 = G2::KS;
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    float4* stash = reinterpret_cast<float4*>(lds + 2 * G::BUF);
+    unsigned* slot_max = reinterpret_cast<unsigned*>(lds + G::SLOTS);
+    unsigned* slot_mnz = slot_max + 8;
+    float2* R = reinterpret_cast<float2*>(lds + C::R);
+    unsigned char* P2 = lds + C::P2;
+    _Float16* F2 = reinterpret_cast<_Float16*>(lds + C::F2);
+    unsigned* s2_max = reinterpret_cast<unsigned*>(lds + C::S2);
+    unsigned* s2_mnz = s2_max + 4;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int64_t n1 = 2 * n_out;
+    const int64_t n_in = 4 * n_out;
+
+    if (blockIdx.x == 0) {
+        for (int j = tid; j < L1 - 1; j += G::NT) hist1_out[j] = virt(in, hist1_in, n_in - (L1 - 1) + j, n_in, L1);
+    }
+
+    f16x8 B0[D][KS + 1], B1[D][KS + 1];
+    f16x4 T0[D], T1[D];
+#pragma unroll
+    for (int r = 0; r < D; ++r) {
+        const _Float16* fr = frag1 + (size_t)r * G::PER_PHASE;
+#pragma unroll
+        for (int st = 0; st < KS; ++st) {
+            B0[r][st] = reinterpret_cast<const f16x8*>(fr)[(0 * KS + st) * 64 + lane];
+            B1[r][st] = reinterpret_cast<const f16x8*>(fr)[(1 * KS + st) * 64 + lane];
+        }
+        const f16x4* tf = reinterpret_cast<const f16x4*>(fr + 2 * KS * 64 * 8);
+        T0[r] = tf[lane];
+        T1[r] = tf[64 + lane];
+    }
+    for (int i = tid; i < 2 * G2::PER_PHASE / 8; i += G::NT)
+        reinterpret_cast<f16x8*>(F2)[i] = reinterpret_cast<const f16x8*>(frag2)[i];
+
+    const int64_t nchunks = (n1 + G::CHUNK - 1) / G::CHUNK;
+    const int64_t per = (nchunks + gridDim.x - 1) / gridDim.x;
+    const int64_t c_begin = (int64_t)blockIdx.x * per;
+    const int64_t c_end = c_begin + per < nchunks ? c_begin + per : nchunks;
+    if (c_begin >= c_end) return;
+    const int64_t c_last = c_end - 1;
+
+    const int rho = lane & 15;
+    const int c = rho & 1, b = rho >> 1;
+    const int g = lane >> 4;
+    const int phase = lane & 15;
+    const int row_base = c * G::IM_OFF + (G::HR + wave * (G::WAVE_OUT / 16) + b) * 32;
+    const int row_base2 = c * G2::IM_OFF + (G2::HR + wave * (G2::WAVE_OUT / 16) + b) * 32;
+    const bool tail_owner = tid >= G::NT - G::H / 2;
+    auto clamp = [&](int64_t x) { return x <= c_last ? x : c_last; };
+    auto load = [&](float4 (&v)[4], int64_t ch) {
+        const __amdgpu_buffer_rsrc_t r = chunk_rsrc<G::CHUNK_IN>(in, ch, n_in);
+#pragma unroll
+        for (int u = 0; u < G::UNITS; ++u)
+#pragma unroll
+            for (int f = 0; f < D; ++f) v[u * D + f] = buf_load_f4(r, ((tid + G::NT * u) * D + f) * 16);
+    };
+    auto stash_tail = [&](float4* st, const float4 (&v)[4]) {
+        if (tail_owner) {
+#pragma unroll
+            for (int f = 0; f < D; ++f) st[(tid - (G::NT - G::H / 2)) * D + f] = v[(G::UNITS - 1) * D + f];
+        }
+    };
+    auto put_chunk = [&](unsigned char* buf, const float4* hsrc, const float4 (&v)[4], bool raw, int sc) {
+        if (raw) {
+            float4* rb = reinterpret_cast<float4*>(buf);
+            if (tid < G::HP) rb[tid] = hsrc[tid];
+#pragma unroll
+            for (int u = 0; u < G::UNITS; ++u)
+#pragma unroll
+                for (int f = 0; f < D; ++f) rb[G::HP + (tid + G::NT * u) * D + f] = v[u * D + f];
+            return;
+        }
+        if (tid < D * (G::H / 2)) {
+            const int r = tid / (G::H / 2), pi = tid % (G::H / 2);
+            const int sr = r == 0 ? 0 : D - r;
+            const int pa = D * (2 * pi) + sr, pb = D * (2 * pi + 1) + sr;
+            const float2 a = f4_sample(hsrc[pa >> 1], pa & 1), bb = f4_sample(hsrc[pb >> 1], pb & 1);
+            store_pair11<D, QH1>(buf, r, 2 * pi, a.x, bb.x, a.y, bb.y, sc);
+        }
+#pragma unroll
+        for (int u = 0; u < G::UNITS; ++u) {
+            const int i0 = 2 * (tid + G::NT * u);
+#pragma unroll
+            for (int r = 0; r < D; ++r) {
+                const int sr = r == 0 ? 0 : D - r;
+                const int la = sr, lb = D + sr;
+                const float2 a = f4_sample(v[u * D + la / 2], la & 1);
+                const float2 bb = f4_sample(v[u * D + lb / 2], lb & 1);
+                store_pair11<D, QH1>(buf, r, G::H + i0, a.x, bb.x, a.y, bb.y, sc);
+            }
+        }
+    };
+    auto reduce = [&](const float4 (&v)[4], unsigned& m, unsigned& z) {
+        m = 0;
+        z = ~0u;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            m = max(m, max_mag(v[u]));
+            z = min(z, min_nz1(v[u]));
+        }
+        m = wave_max(m);
+        z = wave_min(z);
+    };
+    auto mfma_tile = [&](const unsigned char* cur, int unscale, nf2 (&o)[2 * G::TILES]) {
+        f32x4 hi[G::TILES], lo[G::TILES], hi_t[G::TILES], lo_t[G::TILES];
+#pragma unroll
+        for (int t = 0; t < G::TILES; ++t) {
+            hi[t] = f32x4{ 0.f, 0.f, 0.f, 0.f };
+            lo[t] = f32x4{ 0.f, 0.f, 0.f, 0.f };
+            hi_t[t] = f32x4{ 0.f, 0.f, 0.f, 0.f };
+            lo_t[t] = f32x4{ 0.f, 0.f, 0.f, 0.f };
+        }
+#pragma unroll
+        for (int r = 0; r < D; ++r) {
+            const unsigned char* ph = cur + r * G::PH;
+#pragma unroll
+            for (int st = 0; st < KS; ++st) {
+                const int q = 2 * st + (g >> 1);
+#pragma unroll
+                for (int t = 0; t < G::TILES; ++t) {
+                    const int off = row_base + t * 8 * 32 - q * 32 + (g & 1) * 16;
+                    const f16x8 A0 = *reinterpret_cast<const f16x8*>(ph + off);
+                    const f16x8 A1 = *reinterpret_cast<const f16x8*>(ph + off + G::PLANE);
+                    hi[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0, B0[r][st], hi[t], 0, 0, 0);
+                    lo[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0, B1[r][st], lo[t], 0, 0, 0);
+                    lo[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1, B0[r][st], lo[t], 0, 0, 0);
+                }
+            }
+            if constexpr (G::TAIL) {
+#pragma unroll
+                for (int t = 0; t < G::TILES; ++t) {
+                    const int off = row_base + t * 8 * 32 - (QH1 - 1) * 32 + g * 8;
+                    const f16x4 A0 = *reinterpret_cast<const f16x4*>(ph + off);
+                    const f16x4 A1 = *reinterpret_cast<const f16x4*>(ph + off + G::PLANE);
+                    hi_t[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(A0, T0[r], hi_t[t], 0, 0, 0);
+                    lo_t[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(A0, T1[r], lo_t[t], 0, 0, 0);
+                    lo_t[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(A1, T0[r], lo_t[t], 0, 0, 0);
+                }
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < G::TILES; ++t)
+#pragma unroll
+            for (int half = 0; half < 2; ++half)
+                o[2 * t + half] = nf2{ __builtin_ldexpf((hi[t][2 * half] + hi_t[t][2 * half]) + (lo[t][2 * half] + lo_t[t][2 * half]), unscale),
+                                       __builtin_ldexpf((hi[t][2 * half + 1] + hi_t[t][2 * half + 1]) +
+                                                            (lo[t][2 * half + 1] + lo_t[t][2 * half + 1]), unscale) };
+    };
+    auto direct_tile = [&](const unsigned char* cur, nf2 (&o)[2 * G::TILES]) {
+        const float2* raw = reinterpret_cast<const float2*>(cur);
+        for (int oi = 0; oi < 2 * G::TILES; ++oi) {
+            const int blk = (oi >> 1) * 8 + 2 * g + (oi & 1);
+            const int j = D * G::H + D * (wave * G::WAVE_OUT + blk * 16 + phase);
+            float re = 0.f, im = 0.f;
+            for (int k = 0; k < L1; ++k) {
+                const float2 x = raw[j - k];
+                re = fmaf(taps1[k], x.x, re);
+                im = fmaf(taps1[k], x.y, im);
+            }
+            o[oi] = nf2{ re, im };
+        }
+    };
+    // ---- stage 2 on the y1 chunk in R half rc (halo: the tail of half rp)
+    auto put_chunk2 = [&](const float2* rc, const float2* rp, bool raw, int sc) {
+        const float4* c4 = reinterpret_cast<const float4*>(rc);
+        const float4* p4 = reinterpret_cast<const float4*>(rp + 1024 - 2 * G2::H);
+        if (raw) {
+            float4* rb = reinterpret_cast<float4*>(P2);
+            if (tid < G2::H) rb[tid] = p4[tid];
+            rb[G2::H + tid] = c4[tid];
+            rb[G2::H + 256 + tid] = c4[256 + tid];
+            return;
+        }
+        if (tid < G2::H / 2) { // y1 halo samples 4t..4t+3 -> phase 0 (4t, 4t+2), phase 1 (4t+1, 4t+3)
+            const float4 u = p4[2 * tid], w = p4[2 * tid + 1];
+            store_pair_g<G2>(P2, 0, 2 * tid, u.x, w.x, u.y, w.y, sc);
+            store_pair_g<G2>(P2, 1, 2 * tid, u.z, w.z, u.w, w.w, sc);
+        }
+        const float4 u = c4[2 * tid], w = c4[2 * tid + 1];
+        store_pair_g<G2>(P2, 0, G2::H + 2 * tid, u.x, w.x, u.y, w.y, sc);
+        store_pair_g<G2>(P2, 1, G2::H + 2 * tid, u.z, w.z, u.w, w.w, sc);
+    };
+    auto mfma_tile2 = [&](int unscale, nf2 (&o)[2]) {
+        f32x4 hi = { 0.f, 0.f, 0.f, 0.f }, lo = { 0.f, 0.f, 0.f, 0.f };
+        f32x4 hi_t = { 0.f, 0.f, 0.f, 0.f }, lo_t = { 0.f, 0.f, 0.f, 0.f };
+#pragma unroll
+        for (int r = 0; r < D; ++r) {
+            const unsigned char* ph = P2 + r * G2::PH;
+            const _Float16* fr = F2 + r * G2::PER_PHASE;
+#pragma unroll
+            for (int st = 0; st < KS2; ++st) {
+                const int q = 2 * st + (g >> 1);
+                const int off = row_base2 - q * 32 + (g & 1) * 16;
+                const f16x8 A0 = *reinterpret_cast<const f16x8*>(ph + off);
+                const f16x8 A1 = *reinterpret_cast<const f16x8*>(ph + off + G2::PLANE);
+                const f16x8 b0 = reinterpret_cast<const f16x8*>(fr)[(0 * KS2 + st) * 64 + lane];
+                const f16x8 b1 = reinterpret_cast<const f16x8*>(fr)[(1 * KS2 + st) * 64 + lane];
+                hi = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0, b0, hi, 0, 0, 0);
+                lo = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0, b1, lo, 0, 0, 0);
+                lo = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1, b0, lo, 0, 0, 0);
+            }
+            if constexpr (G2::TAIL) {
+                const int off = row_base2 - (QH2 - 1) * 32 + g * 8;
+                const f16x4 A0 = *reinterpret_cast<const f16x4*>(ph + off);
+                const f16x4 A1 = *reinterpret_cast<const f16x4*>(ph + off + G2::PLANE);
+                const f16x4* tf = reinterpret_cast<const f16x4*>(fr + 2 * KS2 * 64 * 8);
+                const f16x4 t0 = tf[lane], t1 = tf[64 + lane];
+                hi_t = __builtin_amdgcn_mfma_f32_16x16x16f16(A0, t0, hi_t, 0, 0, 0);
+                lo_t = __builtin_amdgcn_mfma_f32_16x16x16f16(A0, t1, lo_t, 0, 0, 0);
+                lo_t = __builtin_amdgcn_mfma_f32_16x16x16f16(A1, t0, lo_t, 0, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int half = 0; half < 2; ++half)
+            o[half] = nf2{ __builtin_ldexpf((hi[2 * half] + hi_t[2 * half]) + (lo[2 * half] + lo_t[2 * half]), unscale),
+                           __builtin_ldexpf((hi[2 * half + 1] + hi_t[2 * half + 1]) + (lo[2 * half + 1] + lo_t[2 * half + 1]), unscale) };
+    };
+    auto direct_tile2 = [&](nf2 (&o)[2]) {
+        const float2* raw = reinterpret_cast<const float2*>(P2);
+        for (int half = 0; half < 2; ++half) {
+            const int j = 2 * G2::H + 2 * (wave * G2::WAVE_OUT + (2 * g + half) * 16 + phase);
+            float re = 0.f, im = 0.f;
+            for (int k = 0; k < L2; ++k) {
+                const float2 x = raw[j - k];
+                re = fmaf(taps2[k], x.x, re);
+                im = fmaf(taps2[k], x.y, im);
+            }
+            o[half] = nf2{ re, im };
+        }
+    };
+    auto store_tile2 = [&](int64_t ch, const nf2 (&o)[2]) {
+        const __amdgpu_buffer_rsrc_t r = chunk_rsrc<G2::CHUNK>(out, ch, n_out);
+#pragma unroll
+        for (int half = 0; half < 2; ++half)
+            buf_store_f2(r, (wave * G2::WAVE_OUT + (2 * g + half) * 16 + phase) * 8, o[half]);
+    };
+
+    // ---- prologue. Stage 1 as k_fir_mfma11's; stage 2's first halo (y1 samples
+    // [1024 c_begin - 2 H2, 1024 c_begin)) into the tail of R half 1
+    float4 va[4], vb[4], vc[4];
+    float4 hv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (tid < G::HP) {
+        const int64_t gg = c_begin * G::CHUNK_IN - 2 * G::HP + 2 * tid;
+        const float2 x0 = virt(in, hist1_in, gg, n_in, L1), x1 = virt(in, hist1_in, gg + 1, n_in, L1);
+        hv = make_float4(x0.x, x0.y, x1.x, x1.y);
+        stash[G::HP + tid] = hv;
+    }
+    float2 yh = make_float2(0.f, 0.f);
+    if (tid < 2 * G2::H) {
+        const int64_t v = c_begin * G::CHUNK - 2 * G2::H + tid;
+        if (c_begin == 0) {
+            if (v >= -(int64_t)(L2 - 1)) yh = hist2_in[v + (L2 - 1)];
+        } else { // y1[v] = sum_k h1[k] x[2 v - k]; 2 v - k >= 2 (1024 - 2 H2) - (L1 - 1) > 0
+            float re = 0.f, im = 0.f;
+            for (int k = 0; k < L1; ++k) {
+                const float2 x = in[2 * v - k];
+                re = fmaf(taps1[k], x.x, re);
+                im = fmaf(taps1[k], x.y, im);
+            }
+            yh = make_float2(re, im);
+        }
+        R[2 * 1024 - 2 * G2::H + tid] = yh;
+    }
+    load(va, c_begin);
+    {
+        unsigned m, z;
+        reduce(va, m, z);
+        m = max(m, wave_max(max_mag(hv)));
+        z = min(z, wave_min(min_nz1(hv)));
+        const unsigned m2 = wave_max(max(mag(yh.x), mag(yh.y)));
+        const unsigned z2 = wave_min(min(mag(yh.x) - 1u, mag(yh.y) - 1u));
+        if (lane == 0) {
+            slot_max[wave] = m;
+            slot_mnz[wave] = z;
+            s2_max[wave] = m2;
+            s2_mnz[wave] = z2;
+        }
+    }
+    nsh::lds_barrier();
+    unsigned m_prev = max(max(slot_max[0], slot_max[1]), max(slot_max[2], slot_max[3]));
+    unsigned z_prev = min(min(slot_mnz[0], slot_mnz[1]), min(slot_mnz[2], slot_mnz[3]));
+    unsigned m2_prev = max(max(s2_max[0], s2_max[1]), max(s2_max[2], s2_max[3]));
+    unsigned z2_prev = min(min(s2_mnz[0], s2_mnz[1]), min(s2_mnz[2], s2_mnz[3]));
+    int s_cur = scale_of(m_prev);
+    bool ex_cur = chunk_needs_exact(m_prev, z_prev, s_cur);
+    put_chunk(lds, stash + G::HP, va, ex_cur, s_cur);
+    stash_tail(stash, va);
+    load(va, clamp(c_begin + 1));
+    load(vb, clamp(c_begin + 2));
+    {
+        unsigned m, z;
+        reduce(va, m, z);
+        nsh::lds_barrier();
+        if (lane == 0) {
+            slot_max[4 + wave] = m;
+            slot_mnz[4 + wave] = z;
+        }
+    }
+    nsh::lds_barrier();
+
+    auto step = [&](float4 (&nxt)[4], float4 (&nn)[4], float4 (&ld)[4], int64_t ch) {
+        const int i = (int)(ch - c_begin);
+        const int pi = i & 1, pn = pi ^ 1;
+        const unsigned char* cur = lds + pi * G::BUF;
+        unsigned char* nbuf = lds + pn * G::BUF;
+        const unsigned m_nxt = max(max(slot_max[4 * pn], slot_max[4 * pn + 1]), max(slot_max[4 * pn + 2], slot_max[4 * pn + 3]));
+        const unsigned z_nxt = min(min(slot_mnz[4 * pn], slot_mnz[4 * pn + 1]), min(slot_mnz[4 * pn + 2], slot_mnz[4 * pn + 3]));
+        const unsigned m2 = max(m_prev, m_nxt);
+        const int s_nxt = scale_of(m2);
+        const bool ex_nxt = chunk_needs_exact(m2, min(z_prev, z_nxt), s_nxt);
+        load(ld, clamp(ch + 3));
+        put_chunk(nbuf, stash + pi * G::HP, nxt, ex_nxt, s_nxt);
+        stash_tail(stash + pn * G::HP, nxt);
+        nf2 o[2 * G::TILES];
+        if (ex_cur)
+            direct_tile(cur, o);
+        else
+            mfma_tile(cur, -(s_cur + sh1), o);
+        // y1 chunk ch -> R half pi, with its magnitude range for stage 2's scale
+        float2* rc = R + pi * 1024;
+        unsigned ym = 0, yz = ~0u;
+#pragma unroll
+        for (int oi = 0; oi < 2 * G::TILES; ++oi) {
+            rc[wave * G::WAVE_OUT + ((oi >> 1) * 8 + 2 * g + (oi & 1)) * 16 + phase] = make_float2(o[oi].x, o[oi].y);
+            ym = max(ym, max(mag(o[oi].x), mag(o[oi].y)));
+            yz = min(yz, min(mag(o[oi].x) - 1u, mag(o[oi].y) - 1u));
+        }
+        ym = wave_max(ym);
+        yz = wave_min(yz);
+        unsigned m, z;
+        reduce(nn, m, z);
+        if (lane == 0) {
+            slot_max[4 * pi + wave] = m;
+            slot_mnz[4 * pi + wave] = z;
+            s2_max[wave] = ym;
+            s2_mnz[wave] = yz;
+        }
+        m_prev = m_nxt;
+        z_prev = z_nxt;
+        ex_cur = ex_nxt;
+        s_cur = s_nxt;
+        nsh::lds_barrier();
+        const unsigned m2c = max(max(s2_max[0], s2_max[1]), max(s2_max[2], s2_max[3]));
+        const unsigned z2c = min(min(s2_mnz[0], s2_mnz[1]), min(s2_mnz[2], s2_mnz[3]));
+        const unsigned mm = max(m2c, m2_prev);
+        const int s2 = scale_of(mm);
+        const bool ex2 = chunk_needs_exact(mm, min(z2c, z2_prev), s2);
+        m2_prev = m2c;
+        z2_prev = z2c;
+        put_chunk2(rc, R + pn * 1024, ex2, s2);
+        nsh::lds_barrier();
+        nf2 o2[2];
+        if (ex2)
+            direct_tile2(o2);
+        else
+            mfma_tile2(-(s2 + sh2), o2);
+        store_tile2(ch, o2);
+    };
+    int64_t ch = c_begin;
+    for (; ch + 2 <= c_last; ch += 3) {
+        step(va, vb, vc, ch);
+        step(vb, vc, va, ch + 1);
+        step(vc, va, vb, ch + 2);
+    }
+    if (ch <= c_last) step(va, vb, vc, ch++);
+    if (ch <= c_last) step(vb, vc, va, ch);
+
+    // y1 history: the last L2 - 1 samples, from R (chunk c_last in half hl, its predecessor's
+    // tail -- or the first halo -- in the other)
+    if (c_end == nchunks) {
+        const int hl = (int)((c_last - c_begin) & 1);
+        for (int j = tid; j < L2 - 1; j += G::NT) {
+            const int64_t u = n1 - (L2 - 1) + j - c_last * G::CHUNK;
+            hist2_out[j] = u >= 0 ? R[hl * 1024 + u] : R[(hl ^ 1) * 1024 + 1024 + u];
+        }
+    }
+}
+
+template <int QH1, int QH2>
+int launch_casc2(const nsh_fir_plan* p1, const nsh_fir_plan* p2, const float2* in, const float2* h1i, float2* h1o,
+                 const float2* h2i, float2* h2o, float2* out, int64_t n_out, hipStream_t s)
+{
+    using C = geomcasc<QH1, QH2>;
+    static bool attr_set = false;
+    if (!attr_set) {
+        NSH_CK(hipFuncSetAttribute((const void*)k_fir_casc2<QH1, QH2>, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS));
+        attr_set = true;
+    }
+    const int64_t nchunks = (2 * n_out + 1023) / 1024;
+    int n_cu = 256;
+    (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, p1->dev);
+    const int64_t max_grid = (int64_t)n_cu * 2;
+    const unsigned grid = (unsigned)(nchunks < max_grid ? nchunks : max_grid);
+    hipLaunchKernelGGL((k_fir_casc2<QH1, QH2>), dim3(grid), dim3(256), C::LDS, s, in, h1i, h1o, h2i, h2o, out,
+                       (const _Float16*)p1->fragd8_dev, (const float*)p1->taps_dev, p1->L, p1->sh8,
+                       (const _Float16*)p2->fragd8_dev, (const float*)p2->taps_dev, p2->L, p2->sh8, n_out);
+    NSH_CK_LAUNCH("nsh_fir_cascade2_ccf");
+    return 0;
+}
+
+template <int QH1>
+int casc2_qh2(const nsh_fir_plan* p1, const nsh_fir_plan* p2, const float2* in, const float2* h1i, float2* h1o,
+              const float2* h2i, float2* h2o, float2* out, int64_t n_out, hipStream_t s)
+{
+    switch (p2->QHD) {
+    case 3: return launch_casc2<QH1, 3>(p1, p2, in, h1i, h1o, h2i, h2o, out, n_out, s);
+    case 4: return launch_casc2<QH1, 4>(p1, p2, in, h1i, h1o, h2i, h2o, out, n_out, s);
+    case 5: return launch_casc2<QH1, 5>(p1, p2, in, h1i, h1o, h2i, h2o, out, n_out, s);
+    case 6: return launch_casc2<QH1, 6>(p1, p2, in, h1i, h1o, h2i, h2o, out, n_out, s);
+    default: return nsh::fail_msg("nsh_fir_cascade2_ccf: unsupported stage-2 tap count");
     }
 }
 
@@ -2086,5 +2577,26 @@ int nsh_fir_mfma_run(const nsh_fir_plan* p, const float2* in, const float2* hist
     case 5: return launch_q<5>(p, in, hist_in, hist_out, out, n_out, s);
     case 6: return launch_q<6>(p, in, hist_in, hist_out, out, n_out, s);
     default: return nsh::fail_msg("nsh_fir_ccf(mfma): unsupported tap count");
+    }
+}
+
+bool nsh_fir_cascade2_ok(const nsh_fir_plan* p1, const nsh_fir_plan* p2)
+{
+    auto ok = [](const nsh_fir_plan* p) {
+        return p && p->D == 2 && (p->algo == NSH_FIR_MFMA) && p->fragd8_dev && p->variant != 7 && p->QHD >= 3 &&
+               p->QHD <= 6;
+    };
+    return ok(p1) && ok(p2) && p1->dev == p2->dev;
+}
+
+int nsh_fir_cascade2_run(const nsh_fir_plan* p1, const nsh_fir_plan* p2, const float2* in, const float2* h1i, float2* h1o,
+                         const float2* h2i, float2* h2o, float2* out, int64_t n_out, hipStream_t s)
+{
+    switch (p1->QHD) {
+    case 3: return casc2_qh2<3>(p1, p2, in, h1i, h1o, h2i, h2o, out, n_out, s);
+    case 4: return casc2_qh2<4>(p1, p2, in, h1i, h1o, h2i, h2o, out, n_out, s);
+    case 5: return casc2_qh2<5>(p1, p2, in, h1i, h1o, h2i, h2o, out, n_out, s);
+    case 6: return casc2_qh2<6>(p1, p2, in, h1i, h1o, h2i, h2o, out, n_out, s);
+    default: return nsh::fail_msg("nsh_fir_cascade2_ccf: unsupported stage-1 tap count");
     }
 }

@@ -45,3 +45,6 @@ int nsh_fir_mfma_run(const nsh_fir_plan* p, const float2* in, const float2* hist
                      float2* out, int64_t n_out, hipStream_t s);
 int nsh_fir_mfma16_run(const nsh_fir_plan* p, const float2* in, const float2* hist_in, float2* hist_out,
                        float2* out, int64_t n_out, hipStream_t s);
+bool nsh_fir_cascade2_ok(const nsh_fir_plan* p1, const nsh_fir_plan* p2);
+int nsh_fir_cascade2_run(const nsh_fir_plan* p1, const nsh_fir_plan* p2, const float2* in, const float2* h1i, float2* h1o,
+                         const float2* h2i, float2* h2o, float2* out, int64_t n_out, hipStream_t s);

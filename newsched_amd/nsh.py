@@ -60,6 +60,8 @@ SIGNATURES = {
     "nsh_fir_plan_algo": (_i, [_vp]),
     "nsh_fir_plan_kernel": (C.c_char_p, [_vp]),
     "nsh_fir_ccf": (_i, [_vp, _vp, _vp, _vp, _vp, _i64, _vp]),
+    "nsh_fir_cascade2_supported": (_i, [_vp, _vp]),
+    "nsh_fir_cascade2_ccf": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp]),
     "nsh_fft1024_c2c": (_i, [_vp, _vp, _i64, _i, _vp]),
     "nsh_channelizer1024": (_i, [_vp, _vp, _vp, _i64, _vp]),
 }
@@ -173,6 +175,16 @@ class FirPlan:
     def __call__(self, x, hist_in, hist_out, y, n_out: int, stream=None):
         check(lib().nsh_fir_ccf(self._h, ptr(x), ptr(hist_in), ptr(hist_out), ptr(y), n_out,
                                 stream_ptr(stream)), "nsh_fir_ccf")
+
+    def cascade2_supported(self, stage2: "FirPlan") -> bool:
+        return bool(lib().nsh_fir_cascade2_supported(self._h, stage2._h))
+
+    def cascade2(self, stage2: "FirPlan", x, hist1_in, hist1_out, hist2_in, hist2_out, y, n_out: int,
+                 stream=None):
+        """self (decim 2) then stage2 (decim 2) in one launch: n_out outputs from 4 n_out inputs."""
+        check(lib().nsh_fir_cascade2_ccf(self._h, stage2._h, ptr(x), ptr(hist1_in), ptr(hist1_out),
+                                         ptr(hist2_in), ptr(hist2_out), ptr(y), n_out,
+                                         stream_ptr(stream)), "nsh_fir_cascade2_ccf")
 
     def close(self):
         if getattr(self, "_h", None):
