@@ -1744,18 +1744,24 @@ int launch_dec(const nsh_fir_plan* p, const float2* in, const float2* hin, float
     }
 }
 
-// ---- k_fir_casc2: two decimate-by-2 FIRs fused, stage 1's outputs kept in LDS ---------------
-// y1 = fir(h1, 2) x, y2 = fir(h2, 2) y1 in one launch: each step runs k_fir_mfma11<2, QH1>'s
-// step on input chunk ch (2048 x -> 1024 y1), writes the 1024 y1 raw (fp32) into one half of
-// an LDS ring R instead of global memory, then filters that y1 chunk with stage 2 (k_fir_mfma11's
-// numerics over 1024-sample chunks: 512 y2 per step, one 16x16 tile per wave): per-chunk scale
-// from the y1 chunk's maximum and its predecessor's, fp16x2 split from R into stage-2 planes (or
-// raw when the chunk needs the exact path), MFMA, store. HBM per input sample: 8 B in + 0.5 B
-// out, against 8 + 4 + 4 + 2 for the two kernels apart. The stage-2 halo (2 H2 y1 samples) is the
-// tail of R's other half; a workgroup's first y1 chunk gets it from the fp32 direct form over
-// its x window (or from the y1 history at the stream start). Stage-2 taps live in LDS (the
-// stage-1 B fragments already fill the VGPR budget). Two LDS barriers per step: after y1 is in R,
-// after the stage-2 planes are.
+// ---- k_fir_casc2: two decimate-by-2 FIRs fused, stage 1's outputs never leave the CU -------
+// y1 = fir(h1, 2) x, y2 = fir(h2, 2) y1 in one launch. HBM per input sample: 8 B in + 0.5 B
+// out, against 8 + 4 + 4 + 2 for the two kernels apart. Step s of a workgroup (one LDS
+// barrier, every memory operation unconditional) does, for its chunk sequence:
+//   stage 1, as k_fir_mfma11<2, QH1>'s step: prefetch x chunk s+3, split chunk s+1, MFMA
+//     chunk s -> y1 (1024 samples, 4 per lane), kept in registers until the next step;
+//   stage 2 split of y1 chunk s-1 (the previous step's registers), at a scale set by that
+//     chunk's maximum (reduced last step, read after the barrier) and its predecessor's: lanes
+//     pair same-phase samples y1[m], y1[m+2] with a DPP exchange inside each quad and write the
+//     fp16x2 planes (or raw fp32 when the chunk needs the exact path); the 2 H2-sample halo is
+//     the raw tail of y1 chunk s-2, kept in an LDS stash;
+//   stage 2 MFMA (or fp32 direct form) on y1 chunk s-2's planes -> 512 y2, stored.
+// So stage 2 lags stage 1 by two steps: the loop runs two extra steps (stage 1 on the clamped
+// last chunk, results unused) and the first two steps' stage-2 stores go to an empty buffer
+// range (dropped). The y1 tail before a workgroup's first chunk (its first halo) and the y1
+// history the call hands on are computed by the fp32 direct form from x (or taken from the y1
+// history at the stream start) before the loop. Stage-2 taps live in LDS (the stage-1 B fragments already fill
+// the VGPR budget).
 template <int QH>
 struct geomc2 {
     static constexpr int NT = 256;
@@ -1773,19 +1779,18 @@ struct geomc2 {
     static constexpr int BUF = 2 * PH;
     static constexpr int PER_PHASE = 2 * KS * 64 * 8 + 2 * 64 * 4; // fp16 tap elements
     static_assert((2 * H + CHUNK_IN) * 8 <= BUF, "a raw fp32 y1 chunk + halo fits the plane buffer");
-    static_assert(H / 2 <= NT, "halo pairs: one per thread");
+    static_assert(H / 2 <= NT, "halo: one thread per 4 samples");
 };
 template <int QH1, int QH2>
 struct geomcasc {
     using G1 = geom11<2, QH1>;
     using G2 = geomc2<QH2>;
-    static constexpr int R = G1::SLOTS + 64;                   // float2 [2][1024]
-    static constexpr int P2 = R + 2 * 1024 * 8;
-    static constexpr int F2 = P2 + G2::BUF;                    // stage-2 fragments, 2 phases
-    static constexpr int S2 = F2 + 2 * G2::PER_PHASE * 2;      // u32 max[4], mnz[4]
-    static constexpr int LDS = S2 + 32;
+    static constexpr int P2 = G1::SLOTS + 64;                  // stage-2 planes [2][BUF]
+    static constexpr int ST2 = P2 + 2 * G2::BUF;               // raw y1 tails float2 [2][2 H2]
+    static constexpr int F2 = ST2 + 2 * 2 * G2::H * 8;         // stage-2 fragments, 2 phases
+    static constexpr int S2 = F2 + 2 * G2::PER_PHASE * 2;      // u32 max[2][4], mnz[2][4]
+    static constexpr int LDS = S2 + 64;
     static_assert(2 * LDS <= 160 * 1024, "two workgroups per CU");
-    static_assert(2 * G2::H >= 2 * 16 && 2 * G2::H <= 1024, "halo");
 };
 
 template <int QH1, int QH2>
@@ -1807,16 +1812,16 @@ __global__ __launch_bounds__(256, 2) void k_fir_casc2(const float2* __restrict__
     using G2 = geomc2<QH2>;
     constexpr int KS = G::KS;
     constexpr int KS2 = G2::KS;
+    constexpr int HY = 2 * G2::H; // stage-2 halo, y1 samples
     typedef float f32x4 __attribute__((ext_vector_type(4)));
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     float4* stash = reinterpret_cast<float4*>(lds + 2 * G::BUF);
     unsigned* slot_max = reinterpret_cast<unsigned*>(lds + G::SLOTS);
     unsigned* slot_mnz = slot_max + 8;
-    float2* R = reinterpret_cast<float2*>(lds + C::R);
-    unsigned char* P2 = lds + C::P2;
+    float2* st2 = reinterpret_cast<float2*>(lds + C::ST2);
     _Float16* F2 = reinterpret_cast<_Float16*>(lds + C::F2);
     unsigned* s2_max = reinterpret_cast<unsigned*>(lds + C::S2);
-    unsigned* s2_mnz = s2_max + 4;
+    unsigned* s2_mnz = s2_max + 8;
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -1827,6 +1832,28 @@ __global__ __launch_bounds__(256, 2) void k_fir_casc2(const float2* __restrict__
     if (blockIdx.x == 0) {
         for (int j = tid; j < L1 - 1; j += G::NT) hist1_out[j] = virt(in, hist1_in, n_in - (L1 - 1) + j, n_in, L1);
     }
+    // y1[v] by the fp32 direct form (v < 0: the y1 history); plain loads when the window lies
+    // inside this call's input (every workgroup's first halo but the stream start's)
+    auto y1_direct = [&](int64_t v) -> float2 {
+        if (v < 0) return v >= -(int64_t)(L2 - 1) ? hist2_in[v + (L2 - 1)] : make_float2(0.f, 0.f);
+        float re = 0.f, im = 0.f;
+        if (2 * v - (L1 - 1) >= 0 && 2 * v < n_in) {
+            const float2* xv = in + 2 * v;
+#pragma unroll 8
+            for (int k = 0; k < L1; ++k) {
+                const float2 x = xv[-k];
+                re = fmaf(taps1[k], x.x, re);
+                im = fmaf(taps1[k], x.y, im);
+            }
+        } else {
+            for (int k = 0; k < L1; ++k) {
+                const float2 x = virt(in, hist1_in, 2 * v - k, n_in, L1);
+                re = fmaf(taps1[k], x.x, re);
+                im = fmaf(taps1[k], x.y, im);
+            }
+        }
+        return make_float2(re, im);
+    };
 
     f16x8 B0[D][KS + 1], B1[D][KS + 1];
     f16x4 T0[D], T1[D];
@@ -1851,14 +1878,22 @@ __global__ __launch_bounds__(256, 2) void k_fir_casc2(const float2* __restrict__
     const int64_t c_end = c_begin + per < nchunks ? c_begin + per : nchunks;
     if (c_begin >= c_end) return;
     const int64_t c_last = c_end - 1;
+    // the y1 history the next call needs (its last L2 - 1 samples), by the workgroup that ends
+    // the stream, up front so that it overlaps the other workgroups' work
+    if (c_end == nchunks) {
+        for (int j = tid; j < L2 - 1; j += G::NT) hist2_out[j] = y1_direct(n1 - (L2 - 1) + j);
+    }
 
     const int rho = lane & 15;
     const int c = rho & 1, b = rho >> 1;
     const int g = lane >> 4;
     const int phase = lane & 15;
+    const int q4 = lane & 3;
     const int row_base = c * G::IM_OFF + (G::HR + wave * (G::WAVE_OUT / 16) + b) * 32;
     const int row_base2 = c * G2::IM_OFF + (G2::HR + wave * (G2::WAVE_OUT / 16) + b) * 32;
     const bool tail_owner = tid >= G::NT - G::H / 2;
+    // y1 chunk position of the lane's stage-1 output oi
+    auto y1_pos = [&](int oi) { return wave * G::WAVE_OUT + ((oi >> 1) * 8 + 2 * g + (oi & 1)) * 16 + phase; };
     auto clamp = [&](int64_t x) { return x <= c_last ? x : c_last; };
     auto load = [&](float4 (&v)[4], int64_t ch) {
         const __amdgpu_buffer_rsrc_t r = chunk_rsrc<G::CHUNK_IN>(in, ch, n_in);
@@ -1962,8 +1997,7 @@ __global__ __launch_bounds__(256, 2) void k_fir_casc2(const float2* __restrict__
     auto direct_tile = [&](const unsigned char* cur, nf2 (&o)[2 * G::TILES]) {
         const float2* raw = reinterpret_cast<const float2*>(cur);
         for (int oi = 0; oi < 2 * G::TILES; ++oi) {
-            const int blk = (oi >> 1) * 8 + 2 * g + (oi & 1);
-            const int j = D * G::H + D * (wave * G::WAVE_OUT + blk * 16 + phase);
+            const int j = D * G::H + D * y1_pos(oi);
             float re = 0.f, im = 0.f;
             for (int k = 0; k < L1; ++k) {
                 const float2 x = raw[j - k];
@@ -1973,32 +2007,52 @@ __global__ __launch_bounds__(256, 2) void k_fir_casc2(const float2* __restrict__
             o[oi] = nf2{ re, im };
         }
     };
-    // ---- stage 2 on the y1 chunk in R half rc (halo: the tail of half rp)
-    auto put_chunk2 = [&](const float2* rc, const float2* rp, bool raw, int sc) {
-        const float4* c4 = reinterpret_cast<const float4*>(rc);
-        const float4* p4 = reinterpret_cast<const float4*>(rp + 1024 - 2 * G2::H);
+    // ---- stage 2. Split of y1 chunk (registers y, its halo the raw tail hs of the chunk
+    // before) into planes p2: y1 position m (phase m & 1, index m >> 1). Quad lanes q4 = 0, 1
+    // write the real parts of (y1[m], y1[m + 2]), lanes 2, 3 the imaginary parts of
+    // (y1[m - 2], y1[m]): one DPP exchange (quad_perm [2,3,0,1]) per sample
+    auto put_chunk2 = [&](unsigned char* p2, const float2* hs, float2* hs_next, const nf2 (&y)[2 * G::TILES], bool raw,
+                          int sc) {
         if (raw) {
-            float4* rb = reinterpret_cast<float4*>(P2);
-            if (tid < G2::H) rb[tid] = p4[tid];
-            rb[G2::H + tid] = c4[tid];
-            rb[G2::H + 256 + tid] = c4[256 + tid];
-            return;
+            float2* rb = reinterpret_cast<float2*>(p2);
+            if (tid < HY / 2) reinterpret_cast<float4*>(rb)[tid] = reinterpret_cast<const float4*>(hs)[tid];
+#pragma unroll
+            for (int oi = 0; oi < 2 * G::TILES; ++oi) rb[HY + y1_pos(oi)] = make_float2(y[oi].x, y[oi].y);
+        } else {
+            if (tid < G2::H / 2) { // halo samples 4t..4t+3 -> phase 0 (4t, 4t+2), phase 1 (4t+1, 4t+3)
+                const float4 u = reinterpret_cast<const float4*>(hs)[2 * tid], w = reinterpret_cast<const float4*>(hs)[2 * tid + 1];
+                store_pair_g<G2>(p2, 0, 2 * tid, u.x, w.x, u.y, w.y, sc);
+                store_pair_g<G2>(p2, 1, 2 * tid, u.z, w.z, u.w, w.w, sc);
+            }
+#pragma unroll
+            for (int oi = 0; oi < 2 * G::TILES; ++oi) {
+                const bool lo_q = q4 < 2;
+                const float send = lo_q ? y[oi].y : y[oi].x;
+                const float got = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(send), 0x4E, 0xf, 0xf, false));
+                const float a = lo_q ? y[oi].x : got, bb = lo_q ? got : y[oi].y;
+                const int m = y1_pos(oi) - (lo_q ? 0 : 2);
+                const int s = G2::H + (m >> 1);
+                unsigned char* ph = p2 + (m & 1) * G2::PH + (lo_q ? 0 : G2::IM_OFF);
+                const int off = (s >> 4) * 32 + (s & 15) * 2;
+                const float as = __builtin_ldexpf(a, sc), bs = __builtin_ldexpf(bb, sc);
+                const _Float16 a0 = (_Float16)as, b0 = (_Float16)bs;
+                *reinterpret_cast<unsigned*>(ph + off) = __builtin_bit_cast(unsigned, f16x2{ a0, b0 });
+                *reinterpret_cast<unsigned*>(ph + G2::PLANE + off) =
+                    __builtin_bit_cast(unsigned, f16x2{ (_Float16)(as - (float)a0), (_Float16)(bs - (float)b0) });
+            }
         }
-        if (tid < G2::H / 2) { // y1 halo samples 4t..4t+3 -> phase 0 (4t, 4t+2), phase 1 (4t+1, 4t+3)
-            const float4 u = p4[2 * tid], w = p4[2 * tid + 1];
-            store_pair_g<G2>(P2, 0, 2 * tid, u.x, w.x, u.y, w.y, sc);
-            store_pair_g<G2>(P2, 1, 2 * tid, u.z, w.z, u.w, w.w, sc);
+#pragma unroll
+        for (int oi = 0; oi < 2 * G::TILES; ++oi) {
+            const int m = y1_pos(oi) - (G::CHUNK - HY);
+            if (m >= 0) hs_next[m] = make_float2(y[oi].x, y[oi].y);
         }
-        const float4 u = c4[2 * tid], w = c4[2 * tid + 1];
-        store_pair_g<G2>(P2, 0, G2::H + 2 * tid, u.x, w.x, u.y, w.y, sc);
-        store_pair_g<G2>(P2, 1, G2::H + 2 * tid, u.z, w.z, u.w, w.w, sc);
     };
-    auto mfma_tile2 = [&](int unscale, nf2 (&o)[2]) {
+    auto mfma_tile2 = [&](const unsigned char* p2, int unscale, nf2 (&o)[2]) {
         f32x4 hi = { 0.f, 0.f, 0.f, 0.f }, lo = { 0.f, 0.f, 0.f, 0.f };
         f32x4 hi_t = { 0.f, 0.f, 0.f, 0.f }, lo_t = { 0.f, 0.f, 0.f, 0.f };
 #pragma unroll
         for (int r = 0; r < D; ++r) {
-            const unsigned char* ph = P2 + r * G2::PH;
+            const unsigned char* ph = p2 + r * G2::PH;
             const _Float16* fr = F2 + r * G2::PER_PHASE;
 #pragma unroll
             for (int st = 0; st < KS2; ++st) {
@@ -2028,10 +2082,10 @@ __global__ __launch_bounds__(256, 2) void k_fir_casc2(const float2* __restrict__
             o[half] = nf2{ __builtin_ldexpf((hi[2 * half] + hi_t[2 * half]) + (lo[2 * half] + lo_t[2 * half]), unscale),
                            __builtin_ldexpf((hi[2 * half + 1] + hi_t[2 * half + 1]) + (lo[2 * half + 1] + lo_t[2 * half + 1]), unscale) };
     };
-    auto direct_tile2 = [&](nf2 (&o)[2]) {
-        const float2* raw = reinterpret_cast<const float2*>(P2);
+    auto direct_tile2 = [&](const unsigned char* p2, nf2 (&o)[2]) {
+        const float2* raw = reinterpret_cast<const float2*>(p2);
         for (int half = 0; half < 2; ++half) {
-            const int j = 2 * G2::H + 2 * (wave * G2::WAVE_OUT + (2 * g + half) * 16 + phase);
+            const int j = HY + 2 * (wave * G2::WAVE_OUT + (2 * g + half) * 16 + phase);
             float re = 0.f, im = 0.f;
             for (int k = 0; k < L2; ++k) {
                 const float2 x = raw[j - k];
@@ -2041,15 +2095,18 @@ __global__ __launch_bounds__(256, 2) void k_fir_casc2(const float2* __restrict__
             o[half] = nf2{ re, im };
         }
     };
+    // chunks before c_begin (the first two steps' lagging stage 2) store into an empty range
     auto store_tile2 = [&](int64_t ch, const nf2 (&o)[2]) {
-        const __amdgpu_buffer_rsrc_t r = chunk_rsrc<G2::CHUNK>(out, ch, n_out);
+        const int64_t past = (n_out + G2::CHUNK - 1) / G2::CHUNK;
+        const __amdgpu_buffer_rsrc_t r = chunk_rsrc<G2::CHUNK>(out, ch >= c_begin ? ch : past, n_out);
 #pragma unroll
         for (int half = 0; half < 2; ++half)
             buf_store_f2(r, (wave * G2::WAVE_OUT + (2 * g + half) * 16 + phase) * 8, o[half]);
     };
 
-    // ---- prologue. Stage 1 as k_fir_mfma11's; stage 2's first halo (y1 samples
-    // [1024 c_begin - 2 H2, 1024 c_begin)) into the tail of R half 1
+    // ---- prologue. Stage 1 as k_fir_mfma11's. Stage 2: y (the "chunk c_begin - 1" the first
+    // step splits) holds that chunk's real tail (direct form) in the lanes that own it, zeros
+    // elsewhere; its magnitude range goes to s2 slot 1 (parity of c_begin - 1)
     float4 va[4], vb[4], vc[4];
     float4 hv = make_float4(0.f, 0.f, 0.f, 0.f);
     if (tid < G::HP) {
@@ -2058,42 +2115,36 @@ __global__ __launch_bounds__(256, 2) void k_fir_casc2(const float2* __restrict__
         hv = make_float4(x0.x, x0.y, x1.x, x1.y);
         stash[G::HP + tid] = hv;
     }
-    float2 yh = make_float2(0.f, 0.f);
-    if (tid < 2 * G2::H) {
-        const int64_t v = c_begin * G::CHUNK - 2 * G2::H + tid;
-        if (c_begin == 0) {
-            if (v >= -(int64_t)(L2 - 1)) yh = hist2_in[v + (L2 - 1)];
-        } else { // y1[v] = sum_k h1[k] x[2 v - k]; 2 v - k >= 2 (1024 - 2 H2) - (L1 - 1) > 0
-            float re = 0.f, im = 0.f;
-            for (int k = 0; k < L1; ++k) {
-                const float2 x = in[2 * v - k];
-                re = fmaf(taps1[k], x.x, re);
-                im = fmaf(taps1[k], x.y, im);
-            }
-            yh = make_float2(re, im);
+    nf2 y[2 * G::TILES];
+    unsigned ym = 0, yz = ~0u;
+#pragma unroll
+    for (int oi = 0; oi < 2 * G::TILES; ++oi) {
+        y[oi] = nf2{ 0.f, 0.f };
+        if (y1_pos(oi) >= G::CHUNK - HY) {
+            const float2 v = y1_direct(c_begin * G::CHUNK - G::CHUNK + y1_pos(oi));
+            y[oi] = nf2{ v.x, v.y };
         }
-        R[2 * 1024 - 2 * G2::H + tid] = yh;
+        ym = max(ym, max(mag(y[oi].x), mag(y[oi].y)));
+        yz = min(yz, min(mag(y[oi].x) - 1u, mag(y[oi].y) - 1u));
     }
+    ym = wave_max(ym);
+    yz = wave_min(yz);
     load(va, c_begin);
     {
         unsigned m, z;
         reduce(va, m, z);
         m = max(m, wave_max(max_mag(hv)));
         z = min(z, wave_min(min_nz1(hv)));
-        const unsigned m2 = wave_max(max(mag(yh.x), mag(yh.y)));
-        const unsigned z2 = wave_min(min(mag(yh.x) - 1u, mag(yh.y) - 1u));
         if (lane == 0) {
             slot_max[wave] = m;
             slot_mnz[wave] = z;
-            s2_max[wave] = m2;
-            s2_mnz[wave] = z2;
+            s2_max[4 + wave] = ym;
+            s2_mnz[4 + wave] = yz;
         }
     }
     nsh::lds_barrier();
     unsigned m_prev = max(max(slot_max[0], slot_max[1]), max(slot_max[2], slot_max[3]));
     unsigned z_prev = min(min(slot_mnz[0], slot_mnz[1]), min(slot_mnz[2], slot_mnz[3]));
-    unsigned m2_prev = max(max(s2_max[0], s2_max[1]), max(s2_max[2], s2_max[3]));
-    unsigned z2_prev = min(min(s2_mnz[0], s2_mnz[1]), min(s2_mnz[2], s2_mnz[3]));
     int s_cur = scale_of(m_prev);
     bool ex_cur = chunk_needs_exact(m_prev, z_prev, s_cur);
     put_chunk(lds, stash + G::HP, va, ex_cur, s_cur);
@@ -2110,7 +2161,12 @@ __global__ __launch_bounds__(256, 2) void k_fir_casc2(const float2* __restrict__
         }
     }
     nsh::lds_barrier();
+    unsigned m2_prev = 0, z2_prev = ~0u; // y1 chunk before the one being split
+    int s2_lag = 0;                       // chunk s-2's stage-2 scale / exact flag
+    bool ex2_lag = false;
 
+    // step for chunk ch (i = ch - c_begin): stage 1 on ch, stage-2 split of ch-1, stage-2
+    // MFMA + store of ch-2
     auto step = [&](float4 (&nxt)[4], float4 (&nn)[4], float4 (&ld)[4], int64_t ch) {
         const int i = (int)(ch - c_begin);
         const int pi = i & 1, pn = pi ^ 1;
@@ -2121,72 +2177,62 @@ __global__ __launch_bounds__(256, 2) void k_fir_casc2(const float2* __restrict__
         const unsigned m2 = max(m_prev, m_nxt);
         const int s_nxt = scale_of(m2);
         const bool ex_nxt = chunk_needs_exact(m2, min(z_prev, z_nxt), s_nxt);
+        // y1 chunk ch-1 (parity pn): its range was reduced last step
+        const unsigned m2c = max(max(s2_max[4 * pn], s2_max[4 * pn + 1]), max(s2_max[4 * pn + 2], s2_max[4 * pn + 3]));
+        const unsigned z2c = min(min(s2_mnz[4 * pn], s2_mnz[4 * pn + 1]), min(s2_mnz[4 * pn + 2], s2_mnz[4 * pn + 3]));
+        const unsigned mm = max(m2c, m2_prev);
+        const int s2 = scale_of(mm);
+        const bool ex2 = chunk_needs_exact(mm, min(z2c, z2_prev), s2);
         load(ld, clamp(ch + 3));
         put_chunk(nbuf, stash + pi * G::HP, nxt, ex_nxt, s_nxt);
         stash_tail(stash + pn * G::HP, nxt);
-        nf2 o[2 * G::TILES];
+        // y1 chunk ch-1 -> planes [pn]; halo = raw tail of ch-2 (stash [pi]); its tail -> [pn]
+        put_chunk2(lds + C::P2 + pn * G2::BUF, st2 + pi * HY, st2 + pn * HY, y, ex2, s2);
         if (ex_cur)
-            direct_tile(cur, o);
+            direct_tile(cur, y);
         else
-            mfma_tile(cur, -(s_cur + sh1), o);
-        // y1 chunk ch -> R half pi, with its magnitude range for stage 2's scale
-        float2* rc = R + pi * 1024;
-        unsigned ym = 0, yz = ~0u;
+            mfma_tile(cur, -(s_cur + sh1), y);
+        nf2 o2[2];
+        if (ex2_lag)
+            direct_tile2(lds + C::P2 + pi * G2::BUF, o2);
+        else
+            mfma_tile2(lds + C::P2 + pi * G2::BUF, -(s2_lag + sh2), o2);
+        store_tile2(ch - 2, o2);
+        unsigned ymx = 0, yzn = ~0u;
 #pragma unroll
         for (int oi = 0; oi < 2 * G::TILES; ++oi) {
-            rc[wave * G::WAVE_OUT + ((oi >> 1) * 8 + 2 * g + (oi & 1)) * 16 + phase] = make_float2(o[oi].x, o[oi].y);
-            ym = max(ym, max(mag(o[oi].x), mag(o[oi].y)));
-            yz = min(yz, min(mag(o[oi].x) - 1u, mag(o[oi].y) - 1u));
+            ymx = max(ymx, max(mag(y[oi].x), mag(y[oi].y)));
+            yzn = min(yzn, min(mag(y[oi].x) - 1u, mag(y[oi].y) - 1u));
         }
-        ym = wave_max(ym);
-        yz = wave_min(yz);
+        ymx = wave_max(ymx);
+        yzn = wave_min(yzn);
         unsigned m, z;
         reduce(nn, m, z);
         if (lane == 0) {
             slot_max[4 * pi + wave] = m;
             slot_mnz[4 * pi + wave] = z;
-            s2_max[wave] = ym;
-            s2_mnz[wave] = yz;
+            s2_max[4 * pi + wave] = ymx;
+            s2_mnz[4 * pi + wave] = yzn;
         }
         m_prev = m_nxt;
         z_prev = z_nxt;
         ex_cur = ex_nxt;
         s_cur = s_nxt;
-        nsh::lds_barrier();
-        const unsigned m2c = max(max(s2_max[0], s2_max[1]), max(s2_max[2], s2_max[3]));
-        const unsigned z2c = min(min(s2_mnz[0], s2_mnz[1]), min(s2_mnz[2], s2_mnz[3]));
-        const unsigned mm = max(m2c, m2_prev);
-        const int s2 = scale_of(mm);
-        const bool ex2 = chunk_needs_exact(mm, min(z2c, z2_prev), s2);
         m2_prev = m2c;
         z2_prev = z2c;
-        put_chunk2(rc, R + pn * 1024, ex2, s2);
+        s2_lag = s2;
+        ex2_lag = ex2;
         nsh::lds_barrier();
-        nf2 o2[2];
-        if (ex2)
-            direct_tile2(o2);
-        else
-            mfma_tile2(-(s2 + sh2), o2);
-        store_tile2(ch, o2);
     };
+    const int64_t s_last = c_last + 2;
     int64_t ch = c_begin;
-    for (; ch + 2 <= c_last; ch += 3) {
+    for (; ch + 2 <= s_last; ch += 3) {
         step(va, vb, vc, ch);
         step(vb, vc, va, ch + 1);
         step(vc, va, vb, ch + 2);
     }
-    if (ch <= c_last) step(va, vb, vc, ch++);
-    if (ch <= c_last) step(vb, vc, va, ch);
-
-    // y1 history: the last L2 - 1 samples, from R (chunk c_last in half hl, its predecessor's
-    // tail -- or the first halo -- in the other)
-    if (c_end == nchunks) {
-        const int hl = (int)((c_last - c_begin) & 1);
-        for (int j = tid; j < L2 - 1; j += G::NT) {
-            const int64_t u = n1 - (L2 - 1) + j - c_last * G::CHUNK;
-            hist2_out[j] = u >= 0 ? R[hl * 1024 + u] : R[(hl ^ 1) * 1024 + 1024 + u];
-        }
-    }
+    if (ch <= s_last) step(va, vb, vc, ch++);
+    if (ch <= s_last) step(vb, vc, va, ch);
 }
 
 template <int QH1, int QH2>
