@@ -977,7 +977,9 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma7(const float2* __restrict__
     const int64_t c_end = c_begin + per < nchunks ? c_begin + per : nchunks;
     if (c_begin >= c_end) return;
     const int64_t c_last = c_end - 1;
-    auto clamp = [&](int64_t x) { return x <= c_last ? x : c_last; };
+    // prefetch index: past the workgroup's range, an empty buffer range (loads return 0 and move
+    // no bytes; a re-load of the last chunk would go to HBM again, the loads are nontemporal)
+    auto clamp = [&](int64_t x) { return x <= c_last ? x : nchunks; };
 
     float4 va[G::VPT], vb[G::VPT];
     v7_load_store_halo<D, QH>(lds, in, hist_in, c_begin, n_in, L);
@@ -1234,7 +1236,9 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma9(const float2* __restrict__
     const int a_base = c * 2 * G::PLANE + ((Q - 1) + 16 * wave + b) * 80 + 16 * h;
     const int phase = lane & 31;
     const bool tail_owner = tid >= G::NT - G::HP; // holds the chunk's last H samples in v[3]
-    auto clamp = [&](int64_t x) { return x <= c_last ? x : c_last; };
+    // prefetch index: past the workgroup's range, an empty buffer range (loads return 0 and move
+    // no bytes; a re-load of the last chunk would go to HBM again, the loads are nontemporal)
+    auto clamp = [&](int64_t x) { return x <= c_last ? x : nchunks; };
     // chunk (halo pairs from hv_or_stash, main pairs from v) -> buffer, raw or split
     auto put_chunk = [&](unsigned char* buf, const float4& halo, const float4 (&v)[4], bool raw, int sc) {
         if (raw) {
@@ -1472,7 +1476,9 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma11(const float2* __restrict_
     const int phase = lane & 15;
     const int row_base = c * G::IM_OFF + (G::HR + wave * (G::WAVE_OUT / 16) + b) * 32;
     const bool tail_owner = tid >= G::NT - G::H / 2; // holds the chunk's last D*H samples (last unit)
-    auto clamp = [&](int64_t x) { return x <= c_last ? x : c_last; };
+    // prefetch index: past the workgroup's range, an empty buffer range (loads return 0 and move
+    // no bytes; a re-load of the last chunk would go to HBM again, the loads are nontemporal)
+    auto clamp = [&](int64_t x) { return x <= c_last ? x : nchunks; };
     auto load = [&](float4 (&v)[4], int64_t ch) {
         const __amdgpu_buffer_rsrc_t r = chunk_rsrc<G::CHUNK_IN>(in, ch, n_in);
 #pragma unroll
@@ -1894,7 +1900,9 @@ __global__ __launch_bounds__(256, 2) void k_fir_casc2(const float2* __restrict__
     const bool tail_owner = tid >= G::NT - G::H / 2;
     // y1 chunk position of the lane's stage-1 output oi
     auto y1_pos = [&](int oi) { return wave * G::WAVE_OUT + ((oi >> 1) * 8 + 2 * g + (oi & 1)) * 16 + phase; };
-    auto clamp = [&](int64_t x) { return x <= c_last ? x : c_last; };
+    // prefetch index: past the workgroup's range, an empty buffer range (loads return 0 and move
+    // no bytes; a re-load of the last chunk would go to HBM again, the loads are nontemporal)
+    auto clamp = [&](int64_t x) { return x <= c_last ? x : nchunks; };
     auto load = [&](float4 (&v)[4], int64_t ch) {
         const __amdgpu_buffer_rsrc_t r = chunk_rsrc<G::CHUNK_IN>(in, ch, n_in);
 #pragma unroll
