@@ -76,7 +76,7 @@ int main(int argc, char** argv)
         snprintf(nm, 64, "runs of 16, d2 grid 512"); run(nm, [&] { hipLaunchKernelGGL((k<true, 2, 16>), dim3(512), dim3(NT), 0, 0, a, b, nchunks); });
         snprintf(nm, 64, "runs of 64, d2 grid 512"); run(nm, [&] { hipLaunchKernelGGL((k<true, 2, 64>), dim3(512), dim3(NT), 0, 0, a, b, nchunks); });
     }
-    for (int g : {512, 768, 1024, 2048}) {
+    for (int g : {512, 1024, 2048, 4096}) {
         char nm[64];
         snprintf(nm, 64, "contiguous d1 grid %d", g); run(nm, [&] { hipLaunchKernelGGL((k<false, 1>), dim3(g), dim3(NT), 0, 0, a, b, nchunks); });
         snprintf(nm, 64, "contiguous d2 grid %d", g); run(nm, [&] { hipLaunchKernelGGL((k<false, 2>), dim3(g), dim3(NT), 0, 0, a, b, nchunks); });
