@@ -31,42 +31,56 @@ namespace {
 constexpr int N = 1024;
 constexpr int NT = 256;
 
-__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
-__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
-__device__ __forceinline__ float2 cmul(float2 a, float2 b) { return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x); }
+// A complex value is a packed pair (re, im): adds are one v_pk_add_f32, a twiddle multiply is
+// one v_pk_mul_f32 + one v_pk_fma_f32 with the swizzles/negations as operand modifiers. (Written
+// on HIP's float2 struct, the compiler packed the same arithmetic itself but built the operand
+// pairs with ~380 v_mov per channelizer frame, a third of its VALU issue.)
+typedef float cf __attribute__((ext_vector_type(2)));
+
+// a * w with a fused second product: re = fma(-a.y, w.y, a.x w.x), im = fma(a.y, w.x, a.x w.y)
+__device__ __forceinline__ cf cmulw(cf a, cf w)
+{
+    return __builtin_elementwise_fma(a.yy, cf{ -w.y, w.x }, a.xx * w);
+}
+// the channelizer's spectrum multiply: nsh_mul_const_vcc's two-product rounding exactly, so
+// the fused channelizer stays bit-identical to fft -> multiply_const_vcc -> ifft
+__device__ __forceinline__ cf cmul_rn(cf a, cf b)
+{
+    return cf{ __fsub_rn(__fmul_rn(a.x, b.x), __fmul_rn(a.y, b.y)), __fadd_rn(__fmul_rn(a.x, b.y), __fmul_rn(a.y, b.x)) };
+}
 // multiply by -i (forward) or +i (inverse)
 template <bool INV>
-__device__ __forceinline__ float2 rot(float2 a)
+__device__ __forceinline__ cf rot(cf a)
 {
-    return INV ? make_float2(-a.y, a.x) : make_float2(a.y, -a.x);
+    return INV ? cf{ -a.y, a.x } : cf{ a.y, -a.x };
 }
 
 // In-place DFT4 of (a, b, c, d): X_k = sum_n x_n W_4^{nk}, W_4 = e^{-+i pi/2}.
 template <bool INV>
-__device__ __forceinline__ void dft4(float2& a, float2& b, float2& c, float2& d)
+__device__ __forceinline__ void dft4(cf& a, cf& b, cf& c, cf& d)
 {
-    const float2 s0 = cadd(a, c), d0 = csub(a, c);
-    const float2 s1 = cadd(b, d), d1 = rot<INV>(csub(b, d));
-    a = cadd(s0, s1);
-    c = csub(s0, s1);
-    b = cadd(d0, d1);
-    d = csub(d0, d1);
+    const cf s0 = a + c, d0 = a - c;
+    const cf s1 = b + d, d1 = rot<INV>(b - d);
+    a = s0 + s1;
+    c = s0 - s1;
+    b = d0 + d1;
+    d = d0 - d1;
 }
 
 // W_16^m, m = 0..9 (forward; conjugated for the inverse)
 template <bool INV>
-__device__ __forceinline__ float2 w16(int m)
+__device__ __forceinline__ cf w16(int m)
 {
     constexpr float C1 = 0.92387953251128674f, S1 = 0.38268343236508978f, R2 = 0.70710678118654757f;
-    float2 w;
+    cf w;
     switch (m) {
-    case 1: w = make_float2(C1, -S1); break;
-    case 2: w = make_float2(R2, -R2); break;
-    case 3: w = make_float2(S1, -C1); break;
-    case 4: w = make_float2(0.f, -1.f); break;
-    case 6: w = make_float2(-R2, -R2); break;
-    case 9: w = make_float2(-C1, S1); break;
-    default: w = make_float2(1.f, 0.f); break;
+    case 1: w = cf{ C1, -S1 }; break;
+    case 2: w = cf{ R2, -R2 }; break;
+    case 3: w = cf{ S1, -C1 }; break;
+    case 4: w = cf{ 0.f, -1.f }; break;
+    case 6: w = cf{ -R2, -R2 }; break;
+    case 9: w = cf{ -C1, S1 }; break;
+    default: w = cf{ 1.f, 0.f }; break;
     }
     if (INV) w.y = -w.y;
     return w;
@@ -75,17 +89,23 @@ __device__ __forceinline__ float2 w16(int m)
 // In-place DFT16, natural order in and out: n = 4 n1 + n2, k = k1 + 4 k2,
 // X[k] = sum_n2 W_4^{n2 k2} W_16^{n2 k1} sum_n1 x[4 n1 + n2] W_4^{n1 k1}.
 template <bool INV>
-__device__ __forceinline__ void dft16(float2 (&v)[16])
+__device__ __forceinline__ void dft16(cf (&v)[16])
 {
 #pragma unroll
     for (int n2 = 0; n2 < 4; ++n2) dft4<INV>(v[n2], v[n2 + 4], v[n2 + 8], v[n2 + 12]); // v[n2 + 4 k1] = Y[n2][k1]
 #pragma unroll
     for (int n2 = 1; n2 < 4; ++n2)
 #pragma unroll
-        for (int k1 = 1; k1 < 4; ++k1) v[n2 + 4 * k1] = cmul(v[n2 + 4 * k1], w16<INV>(n2 * k1));
+        for (int k1 = 1; k1 < 4; ++k1) {
+            const int m = n2 * k1;
+            if (m == 4) // W_16^4 = -+i
+                v[n2 + 4 * k1] = rot<INV>(v[n2 + 4 * k1]);
+            else
+                v[n2 + 4 * k1] = cmulw(v[n2 + 4 * k1], w16<INV>(m));
+        }
 #pragma unroll
     for (int k1 = 0; k1 < 4; ++k1) dft4<INV>(v[4 * k1], v[4 * k1 + 1], v[4 * k1 + 2], v[4 * k1 + 3]); // v[4 k1 + k2] = X[k1 + 4 k2]
-    float2 t[16];
+    cf t[16];
 #pragma unroll
     for (int k1 = 0; k1 < 4; ++k1)
 #pragma unroll
@@ -98,9 +118,9 @@ constexpr int WLDS = N + N / 16; // one wave's padded image
 __device__ __forceinline__ int pad(int i) { return i + (i >> 4); }
 
 template <bool INV>
-__device__ __forceinline__ float2 twid(const float2* __restrict__ tw, int t)
+__device__ __forceinline__ cf twid(const cf* __restrict__ tw, int t)
 {
-    float2 w = tw[t & (N - 1)];
+    cf w = tw[t & (N - 1)];
     if (INV) w.y = -w.y;
     return w;
 }
@@ -108,7 +128,7 @@ __device__ __forceinline__ float2 twid(const float2* __restrict__ tw, int t)
 // Transform of one frame held as v[m] = x[lane + 64 m]; on return v[m] = X[lane + 64 m]
 // (pass 3 output kept in registers: m = b + 4 r for butterfly b, output r).
 template <bool INV>
-__device__ __forceinline__ void fft_wave(float2 (&v)[16], float2* __restrict__ img, const float2* __restrict__ tw)
+__device__ __forceinline__ void fft_wave(cf (&v)[16], cf* __restrict__ img, const cf* __restrict__ tw)
 {
     const int j = threadIdx.x & 63;
     // pass 1: Ns = 1, radix 16 -> dst[16 j + r]
@@ -121,7 +141,7 @@ __device__ __forceinline__ void fft_wave(float2 (&v)[16], float2* __restrict__ i
 #pragma unroll
     for (int r = 0; r < 16; ++r) v[r] = img[pad(j + 64 * r)];
 #pragma unroll
-    for (int r = 1; r < 16; ++r) v[r] = cmul(v[r], twid<INV>(tw, 4 * k2 * r));
+    for (int r = 1; r < 16; ++r) v[r] = cmulw(v[r], twid<INV>(tw, 4 * k2 * r));
     dft16<INV>(v);
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -129,14 +149,14 @@ __device__ __forceinline__ void fft_wave(float2 (&v)[16], float2* __restrict__ i
     __builtin_amdgcn_wave_barrier();
     // pass 3: Ns = 256, radix 4; butterfly b of this lane: j' = j + 64 b, src[j' + 256 r],
     // twiddle W_1024^{j' r}, output index j' + 256 r  -> v[b + 4 r]
-    float2 o[16];
+    cf o[16];
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
         const int jp = j + 64 * b;
-        float2 a0 = img[pad(jp)], a1 = img[pad(jp + 256)], a2 = img[pad(jp + 512)], a3 = img[pad(jp + 768)];
-        a1 = cmul(a1, twid<INV>(tw, jp));
-        a2 = cmul(a2, twid<INV>(tw, 2 * jp));
-        a3 = cmul(a3, twid<INV>(tw, 3 * jp));
+        cf a0 = img[pad(jp)], a1 = img[pad(jp + 256)], a2 = img[pad(jp + 512)], a3 = img[pad(jp + 768)];
+        a1 = cmulw(a1, twid<INV>(tw, jp));
+        a2 = cmulw(a2, twid<INV>(tw, 2 * jp));
+        a3 = cmulw(a3, twid<INV>(tw, 3 * jp));
         dft4<INV>(a0, a1, a2, a3);
         o[b] = a0;
         o[b + 4] = a1;
@@ -152,19 +172,20 @@ __device__ __forceinline__ void fft_wave(float2 (&v)[16], float2* __restrict__ i
 // past the end reads zeros and drops its stores, so the loop issues the same memory
 // instructions every iteration (no conditional prefetch) and the compiler's vmcnt waits stay
 // exact -- the next frame's loads remain in flight across this frame's transform and stores.
-__device__ __forceinline__ void load_frame16(float2 (&v)[16], const float2* __restrict__ in, int64_t f, int64_t nframes)
+__device__ __forceinline__ void load_frame16(cf (&v)[16], const float2* __restrict__ in, int64_t f, int64_t nframes)
 {
     const int j = threadIdx.x & 63;
     const __amdgpu_buffer_rsrc_t r = nsh::chunk_rsrc<N>(in, f, nframes * N);
 #pragma unroll
-    for (int m = 0; m < 16; ++m) v[m] = nsh::buf_load_f2(r, (j + 64 * m) * 8);
+    for (int m = 0; m < 16; ++m)
+        v[m] = __builtin_bit_cast(cf, __builtin_amdgcn_raw_buffer_load_b64(r, (j + 64 * m) * 8, 0, nsh::AUX_NT));
 }
-__device__ __forceinline__ void store_frame16(const float2 (&v)[16], float2* __restrict__ out, int64_t f, int64_t nframes)
+__device__ __forceinline__ void store_frame16(const cf (&v)[16], float2* __restrict__ out, int64_t f, int64_t nframes)
 {
     const int j = threadIdx.x & 63;
     const __amdgpu_buffer_rsrc_t r = nsh::chunk_rsrc<N>(out, f, nframes * N);
 #pragma unroll
-    for (int m = 0; m < 16; ++m) nsh::buf_store_f2(r, (j + 64 * m) * 8, nsh::buf_f2{ v[m].x, v[m].y });
+    for (int m = 0; m < 16; ++m) nsh::buf_store_f2(r, (j + 64 * m) * 8, v[m]);
 }
 
 constexpr int FPW = NT / 64; // frames (waves) per workgroup
@@ -173,15 +194,15 @@ template <bool INV>
 __global__ __launch_bounds__(NT) void k_fft1024(const float2* __restrict__ in, float2* __restrict__ out, int64_t nframes,
                                                 const float2* __restrict__ tw_g)
 {
-    __shared__ float2 tw[N];
-    __shared__ float2 img_all[FPW * WLDS];
-    for (int t = threadIdx.x; t < N; t += NT) tw[t] = tw_g[t];
+    __shared__ cf tw[N];
+    __shared__ cf img_all[FPW * WLDS];
+    for (int t = threadIdx.x; t < N; t += NT) tw[t] = cf{ tw_g[t].x, tw_g[t].y };
     __syncthreads();
-    float2* img = img_all + (threadIdx.x >> 6) * WLDS;
+    cf* img = img_all + (threadIdx.x >> 6) * WLDS;
     const int64_t stride = (int64_t)gridDim.x * FPW;
     int64_t f = (int64_t)blockIdx.x * FPW + (threadIdx.x >> 6);
     if (f >= nframes) return;
-    float2 v[16], nx[16];
+    cf v[16], nx[16];
     load_frame16(v, in, f, nframes);
     for (; f < nframes; f += stride) {
         load_frame16(nx, in, f + stride, nframes);
@@ -199,23 +220,23 @@ __global__ __launch_bounds__(NT) void k_fft1024(const float2* __restrict__ in, f
 __global__ __launch_bounds__(NT, 2) void k_chan1024(const float2* __restrict__ in, float2* __restrict__ out, int64_t nframes,
                                                     const float2* __restrict__ tw_g, const float2* __restrict__ w)
 {
-    __shared__ float2 tw[N];
-    __shared__ float2 wl[N];
-    __shared__ float2 img_all[FPW * WLDS];
+    __shared__ cf tw[N];
+    __shared__ cf wl[N];
+    __shared__ cf img_all[FPW * WLDS];
     for (int t = threadIdx.x; t < N; t += NT) {
-        tw[t] = tw_g[t];
-        wl[t] = w[t];
+        tw[t] = cf{ tw_g[t].x, tw_g[t].y };
+        wl[t] = cf{ w[t].x, w[t].y };
     }
     __syncthreads();
-    float2* img = img_all + (threadIdx.x >> 6) * WLDS;
+    cf* img = img_all + (threadIdx.x >> 6) * WLDS;
     const int j = threadIdx.x & 63;
     const int64_t stride = (int64_t)gridDim.x * FPW;
-    float2 v[16];
+    cf v[16];
     for (int64_t f = (int64_t)blockIdx.x * FPW + (threadIdx.x >> 6); f < nframes; f += stride) {
         load_frame16(v, in, f, nframes);
         fft_wave<false>(v, img, tw);
 #pragma unroll
-        for (int m = 0; m < 16; ++m) v[m] = cmul(v[m], wl[j + 64 * m]);
+        for (int m = 0; m < 16; ++m) v[m] = cmul_rn(v[m], wl[j + 64 * m]);
         fft_wave<true>(v, img, tw);
         store_frame16(v, out, f, nframes);
     }
