@@ -1026,6 +1026,18 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma7(const float2* __restrict__
 // c+1 is re-split from the raw fp32 tail of chunk c kept in an LDS stash, not copied.
 typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
 typedef __attribute__((ext_vector_type(2))) _Float16 f16x2;
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+// fp16x2 split of the pair (a, b) * 2^sc: hi = RNE fp16 of each, lo = RNE fp16 of the exact
+// residuals. As packed vectors: one v_cvt_pk_f16_f32 per plane, the residual as one packed
+// subtract (the scalar form converted every value twice).
+__device__ __forceinline__ void split_pair16(float a, float b, int sc, unsigned& hi, unsigned& lo)
+{
+    const f32x2 x = f32x2{ __builtin_ldexpf(a, sc), __builtin_ldexpf(b, sc) };
+    const f16x2 h = __builtin_convertvector(x, f16x2);
+    const f32x2 r = x - __builtin_convertvector(h, f32x2);
+    hi = __builtin_bit_cast(unsigned, h);
+    lo = __builtin_bit_cast(unsigned, __builtin_convertvector(r, f16x2));
+}
 
 template <int Q>
 struct geom8 {
@@ -1127,15 +1139,13 @@ __device__ __forceinline__ void store_pair9(const float4& v, unsigned char* buf,
     *reinterpret_cast<unsigned*>(buf + 3 * G::PLANE + off) = __float_as_uint(v.w);
     return;
 #endif
-    const float ar = __builtin_ldexpf(v.x, sc), br = __builtin_ldexpf(v.z, sc);
-    const float ai = __builtin_ldexpf(v.y, sc), bi = __builtin_ldexpf(v.w, sc);
-    const _Float16 ar0 = (_Float16)ar, br0 = (_Float16)br, ai0 = (_Float16)ai, bi0 = (_Float16)bi;
-    *reinterpret_cast<unsigned*>(buf + 0 * G::PLANE + off) = __builtin_bit_cast(unsigned, f16x2{ ar0, br0 });
-    *reinterpret_cast<unsigned*>(buf + 1 * G::PLANE + off) =
-        __builtin_bit_cast(unsigned, f16x2{ (_Float16)(ar - (float)ar0), (_Float16)(br - (float)br0) });
-    *reinterpret_cast<unsigned*>(buf + 2 * G::PLANE + off) = __builtin_bit_cast(unsigned, f16x2{ ai0, bi0 });
-    *reinterpret_cast<unsigned*>(buf + 3 * G::PLANE + off) =
-        __builtin_bit_cast(unsigned, f16x2{ (_Float16)(ai - (float)ai0), (_Float16)(bi - (float)bi0) });
+    unsigned rh, rl, ih, il;
+    split_pair16(v.x, v.z, sc, rh, rl);
+    split_pair16(v.y, v.w, sc, ih, il);
+    *reinterpret_cast<unsigned*>(buf + 0 * G::PLANE + off) = rh;
+    *reinterpret_cast<unsigned*>(buf + 1 * G::PLANE + off) = rl;
+    *reinterpret_cast<unsigned*>(buf + 2 * G::PLANE + off) = ih;
+    *reinterpret_cast<unsigned*>(buf + 3 * G::PLANE + off) = il;
 }
 
 // MFMA tile -> the lane's 8 outputs, unscaled (lane holds phase rho of blocks (reg & 3) +
@@ -1403,15 +1413,13 @@ __device__ __forceinline__ void store_pair_g(unsigned char* buf, int r, int s, f
 {
     unsigned char* ph = buf + r * G::PH;
     const int off = (s >> 4) * 32 + (s & 15) * 2;
-    const float ar = __builtin_ldexpf(a_re, sc), br = __builtin_ldexpf(b_re, sc);
-    const float ai = __builtin_ldexpf(a_im, sc), bi = __builtin_ldexpf(b_im, sc);
-    const _Float16 ar0 = (_Float16)ar, br0 = (_Float16)br, ai0 = (_Float16)ai, bi0 = (_Float16)bi;
-    *reinterpret_cast<unsigned*>(ph + off) = __builtin_bit_cast(unsigned, f16x2{ ar0, br0 });
-    *reinterpret_cast<unsigned*>(ph + G::PLANE + off) =
-        __builtin_bit_cast(unsigned, f16x2{ (_Float16)(ar - (float)ar0), (_Float16)(br - (float)br0) });
-    *reinterpret_cast<unsigned*>(ph + G::IM_OFF + off) = __builtin_bit_cast(unsigned, f16x2{ ai0, bi0 });
-    *reinterpret_cast<unsigned*>(ph + G::IM_OFF + G::PLANE + off) =
-        __builtin_bit_cast(unsigned, f16x2{ (_Float16)(ai - (float)ai0), (_Float16)(bi - (float)bi0) });
+    unsigned rh, rl, ih, il;
+    split_pair16(a_re, b_re, sc, rh, rl);
+    split_pair16(a_im, b_im, sc, ih, il);
+    *reinterpret_cast<unsigned*>(ph + off) = rh;
+    *reinterpret_cast<unsigned*>(ph + G::PLANE + off) = rl;
+    *reinterpret_cast<unsigned*>(ph + G::IM_OFF + off) = ih;
+    *reinterpret_cast<unsigned*>(ph + G::IM_OFF + G::PLANE + off) = il;
 }
 template <int D, int QH>
 __device__ __forceinline__ void store_pair11(unsigned char* buf, int r, int s, float a_re, float b_re, float a_im,
@@ -2042,11 +2050,10 @@ __global__ __launch_bounds__(256, 2) void k_fir_casc2(const float2* __restrict__
                 const int s = G2::H + (m >> 1);
                 unsigned char* ph = p2 + (m & 1) * G2::PH + (lo_q ? 0 : G2::IM_OFF);
                 const int off = (s >> 4) * 32 + (s & 15) * 2;
-                const float as = __builtin_ldexpf(a, sc), bs = __builtin_ldexpf(bb, sc);
-                const _Float16 a0 = (_Float16)as, b0 = (_Float16)bs;
-                *reinterpret_cast<unsigned*>(ph + off) = __builtin_bit_cast(unsigned, f16x2{ a0, b0 });
-                *reinterpret_cast<unsigned*>(ph + G2::PLANE + off) =
-                    __builtin_bit_cast(unsigned, f16x2{ (_Float16)(as - (float)a0), (_Float16)(bs - (float)b0) });
+                unsigned hi, lo;
+                split_pair16(a, bb, sc, hi, lo);
+                *reinterpret_cast<unsigned*>(ph + off) = hi;
+                *reinterpret_cast<unsigned*>(ph + G2::PLANE + off) = lo;
             }
         }
 #pragma unroll
