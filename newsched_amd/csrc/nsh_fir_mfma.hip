@@ -1170,10 +1170,15 @@ __device__ __forceinline__ void mfma_tile9(const unsigned char* lds, const f16x8
         acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, B1[st], acc_lo, 0, 0, 0);
         acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, B0[st], acc_lo, 0, 0, 0);
     }
+    const f32x16 sum = acc_hi + acc_lo; // packed adds
+    if (unscale >= -126 && unscale <= 127) { // 2^unscale is a normal float: the multiply rounds as ldexp does
+        const nf2 f = nf2{ __builtin_bit_cast(float, (unscale + 127) << 23), __builtin_bit_cast(float, (unscale + 127) << 23) };
 #pragma unroll
-    for (int reg = 0; reg < 8; ++reg)
-        o[reg] = nf2{ __builtin_ldexpf(acc_hi[reg] + acc_lo[reg], unscale),
-                      __builtin_ldexpf(acc_hi[reg + 8] + acc_lo[reg + 8], unscale) };
+        for (int reg = 0; reg < 8; ++reg) o[reg] = nf2{ sum[reg], sum[reg + 8] } * f;
+    } else {
+#pragma unroll
+        for (int reg = 0; reg < 8; ++reg) o[reg] = nf2{ __builtin_ldexpf(sum[reg], unscale), __builtin_ldexpf(sum[reg + 8], unscale) };
+    }
 }
 
 // The exact path on a raw fp32 chunk in LDS (local sample j at float2 index j, halo first):
