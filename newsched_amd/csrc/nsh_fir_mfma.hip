@@ -1426,6 +1426,20 @@ __device__ __forceinline__ void store_pair_g(unsigned char* buf, int r, int s, f
     *reinterpret_cast<unsigned*>(ph + G::IM_OFF + off) = ih;
     *reinterpret_cast<unsigned*>(ph + G::IM_OFF + G::PLANE + off) = il;
 }
+// o = s * 2^u per (re, im) pair: one packed multiply when 2^u is a normal float (it rounds as
+// ldexp does), else ldexp
+template <int M>
+__device__ __forceinline__ void unscale_tile(const nf2 (&s)[M], int u, nf2 (&o)[M])
+{
+    if (u >= -126 && u <= 127) {
+        const float f = __builtin_bit_cast(float, (u + 127) << 23);
+#pragma unroll
+        for (int i = 0; i < M; ++i) o[i] = s[i] * f;
+    } else {
+#pragma unroll
+        for (int i = 0; i < M; ++i) o[i] = nf2{ __builtin_ldexpf(s[i].x, u), __builtin_ldexpf(s[i].y, u) };
+    }
+}
 template <int D, int QH>
 __device__ __forceinline__ void store_pair11(unsigned char* buf, int r, int s, float a_re, float b_re, float a_im,
                                              float b_im, int sc)
@@ -1584,13 +1598,14 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma11(const float2* __restrict_
                 }
             }
         }
+        nf2 sum[2 * G::TILES];
 #pragma unroll
         for (int t = 0; t < G::TILES; ++t)
 #pragma unroll
             for (int half = 0; half < 2; ++half)
-                o[2 * t + half] = nf2{ __builtin_ldexpf((hi[t][2 * half] + hi_t[t][2 * half]) + (lo[t][2 * half] + lo_t[t][2 * half]), unscale),
-                                       __builtin_ldexpf((hi[t][2 * half + 1] + hi_t[t][2 * half + 1]) +
-                                                            (lo[t][2 * half + 1] + lo_t[t][2 * half + 1]), unscale) };
+                sum[2 * t + half] = (nf2{ hi[t][2 * half], hi[t][2 * half + 1] } + nf2{ hi_t[t][2 * half], hi_t[t][2 * half + 1] }) +
+                                    (nf2{ lo[t][2 * half], lo[t][2 * half + 1] } + nf2{ lo_t[t][2 * half], lo_t[t][2 * half + 1] });
+        unscale_tile(sum, unscale, o);
     };
     // exact path: y[m] = sum_k h[k] x[D m - k] from the raw chunk (float2 index D H + D m - k)
     auto direct_tile = [&](const unsigned char* cur, nf2 (&o)[2 * G::TILES]) {
@@ -2007,13 +2022,14 @@ __global__ __launch_bounds__(256, 2) void k_fir_casc2(const float2* __restrict__
                 }
             }
         }
+        nf2 sum[2 * G::TILES];
 #pragma unroll
         for (int t = 0; t < G::TILES; ++t)
 #pragma unroll
             for (int half = 0; half < 2; ++half)
-                o[2 * t + half] = nf2{ __builtin_ldexpf((hi[t][2 * half] + hi_t[t][2 * half]) + (lo[t][2 * half] + lo_t[t][2 * half]), unscale),
-                                       __builtin_ldexpf((hi[t][2 * half + 1] + hi_t[t][2 * half + 1]) +
-                                                            (lo[t][2 * half + 1] + lo_t[t][2 * half + 1]), unscale) };
+                sum[2 * t + half] = (nf2{ hi[t][2 * half], hi[t][2 * half + 1] } + nf2{ hi_t[t][2 * half], hi_t[t][2 * half + 1] }) +
+                                    (nf2{ lo[t][2 * half], lo[t][2 * half + 1] } + nf2{ lo_t[t][2 * half], lo_t[t][2 * half + 1] });
+        unscale_tile(sum, unscale, o);
     };
     auto direct_tile = [&](const unsigned char* cur, nf2 (&o)[2 * G::TILES]) {
         const float2* raw = reinterpret_cast<const float2*>(cur);
@@ -2097,10 +2113,12 @@ __global__ __launch_bounds__(256, 2) void k_fir_casc2(const float2* __restrict__
                 lo_t = __builtin_amdgcn_mfma_f32_16x16x16f16(A1, t0, lo_t, 0, 0, 0);
             }
         }
+        nf2 sum[2];
 #pragma unroll
         for (int half = 0; half < 2; ++half)
-            o[half] = nf2{ __builtin_ldexpf((hi[2 * half] + hi_t[2 * half]) + (lo[2 * half] + lo_t[2 * half]), unscale),
-                           __builtin_ldexpf((hi[2 * half + 1] + hi_t[2 * half + 1]) + (lo[2 * half + 1] + lo_t[2 * half + 1]), unscale) };
+            sum[half] = (nf2{ hi[2 * half], hi[2 * half + 1] } + nf2{ hi_t[2 * half], hi_t[2 * half + 1] }) +
+                        (nf2{ lo[2 * half], lo[2 * half + 1] } + nf2{ lo_t[2 * half], lo_t[2 * half + 1] });
+        unscale_tile(sum, unscale, o);
     };
     auto direct_tile2 = [&](const unsigned char* p2, nf2 (&o)[2]) {
         const float2* raw = reinterpret_cast<const float2*>(p2);
