@@ -1058,10 +1058,11 @@ struct geom8 {
 };
 
 __device__ __forceinline__ unsigned mag(float x) { return __float_as_uint(x) & 0x7fffffffu; }
-__device__ __forceinline__ unsigned max_mag(const float4& v)
-{
-    return max(max(mag(v.x), mag(v.y)), max(mag(v.z), mag(v.w)));
-}
+// largest magnitude as a bit pattern: NaN-propagating v_maximum3_f32 with |.| operand modifiers
+// (a NaN anywhere gives a NaN, i.e. bits >= 0x7f800000, as the integer form did)
+__device__ __forceinline__ float max_abs(float a, float b) { return __builtin_elementwise_maximum(__builtin_fabsf(a), __builtin_fabsf(b)); }
+__device__ __forceinline__ float max_abs4(const float4& v) { return __builtin_elementwise_maximum(max_abs(v.x, v.y), max_abs(v.z, v.w)); }
+__device__ __forceinline__ unsigned max_mag(const float4& v) { return __float_as_uint(max_abs4(v)); }
 // scale exponent: max magnitude (bit pattern) * 2^s in [2^14, 2^15) (zero/subnormal: 2^141)
 __device__ __forceinline__ int scale_of(unsigned maxbits) { return 141 - (int)(maxbits >> 23); }
 // Wave-wide max / min, uniform result: DPP within each 16-lane row (quad_perm xor 1, xor 2,
@@ -1101,17 +1102,19 @@ __device__ __forceinline__ unsigned wave_max(unsigned v) { return wave_red<true>
 __device__ __forceinline__ unsigned wave_min(unsigned v) { return wave_red<false>(v); }
 // min over components of (magnitude bits - 1): zero maps to 0xffffffff, so the chunk minimum
 // is (smallest nonzero magnitude - 1), or ~0u for an all-zero chunk
+// smallest nonzero magnitude, coded as 2 |x|_bits - 1 (one v_lshl_add per value; zero -> ~0u)
+__device__ __forceinline__ unsigned nz_code(float x) { return (__float_as_uint(x) << 1) - 1u; }
 __device__ __forceinline__ unsigned min_nz1(const float4& v)
 {
-    return min(min(mag(v.x) - 1u, mag(v.y) - 1u), min(mag(v.z) - 1u, mag(v.w) - 1u));
+    return min(min(nz_code(v.x), nz_code(v.y)), min(nz_code(v.z), nz_code(v.w)));
 }
 // The exact-path rule over a whole chunk: non-finite iff its largest magnitude is; a nonzero sample
 // scales below fp16's normal range iff its smallest nonzero one does (ldexp is exact, monotonic)
 __device__ __forceinline__ bool chunk_needs_exact(unsigned maxbits, unsigned mnz1, int s)
 {
     if (maxbits >= 0x7f800000u) return true;
-    if (mnz1 == ~0u) return false;
-    return __builtin_ldexpf(__uint_as_float(mnz1 + 1u), s) < 6.103515625e-05f; // 2^-14
+    if (mnz1 == ~0u) return false; // all zero
+    return __builtin_ldexpf(__uint_as_float((mnz1 >> 1) + 1u), s) < 6.103515625e-05f; // 2^-14
 }
 
 // chunk ch -> registers: lane t holds samples (2t, 2t+1) + 512 u, u < 4
@@ -1268,13 +1271,14 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma9(const float2* __restrict__
         }
     };
     auto reduce = [&](const float4 (&v)[4], unsigned& m, unsigned& z) {
-        m = 0;
+        float mf = 0.f;
         z = ~0u;
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            m = max(m, max_mag(v[u]));
+            mf = __builtin_elementwise_maximum(mf, max_abs4(v[u]));
             z = min(z, min_nz1(v[u]));
         }
+        m = __float_as_uint(mf);
         m = wave_max(m);
         z = wave_min(z);
     };
@@ -1551,13 +1555,14 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma11(const float2* __restrict_
         }
     };
     auto reduce = [&](const float4 (&v)[4], unsigned& m, unsigned& z) {
-        m = 0;
+        float mf = 0.f;
         z = ~0u;
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            m = max(m, max_mag(v[u]));
+            mf = __builtin_elementwise_maximum(mf, max_abs4(v[u]));
             z = min(z, min_nz1(v[u]));
         }
+        m = __float_as_uint(mf);
         m = wave_max(m);
         z = wave_min(z);
     };
@@ -1975,13 +1980,14 @@ __global__ __launch_bounds__(256, 2) void k_fir_casc2(const float2* __restrict__
         }
     };
     auto reduce = [&](const float4 (&v)[4], unsigned& m, unsigned& z) {
-        m = 0;
+        float mf = 0.f;
         z = ~0u;
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            m = max(m, max_mag(v[u]));
+            mf = __builtin_elementwise_maximum(mf, max_abs4(v[u]));
             z = min(z, min_nz1(v[u]));
         }
+        m = __float_as_uint(mf);
         m = wave_max(m);
         z = wave_min(z);
     };
@@ -2162,8 +2168,8 @@ __global__ __launch_bounds__(256, 2) void k_fir_casc2(const float2* __restrict__
             const float2 v = y1_direct(c_begin * G::CHUNK - G::CHUNK + y1_pos(oi));
             y[oi] = nf2{ v.x, v.y };
         }
-        ym = max(ym, max(mag(y[oi].x), mag(y[oi].y)));
-        yz = min(yz, min(mag(y[oi].x) - 1u, mag(y[oi].y) - 1u));
+        ym = max(ym, __float_as_uint(max_abs(y[oi].x, y[oi].y)));
+        yz = min(yz, min(nz_code(y[oi].x), nz_code(y[oi].y)));
     }
     ym = wave_max(ym);
     yz = wave_min(yz);
@@ -2239,8 +2245,8 @@ __global__ __launch_bounds__(256, 2) void k_fir_casc2(const float2* __restrict__
         unsigned ymx = 0, yzn = ~0u;
 #pragma unroll
         for (int oi = 0; oi < 2 * G::TILES; ++oi) {
-            ymx = max(ymx, max(mag(y[oi].x), mag(y[oi].y)));
-            yzn = min(yzn, min(mag(y[oi].x) - 1u, mag(y[oi].y) - 1u));
+            ymx = max(ymx, __float_as_uint(max_abs(y[oi].x, y[oi].y)));
+            yzn = min(yzn, min(nz_code(y[oi].x), nz_code(y[oi].y)));
         }
         ymx = wave_max(ymx);
         yzn = wave_min(yzn);
