@@ -46,7 +46,9 @@ __device__ __forceinline__ cf cmulw(cf a, cf w)
 // the fused channelizer stays bit-identical to fft -> multiply_const_vcc -> ifft
 __device__ __forceinline__ cf cmul_rn(cf a, cf b)
 {
-    return cf{ __fsub_rn(__fmul_rn(a.x, b.x), __fmul_rn(a.y, b.y)), __fadd_rn(__fmul_rn(a.x, b.y), __fmul_rn(a.y, b.x)) };
+    const cf t = a.xx * b;    // (ax bx, ax by), each product rounded
+    const cf u = a.yy * b.yx; // (ay by, ay bx)
+    return t + u * cf{ -1.f, 1.f }; // (ax bx - ay by, ax by + ay bx): exact sign flip, one rounding
 }
 // multiply by -i (forward) or +i (inverse)
 template <bool INV>
