@@ -102,7 +102,8 @@ int nsh_synth_cf32(float* out, int64_t n, uint64_t first_index, uint64_t seed, v
  * its own (ntaps-1)-sample history because the reference block API has none
  * (runtime/include/gnuradio/sync_block.hpp:36-86). Per call:
  *   in       : n_out*decim input samples (device)
- *   hist_in  : ntaps-1 samples that precede in[0] (device; zeros at stream start)
+ *   hist_in  : ntaps-1 samples that precede in[0] (device; zeros at stream start; NULL = zeros,
+ *              which saves the stream-start memset)
  *   hist_out : receives the ntaps-1 samples that precede the NEXT call's in[0]
  *              (must not alias hist_in -- ping-pong two buffers)
  * algo: NSH_FIR_AUTO picks by measurement; NSH_FIR_DIRECT is the fp32 VALU
@@ -126,7 +127,8 @@ int nsh_fir_ccf(void* plan, const float* in, const float* hist_in, float* hist_o
  * in = 4 n_out samples; hist1 = ntaps1-1 x samples, hist2 = ntaps2-1 y1 samples, each an
  * in/out pair as for nsh_fir_ccf (no aliasing). Outputs within the fp16x2 MFMA tolerance of
  * the two-call chain (stage 1's outputs are not rounded through HBM: they are the same fp32
- * values). nsh_fir_cascade2_supported returns 1 when the pair qualifies. */
+ * values; a NULL hist*_in reads as zeros). nsh_fir_cascade2_supported returns 1 when the pair
+ * qualifies. */
 int nsh_fir_cascade2_supported(void* plan1, void* plan2);
 int nsh_fir_cascade2_ccf(void* plan1, void* plan2, const float* in, const float* hist1_in, float* hist1_out,
                          const float* hist2_in, float* hist2_out, float* out, int64_t n_out, void* stream);

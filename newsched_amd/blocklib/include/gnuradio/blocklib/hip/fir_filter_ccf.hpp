@@ -54,6 +54,7 @@ private:
     int _dev = -1;
     void* _plan = nullptr;
     void* _hist[2] = { nullptr, nullptr };
+    bool _zero_hist = true; // the next call reads a null history (zeros): set by start()
     int _cur = 0;
     uint64_t _launches = 0;
 };

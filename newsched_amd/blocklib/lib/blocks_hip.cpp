@@ -152,13 +152,15 @@ bool fir_filter_ccf::start()
         check(nsh_malloc(dev, hbytes, &_hist[1]), "hip::fir_filter_ccf history");
     }
     void* s = current_stream();
-    check(nsh_memset_async(_hist[0], 0, hbytes, s), "hip::fir_filter_ccf history reset");
-    check(nsh_memset_async(_hist[1], 0, hbytes, s), "hip::fir_filter_ccf history reset");
+    // the run's first call reads a null history (zeros in the kernel): no memset launches per run;
+    // every call writes its hist_out in full, so the ping-pong buffers need no clearing
+    _zero_hist = true;
     if (!_init_hist.empty()) {
         if (_init_hist.size() != _taps.size() - 1)
             throw std::invalid_argument("hip::fir_filter_ccf: initial history must have ntaps-1 samples");
         check(nsh_memcpy_async(_hist[0], _init_hist.data(), hbytes, NSH_H2D, s), "hip::fir_filter_ccf history load");
         check(nsh_stream_sync(s), "hip::fir_filter_ccf history load"); // host vector must outlive the copy
+        _zero_hist = false;
     }
     _cur = 0;
     _ev_used = 0;
@@ -181,9 +183,10 @@ work_return_code_t fir_filter_ccf::work(std::vector<block_work_input>& in, std::
         ev = &_ev[_ev_used++];
         check(nsh_event_record(ev->first, s), "hip::fir_filter_ccf timing");
     }
-    check(nsh_fir_ccf(_plan, (const float*)in[0].buffer->read_ptr(), (const float*)_hist[_cur], (float*)_hist[_cur ^ 1],
-                      (float*)out[0].buffer->write_ptr(), n_out, s),
+    check(nsh_fir_ccf(_plan, (const float*)in[0].buffer->read_ptr(), _zero_hist ? nullptr : (const float*)_hist[_cur],
+                      (float*)_hist[_cur ^ 1], (float*)out[0].buffer->write_ptr(), n_out, s),
           "hip::fir_filter_ccf");
+    _zero_hist = false;
     if (ev) {
         check(nsh_event_record(ev->second, s), "hip::fir_filter_ccf timing");
         _timed_samples += (uint64_t)n_out;

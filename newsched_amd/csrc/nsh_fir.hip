@@ -37,7 +37,7 @@ __device__ __forceinline__ float2 virt(const float2* __restrict__ in,
                                        int L)
 {
     if (g >= 0) return g < n_in ? in[g] : make_float2(0.f, 0.f);
-    if (g >= -(int64_t)(L - 1)) return hist[g + (L - 1)];
+    if (g >= -(int64_t)(L - 1)) return hist ? hist[g + (L - 1)] : make_float2(0.f, 0.f); // null: zeros
     return make_float2(0.f, 0.f);
 }
 

@@ -71,7 +71,7 @@ constexpr int QMAX = 6;     // L <= 161
 __device__ __forceinline__ float2 virt(const float2* __restrict__ in, const float2* __restrict__ hist, int64_t g, int64_t n_in, int L)
 {
     if (g >= 0) return g < n_in ? in[g] : make_float2(0.f, 0.f);
-    if (g >= -(int64_t)(L - 1)) return hist[g + (L - 1)];
+    if (g >= -(int64_t)(L - 1)) return hist ? hist[g + (L - 1)] : make_float2(0.f, 0.f); // null: zeros
     return make_float2(0.f, 0.f);
 }
 
@@ -1874,7 +1874,7 @@ __global__ __launch_bounds__(256, 2) void k_fir_casc2(const float2* __restrict__
     // y1[v] by the fp32 direct form (v < 0: the y1 history); plain loads when the window lies
     // inside this call's input (every workgroup's first halo but the stream start's)
     auto y1_direct = [&](int64_t v) -> float2 {
-        if (v < 0) return v >= -(int64_t)(L2 - 1) ? hist2_in[v + (L2 - 1)] : make_float2(0.f, 0.f);
+        if (v < 0) return v >= -(int64_t)(L2 - 1) && hist2_in ? hist2_in[v + (L2 - 1)] : make_float2(0.f, 0.f);
         float re = 0.f, im = 0.f;
         if (2 * v - (L1 - 1) >= 0 && 2 * v < n_in) {
             const float2* xv = in + 2 * v;

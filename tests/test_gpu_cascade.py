@@ -97,6 +97,25 @@ def test_cascade2_nonzero_initial_history(torch_cuda):
         assert ok, (n_out, "hist2", err, scale)
 
 
+def test_cascade2_null_histories(torch_cuda):
+    """NULL hist1_in / hist2_in read as zeros: bit-identical to explicit zero histories."""
+    torch = torch_cuda
+    h = _firwin(127, 0.45)
+    p1, p2 = _plans(h, h)
+    for n_out in (2, 50_000):
+        x = orc.synth(4 * n_out, 3)
+        y0, a0, b0 = run_casc(torch, p1, p2, x, n_out)
+        dx = torch.from_numpy(x).cuda()
+        h1o = torch.zeros(126, dtype=torch.complex64, device="cuda")
+        h2o = torch.zeros_like(h1o)
+        dy = torch.empty(n_out, dtype=torch.complex64, device="cuda")
+        p1.cascade2(p2, dx, 0, h1o, 0, h2o, dy, n_out)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(dy.cpu().numpy(), y0)
+        np.testing.assert_array_equal(h1o.cpu().numpy(), a0)
+        np.testing.assert_array_equal(h2o.cpu().numpy(), b0)
+
+
 def test_cascade2_golden_chain4(torch_cuda, golden):
     """The reference's decimator config (4 x fir(127, decim 2)) as two fused
     launches, against the committed golden 4-stage output."""

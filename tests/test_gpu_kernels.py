@@ -165,6 +165,27 @@ def run_fir(torch, plan, x, n_out, hist=None):
 
 
 @pytest.mark.parametrize("name,algo", ALGOS)
+@pytest.mark.parametrize("decim", [1, 2, 4])
+def test_fir_null_history_reads_zeros(torch_cuda, name, algo, decim):
+    """hist_in = NULL is the stream start (zeros): bit-identical to an explicit zero history,
+    for every kernel form and for calls shorter than the filter."""
+    torch = torch_cuda
+    if name != "direct" and name != "mfma" and decim > 1:
+        pytest.skip("decimation: direct and mfma forms")
+    h = np.hamming(127).astype(np.float32) / 70
+    plan = make_plan(name, h, decim, algo)
+    for n_out in (3, 40_001):
+        x = orc.synth(n_out * decim, 8)
+        y0, h0 = run_fir(torch, plan, x, n_out)
+        dx = dev(torch, x)
+        hout = torch.zeros(126, dtype=torch.complex64, device="cuda")
+        dy = torch.empty(n_out, dtype=torch.complex64, device="cuda")
+        plan(dx, 0, hout, dy, n_out)
+        np.testing.assert_array_equal(host(dy), y0)
+        np.testing.assert_array_equal(host(hout), h0)
+
+
+@pytest.mark.parametrize("name,algo", ALGOS)
 def test_fir127_golden(torch_cuda, golden, name, algo):
     torch = torch_cuda
     g = golden("fir127.npz")
