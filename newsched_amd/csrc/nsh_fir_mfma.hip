@@ -2367,13 +2367,17 @@ int launch_v9(const nsh_fir_plan* p, const float2* in, const float2* hin, float2
     const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
     int n_cu = 256;
     (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, p->dev);
-    // Workgroups over the whole launch (2 resident per CU at a time): about 32 chunks each, at
-    // least 2 and at most 16 per CU. Long streams then walk in shorter contiguous ranges, which
-    // keeps the window of addresses in flight compact: at 2^28 samples 16 per CU runs 807 us vs
-    // 855 with 2 (tools/fir_variants.py, same process); at 2^25-2^27 the rule changes nothing.
+    // Workgroups over the whole launch (2 resident per CU at a time): 16 chunks each from 2^26
+    // samples on (at most 32 per CU), else about 32 chunks each (2..16 per CU). Long streams then
+    // walk in shorter contiguous ranges, which keeps the window of addresses in flight compact:
+    // at 2^28 samples 16 per CU ran 807 us vs 855 with 2; after the step's VALU cuts, 32 per CU
+    // (16 chunks) 773 vs 779 us, and 16 chunks per workgroup also wins at 2^26 and 2^27, while
+    // 2^25 keeps 2 per CU (tools/fir_variants.py VARIANTS=0:g, same process).
     int64_t max_grid = (int64_t)n_cu * 2;
     if (p->wg_per_cu > 0)
         max_grid = (int64_t)n_cu * p->wg_per_cu; // NSH_FIR_WG_PER_CU (A/B)
+    else if (nchunks / 16 >= (int64_t)n_cu * 8) // >= 2^26 samples: 16 chunks per workgroup
+        max_grid = std::min<int64_t>(nchunks / 16, (int64_t)n_cu * 32);
     else if (nchunks / 32 > max_grid)
         max_grid = std::min<int64_t>(nchunks / 32, (int64_t)n_cu * 16);
     const unsigned grid = (unsigned)(nchunks < max_grid ? nchunks : max_grid);
