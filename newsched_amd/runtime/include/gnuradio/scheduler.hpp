@@ -23,6 +23,11 @@ public:
     virtual void initialize(flat_graph_sptr fg, flowgraph_monitor_sptr fgmon,
                             neighbor_interface_map scheduler_adapter_map = neighbor_interface_map()) = 0;
     void push_message(scheduler_message_sptr msg) override = 0;
+    // Re-arm run state that other schedulers' threads can observe (buffer done flags). The
+    // flowgraph calls prepare_run() on every scheduler before it starts any of them: a scheduler
+    // that reset its edges' flags in start() could clear a flag a neighbour domain's thread had
+    // already acted on, or leave a stale one for a thread that started first.
+    virtual void prepare_run() {}
     virtual void start() = 0;
     virtual void stop() = 0;
     virtual void wait() = 0;

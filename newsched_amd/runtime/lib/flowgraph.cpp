@@ -157,6 +157,7 @@ void flowgraph::start()
     if (d_schedulers.empty()) throw std::runtime_error("No Scheduler Specified.");
     if (!d_fgmon) validate();
     d_fgmon->start();
+    for (auto& s : d_schedulers) s->prepare_run(); // every domain's edges re-armed first
     for (auto& s : d_schedulers) s->start();
     d_started = true;
 }

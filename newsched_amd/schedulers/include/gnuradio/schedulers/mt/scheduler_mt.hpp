@@ -35,6 +35,7 @@ public:
                          const std::vector<unsigned int>& affinity_mask = {});
     void initialize(flat_graph_sptr fg, flowgraph_monitor_sptr fgmon,
                     neighbor_interface_map block_sched_map = neighbor_interface_map()) override;
+    void prepare_run() override;
     void start() override;
     void stop() override;
     void wait() override;
@@ -60,6 +61,7 @@ protected:
     std::vector<block_sptr> _blocks;
     std::mutex _fin_mtx;
     size_t _n_finished = 0;
+    bool _prepared = false; // prepare_run() done for the next start()
 };
 
 } // namespace schedulers

@@ -89,14 +89,21 @@ void scheduler_mt::thread_finished(int)
     if (all && _fgmon) _fgmon->push_message(fg_monitor_message(fg_monitor_message_t::FLUSHED, id()));
 }
 
-void scheduler_mt::start()
+void scheduler_mt::prepare_run()
 {
+    _prepared = true;
     {
         std::lock_guard<std::mutex> g(_fin_mtx);
         _n_finished = 0;
     }
     if (_bufman)
         for (auto& b : _bufman->all_buffers()) b->reset_flags();
+}
+
+void scheduler_mt::start()
+{
+    if (!_prepared) prepare_run(); // started directly (not through flowgraph::start)
+    _prepared = false;
     if (_threads.empty()) {
         if (_fgmon) _fgmon->push_message(fg_monitor_message(fg_monitor_message_t::FLUSHED, id()));
         return;
