@@ -53,6 +53,17 @@
 
 namespace {
 
+// CUs of the plan's device: one attribute query per plan instead of one per launch
+int plan_cus(const nsh_fir_plan* p)
+{
+    if (p->n_cu <= 0) {
+        int n = 256;
+        (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, p->dev);
+        const_cast<nsh_fir_plan*>(p)->n_cu = n;
+    }
+    return p->n_cu;
+}
+
 using nsh::AUX_NT;
 using nsh::buf_load_f4;
 using nsh::buf_store_f2;
@@ -714,8 +725,7 @@ int launch_v5(const nsh_fir_plan* p, const float2* in, const float2* hin, float2
         attr_set = true;
     }
     const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
-    int n_cu = 256;
-    (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, p->dev);
+    const int n_cu = plan_cus(p);
     const int64_t max_grid = (int64_t)n_cu * wg_per_cu;
     const unsigned grid = (unsigned)(nchunks < max_grid ? nchunks : max_grid);
     const int aligned = ((uintptr_t)in % 16 == 0) ? 1 : 0;
@@ -1727,8 +1737,7 @@ int launch_v7(const nsh_fir_plan* p, const float2* in, const float2* hin, float2
         attr_set = true;
     }
     const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
-    int n_cu = 256;
-    (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, p->dev);
+    const int n_cu = plan_cus(p);
     const int wg_per_cu = (160 * 1024) / G::LDS >= 3 ? 3 : 2; // LDS-bound residency (VGPRs allow 3)
     const int64_t max_grid = (int64_t)n_cu * wg_per_cu;
     const unsigned grid = (unsigned)(nchunks < max_grid ? nchunks : max_grid);
@@ -1749,8 +1758,7 @@ int launch_v11(const nsh_fir_plan* p, const float2* in, const float2* hin, float
         attr_set = true;
     }
     const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
-    int n_cu = 256;
-    (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, p->dev);
+    const int n_cu = plan_cus(p);
     const int64_t max_grid = (int64_t)n_cu * 2; // launch_v9's longer grids measured 4-7 % slower here
     const unsigned grid = (unsigned)(nchunks < max_grid ? nchunks : max_grid);
     hipLaunchKernelGGL((k_fir_mfma11<D, QH>), dim3(grid), dim3(G::NT), G::LDS, s, in, hin, hout, out,
@@ -2290,8 +2298,7 @@ int launch_casc2(const nsh_fir_plan* p1, const nsh_fir_plan* p2, const float2* i
         attr_set = true;
     }
     const int64_t nchunks = (2 * n_out + 1023) / 1024;
-    int n_cu = 256;
-    (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, p1->dev);
+    const int n_cu = plan_cus(p1);
     const int64_t max_grid = (int64_t)n_cu * 2;
     const unsigned grid = (unsigned)(nchunks < max_grid ? nchunks : max_grid);
     hipLaunchKernelGGL((k_fir_casc2<QH1, QH2>), dim3(grid), dim3(256), C::LDS, s, in, h1i, h1o, h2i, h2o, out,
@@ -2342,8 +2349,7 @@ int launch_v2(const nsh_fir_plan* p, const float2* in, const float2* hin, float2
         attr_set = true;
     }
     const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
-    int n_cu = 256;
-    (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, p->dev);
+    const int n_cu = plan_cus(p);
     const int64_t max_grid = (int64_t)n_cu * wg_per_cu;
     const unsigned grid = (unsigned)(nchunks < max_grid ? nchunks : max_grid);
     const int aligned = ((uintptr_t)in % 16 == 0) ? 1 : 0;
@@ -2365,8 +2371,7 @@ int launch_v9(const nsh_fir_plan* p, const float2* in, const float2* hin, float2
         attr_set = true;
     }
     const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
-    int n_cu = 256;
-    (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, p->dev);
+    const int n_cu = plan_cus(p);
     // Workgroups over the whole launch (2 resident per CU at a time): 16 chunks each from 2^26
     // samples on (at most 32 per CU), else about 32 chunks each (2..16 per CU). Long streams then
     // walk in shorter contiguous ranges, which keeps the window of addresses in flight compact:

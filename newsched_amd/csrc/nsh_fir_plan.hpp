@@ -33,6 +33,7 @@ struct nsh_fir_plan {
     bool force_x3 = false; // NSH_FIR_MFMA_BF16X3: always the bf16x3 six-product kernel
     int variant = 0;      // MFMA kernel tuning variant (0 = default)
     int wg_per_cu = 0;    // decim-1 fp16x2 kernel: workgroups per CU over the launch (0 = auto)
+    int n_cu = 0;         // the device's CU count, queried once (0 = not yet)
     std::string kernel;   // the kernel nsh_fir_ccf launches (rocprof name without namespace)
 };
 
