@@ -132,6 +132,38 @@ TEST(SchedulerMTTest, DomainAdapterBasic)
     }
 }
 
+TEST(SchedulerMTTest, RestartAcrossDomainsNeverHangs)
+{
+    // The restart path of the race fixed in flowgraph::start(): fresh
+    // two-domain flowgraphs, each run twice, both buffer preferences. Each scheduler used to
+    // reset its own edges' done flags inside start(), after the other domain's threads had begun
+    // the run; the host -> GPU -> host variant hung within tens of iterations
+    // (tests/test_restart_stress.py). This all-host variant did not reproduce it on its own
+    // timing; it guards the restart sequence on the CPU suite.
+    const auto data = ramp(20000);
+    for (int it = 0; it < 150; ++it) {
+        auto src = blocks::vector_source_c::make(data);
+        auto m1 = blocks::multiply_const_cc::make(gr_complex(0.5f, 0.f));
+        auto m2 = blocks::multiply_const_cc::make(gr_complex(2.f, 0.f));
+        auto snk = blocks::vector_sink_c::make();
+        auto fg = flowgraph::make();
+        fg->connect(src, 0, m1, 0);
+        fg->connect(m1, 0, m2, 0);
+        fg->connect(m2, 0, snk, 0);
+        auto s1 = schedulers::scheduler_mt::make("a", 4096);
+        auto s2 = schedulers::scheduler_mt::make("b", 4096);
+        fg->add_scheduler(s1);
+        fg->add_scheduler(s2);
+        auto da = domain_adapter_direct_conf::make(it % 2 ? buffer_preference_t::UPSTREAM : buffer_preference_t::DOWNSTREAM);
+        domain_conf_vec dconf{ domain_conf(s1, { src, m1 }, da), domain_conf(s2, { m2, snk }, da) };
+        fg->partition(dconf);
+        for (int r = 0; r < 2; ++r) {
+            fg->run();
+            EXPECT_EQ(snk->data().size(), data.size());
+        }
+    }
+}
+
 TEST(SchedulerMTTest, NullSourceHeadCopyNullSink)
 {
     // BASELINE config C1 (reference schedulers/mt/bench/bm_copy.cpp:77-101 shape)
