@@ -6,9 +6,20 @@ A step = one flowgraph run over the rank's N-sample shard: nop_source -> nop_hea
 [HBM-resident hip_buffer ring, preloaded] -> gr::hip::fir_filter_ccf -> [hip_buffer] ->
 null_sink, all inside one scheduler_hip GPU domain (include/nsr_flowgraph.h). Inputs are
 resident in HBM before timing starts; the run ends only after the partition stream has
-drained. With --gpus N (torchrun, one process per GPU) every rank streams its own
-contiguous time shard x[rank*N, (rank+1)*N) with the 126-sample halo regenerated from the
-counter-based source: weak scaling, no data-path collective.
+drained. With --gpus N every rank (one process per GPU) streams its own contiguous time
+shard x[rank*N, (rank+1)*N) with the 126-sample halo regenerated from the counter-based
+source: weak scaling, no data-path collective.
+
+Ranks: under torchrun (WORLD_SIZE set) this process is one rank. Without it, `--gpus N > 1`
+starts N child processes of this script itself (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set,
+before anything here touches the GPU), relays rank 0's line and exits with the first
+failing child's code. `n_gpus` is the number of ranks the process group saw (all_reduce).
+
+At world > 1, after the headline timing, a second leg runs BASELINE config 5: the 4-stage
+decimating FIR chain domain-partitioned across the ranks (G = 2: stages {1,2}|{3,4};
+G = 4: one stage per rank; 8 ranks = 2 time shards x 4) over domain_adapter_remote, RCCL
+forced when every rank has its own GPU. Its rate, transports and tail parity go into the
+`c5_pipeline` field; a failure there is reported, not fatal to the headline.
 
 Prints ONE JSON line (rank 0) with the roofline of the FIR kernel (HIP events around each
 launch on the partition stream, algorithmic 16 B/sample) and the CPU baseline (the
@@ -21,6 +32,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -33,12 +46,13 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level para
 BYTES_PER_SAMPLE = 16  # algorithmic: read x (8 B) + write y (8 B) per output sample
 FLOP_PER_SAMPLE = 508  # 127 taps x 2 (re, im) x FMA
 METRIC = "MSamples/s through 127-tap fir_filter_ccf flowgraph; % HBM roofline at 1/8 GPU"
+C5_HALO = 1904  # >= 126*(1+2+4+8) = 1890 input samples, a multiple of the total decimation 16
 
 
-def firwin127():
+def firwin(ntaps, cutoff):
     import scipy.signal as ss
 
-    return ss.firwin(127, 0.2).astype(np.float32)  # C3 taps (tests/golden/fir127.npz)
+    return ss.firwin(ntaps, cutoff).astype(np.float32)  # C3: (127, 0.2); C5: (127, 0.45)
 
 
 def cpu_model():
@@ -52,6 +66,12 @@ def cpu_model():
     return "unknown"
 
 
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
 def load_pmc_traffic(kernel, samples_per_launch):
     """HBM bytes per launch from the committed PMC summary (profiles/pmc_fir.json, produced
     by tools/pmc_summary.py from separate rocprofv3 --pmc passes, gfx950 FETCH_SIZE x2
@@ -61,9 +81,115 @@ def load_pmc_traffic(kernel, samples_per_launch):
     try:
         with open(p) as f:
             d = json.load(f)
-        return float(d[kernel]["hbm_bytes_per_sample"]) * samples_per_launch
+        return float(d[kernel]["hbm_bytes_per_sample"]) * samples_per_launch, d.get("_source", "profiles/pmc_fir.json")
     except (OSError, KeyError, ValueError, TypeError):
-        return None
+        return None, None
+
+
+def spawn_ranks(n):
+    """Start n ranks of this script (never exec: the children are fresh processes) and
+    relay their output; returns the exit code. Nothing in this process touches the GPU."""
+    env = dict(os.environ, WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()),
+               LOCAL_WORLD_SIZE=str(n), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    procs = []
+    for r in range(n):
+        e = dict(env, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=e))
+    rc = 0
+    failed_at = None
+    while procs:
+        for p in list(procs):
+            c = p.poll()
+            if c is None:
+                continue
+            procs.remove(p)
+            if c != 0 and rc == 0:
+                rc, failed_at = c, time.time()
+        if rc != 0 and procs and time.time() - failed_at > 30:
+            for p in procs:  # peers left waiting in a collective on the failed rank
+                p.kill()
+        time.sleep(0.05)
+    return rc
+
+
+def c5_layout(world):
+    """(stage groups G, time shards) for `world` ranks: G = 4 when it divides world, else 2,
+    else 1 (G=2 {1,2}|{3,4}; G=4 one stage per GPU; G=8 2 shards x 4)."""
+    for g in (4, 2, 1):
+        if world % g == 0:
+            return g, world // g
+    return 1, world
+
+
+def run_c5(a, dist, backend, rank, world, device, torch, orc, nsr):
+    """BASELINE config 5 over the ranks (see the module docstring)."""
+    G, shards = c5_layout(world)
+    group, shard = rank % G, rank // G
+    n = 1 << a.c5_log2n
+    taps = firwin(127, 0.45)
+    first = max(0, shard * n - C5_HALO)  # shards > 0 start with the chain's halo (discarded)
+    n_in = shard * n + n - first
+    port = torch.tensor([free_port() if rank == 0 else 0], dtype=torch.int64,
+                        device="cuda" if backend == "nccl" else "cpu")
+    if dist is not None:
+        dist.broadcast(port, 0)
+    base_port = int(port.item()) + 1 + 8 * shard
+    own_gpus = torch.cuda.device_count() >= world
+    transport = a.c5_transport if a.c5_transport != "default" else ("rccl" if own_gpus and world > 1 else "auto")
+    res = {"layout": "G=%d stage groups x %d time shards" % (G, shards), "stages": "4 x fir_filter_ccf(firwin(127,0.45), D=2)",
+           "samples_per_shard": n, "transport_requested": transport}
+    pipe = None
+    try:
+        pipe = nsr.C5Pipeline(taps, n_in, group=group, n_groups=G, device=device, first_index=first,
+                              base_port=base_port, transport=transport, buf_bytes=a.c5_buf_mib << 20)
+        for _ in range(a.c5_warmup):
+            pipe.run()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.c5_steps):
+            pipe.run()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        ok, err = True, 0.0
+        if pipe.last:
+            m = 4096
+            J = (first + n_in) // 16  # one past the last output (global output index)
+            lo = 16 * (J - m) - C5_HALO
+            y_ref = orc.synth(16 * m + C5_HALO, lo)
+            for _ in range(4):
+                y_ref = orc.fir_ccf(y_ref, taps, decim=2)
+            ok, err, _ = orc.tol_ok(pipe.tail(m), y_ref[-m:])
+        tr = pipe.transport()
+        status = 0.0
+    except Exception as e:  # reported, not fatal: the headline is already measured
+        el, ok, err, tr, status = 0.0, False, 0.0, "", 1.0
+        res["error_rank%d" % rank] = str(e)[:300]
+    if dist is not None:
+        dev_kind = "cuda" if backend == "nccl" else "cpu"
+        v = torch.tensor([el, 0.0 if ok else 1.0, err, status], dtype=torch.float64, device=dev_kind)
+        dist.all_reduce(v, op=dist.ReduceOp.MAX)
+        el, ok, err, status = float(v[0]), v[1].item() == 0.0, float(v[2]), float(v[3])
+        trs = [None] * world
+        errs = [None] * world
+        dist.all_gather_object(trs, tr)
+        dist.all_gather_object(errs, res.get("error_rank%d" % rank))
+        res["transports"] = {str(r): t for r, t in enumerate(trs) if t}
+        for r, e in enumerate(errs):
+            if e:
+                res["error_rank%d" % r] = e
+    else:
+        res["transports"] = {"0": tr}
+    if pipe is not None:
+        pipe.close()
+    res["ok"] = status == 0.0
+    if status == 0.0:
+        res.update({"steps": a.c5_steps, "warmup": a.c5_warmup, "ms_per_step": round(el / a.c5_steps * 1e3, 3),
+                    "value": round(shards * n * a.c5_steps / el / 1e6, 1), "unit": "MSamples/s (input, whole job)",
+                    "parity": {"check": "last 4096 outputs of every shard vs the oracle's 4-stage chain",
+                               "max_abs_err": err, "ok": bool(ok)}})
+    return res
 
 
 def main():
@@ -71,24 +197,41 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--min-warmup-s", type=float, default=1.0,
+                    help="keep warming up (untimed runs) until this long has passed: clocks settle")
     ap.add_argument("--log2n", type=int, default=28)
     ap.add_argument("--algo", default="auto", choices=["auto", "mfma", "mfma_x3", "mfma16", "direct"])
     ap.add_argument("--out-buf-mib", type=int, default=2048, help="FIR output hip_buffer (default: one launch per 2^28-sample step)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-log2n", type=int, default=28, help="CPU baseline sample (default: the full stream)")
+    ap.add_argument("--c5", choices=["auto", "on", "off"], default="auto", help="C5 pipeline leg (auto: at world > 1)")
+    ap.add_argument("--c5-log2n", type=int, default=26)
+    ap.add_argument("--c5-steps", type=int, default=5)
+    ap.add_argument("--c5-warmup", type=int, default=2)
+    ap.add_argument("--c5-buf-mib", type=int, default=64)
+    ap.add_argument("--c5-transport", default="default", choices=["default", "auto", "rccl", "socket"])
+    ap.add_argument("--rank-check", action="store_true", help=argparse.SUPPRESS)  # launcher test (CPU, gloo)
     a = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(spawn_ranks(a.gpus))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        sys.exit("bench.py: --gpus %d but WORLD_SIZE=%d" % (a.gpus, world))
 
     import torch
 
-    # one process per GPU; more ranks than GPUs (a rehearsal on a 1-GPU box) share devices
-    device = local % max(torch.cuda.device_count(), 1)
-    torch.cuda.set_device(device)
-    dist = None
     backend = os.environ.get("NSH_BENCH_BACKEND", "nccl")  # nccl = RCCL; gloo only for rehearsals
+    if a.rank_check:
+        backend = "gloo"
+    dist = None
+    device = 0
+    if not a.rank_check:
+        # one process per GPU; more ranks than GPUs (a rehearsal on a 1-GPU box) share devices
+        device = local % max(torch.cuda.device_count(), 1)
+        torch.cuda.set_device(device)
     if world > 1:
         import torch.distributed as dist
 
@@ -97,6 +240,18 @@ def main():
             dist.init_process_group(backend="nccl", device_id=torch.device("cuda", device))
         else:
             dist.init_process_group(backend=backend)
+    tdev = "cuda" if backend == "nccl" else "cpu"
+    ranks_seen = world
+    if dist is not None:
+        one = torch.ones(1, dtype=torch.int64, device=tdev)
+        dist.all_reduce(one)
+        ranks_seen = int(one.item())
+    if a.rank_check:
+        if rank == 0:
+            print(json.dumps({"n_gpus": ranks_seen, "world": world}), flush=True)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
 
     from newsched_amd import nsh, nsr
     from oracle import oracle as orc  # checker only: tail parity + CPU-baseline inputs
@@ -104,7 +259,7 @@ def main():
     algo = {"auto": nsh.FIR_AUTO, "mfma": nsh.FIR_MFMA, "mfma16": nsh.FIR_MFMA16, "mfma_x3": nsh.FIR_MFMA_BF16X3,
             "direct": nsh.FIR_DIRECT}[a.algo]
     n = 1 << a.log2n
-    taps = firwin127()
+    taps = firwin(127, 0.2)
     first = rank * n  # this rank's time shard
     fb = nsr.FirBench(taps, n, device=device, algo=algo, first_index=first, out_buf_bytes=a.out_buf_mib << 20)
 
@@ -113,8 +268,14 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    for _ in range(a.warmup):
+    # Warm-up: at least --warmup runs and at least --min-warmup-s seconds of them (the
+    # chip's clocks take ~20 back-to-back runs to settle), untimed.
+    tw = time.perf_counter()
+    warm = 0
+    while warm < a.warmup or time.perf_counter() - tw < a.min_warmup_s:
         fb.run()
+        warm += 1
+    warm_s = time.perf_counter() - tw
     barrier()
     kms = 0.0
     samples = 0
@@ -128,7 +289,7 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=tdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     st = fb.stats()
@@ -148,7 +309,7 @@ def main():
     y_ref = orc.fir_ccf(xw[taps.size - 1:], taps, hist=xw[: taps.size - 1])
     ok, err, scale = orc.tol_ok(y, y_ref)
     if dist is not None:  # every rank's shard tail must pass; report the worst error
-        r = torch.tensor([0.0 if ok else 1.0, err], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
+        r = torch.tensor([0.0 if ok else 1.0, err], dtype=torch.float64, device=tdev)
         dist.all_reduce(r, op=dist.ReduceOp.MAX)
         ok, err = r[0].item() == 0.0, float(r[1].item())
 
@@ -157,7 +318,7 @@ def main():
         "metric": METRIC,
         "value": round(value, 1),
         "unit": "MSamples/s",
-        "n_gpus": world,
+        "n_gpus": ranks_seen,
         "steps": a.steps,
         "warmup": a.warmup,
         "ms_per_step": round(elapsed / a.steps * 1e3, 4),
@@ -177,6 +338,7 @@ def main():
             "samples_per_launch": int(per_launch_samples),
             "parallelism": "time-sharded replicas x%d (126-sample halo regenerated, no collective)" % world,
         },
+        "warmup_done": {"runs": warm, "seconds": round(warm_s, 3), "min_seconds": a.min_warmup_s},
         "roofline": {
             "bound": "hbm",
             "achieved": round(achieved, 1),
@@ -192,9 +354,15 @@ def main():
         "parity": {"check": "last 4096 outputs of the last step vs oracle (double accumulation), every rank",
                    "max_abs_err": err, "scale": scale, "ok": bool(ok)},
     }
-    tr = load_pmc_traffic(kernel, per_launch_samples)
+    tr, src = load_pmc_traffic(kernel, per_launch_samples)
     if tr is not None:
         out["roofline"]["traffic"] = int(tr)
+        out["roofline"]["traffic_source"] = ("HBM B/sample from separate rocprofv3 --pmc passes (%s), scaled to this "
+                                             "launch size; not measured in this run" % src)
+    fb.close()
+
+    if a.c5 == "on" or (a.c5 == "auto" and world > 1):
+        out["c5_pipeline"] = run_c5(a, dist, backend, rank, world, device, torch, orc, nsr)
 
     if rank == 0 and world == 1 and not a.no_cpu:
         ncpu = 1 << a.cpu_log2n
@@ -213,7 +381,6 @@ def main():
         dist.barrier()
     if rank == 0:
         print(json.dumps(out), flush=True)
-    fb.close()
     if dist is not None:
         dist.destroy_process_group()
 

@@ -49,6 +49,9 @@ int nsh_get_device_count(int* count);
 int nsh_set_device(int dev);
 int nsh_device_info(int dev, int* n_cu, int* clock_khz, size_t* hbm_bytes, char* arch, int arch_len);
 int nsh_device_sync(void);
+/* PCI bus id of `dev` ("dddd:bb:dd.f"): identifies a physical GPU across processes whose
+ * device ordinals differ (per-rank HIP_VISIBLE_DEVICES makes every rank device 0). */
+int nsh_device_pci_id(int dev, char* buf, int len);
 
 /* ---- streams and events (opaque hipStream_t / hipEvent_t) ---------------------- */
 int nsh_stream_create(int dev, void** stream);

@@ -40,6 +40,26 @@ const char* nsr_fir_bench_kernel(void* handle);
 int nsr_fir_bench_tail(void* handle, int64_t count, float* out_host);
 int nsr_fir_bench_destroy(void* handle);
 
+/* C5 pipeline leg (BASELINE config 5): synth_source(first_index, n) -> 4 x
+ * hip::fir_filter_ccf(taps, decim) -> null_sink, domain-partitioned over n_groups processes
+ * (n_groups in {1, 2, 4}; group g runs stages [4g/G, 4(g+1)/G) in a scheduler_hip domain on
+ * `dev`, plus the source (g = 0) / the sink (g = G-1); the other groups' domains are
+ * remote_domain placeholders). Every process of one pipeline calls this with the same
+ * arguments except `group` and `dev`. Crossing i listens on 127.0.0.1:base_port+i.
+ * transport: "auto" (RCCL when both rings are device memory on GPUs with different PCI bus
+ * ids, else the TCP socket, staged through pinned memory) | "rccl" (fail otherwise) |
+ * "socket". buf_bytes: scheduler_hip fixed_buf_size. n must be a multiple of decim^4.
+ * Reference: graph_utils.cpp:11-205 (partition), domain_adapter_direct.hpp:236-257. */
+int nsr_c5_create(int group, int n_groups, int dev, const float* taps, int ntaps, int decim, int64_t n,
+                  uint64_t first_index, uint64_t seed, int base_port, const char* transport, size_t buf_bytes,
+                  void** handle);
+int nsr_c5_run(void* handle);
+/* The transports this process's crossings negotiated, e.g. "send1:rccl,recv0:rccl". */
+int nsr_c5_transport(void* handle, char* buf, int len);
+/* The last `count` outputs of the last run -> host (only the process of group n_groups-1). */
+int nsr_c5_tail(void* handle, int64_t count, float* out_host);
+int nsr_c5_destroy(void* handle);
+
 /* CPU baseline: the reference scheduler_mt CPU path restated -- thread per block,
  * vmcircbuf edges of 2*fixed_buf_size bytes (reference default 32768):
  *   vector_source(x[0..nx), repeat) -> head(n) -> blocks::fir_filter_ccf -> null_sink

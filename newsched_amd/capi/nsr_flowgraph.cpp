@@ -9,6 +9,8 @@
 #include <gnuradio/blocklib/blocks/null_sink.hpp>
 #include <gnuradio/blocklib/blocks/vector_source.hpp>
 #include <gnuradio/blocklib/hip/fir_filter_ccf.hpp>
+#include <gnuradio/blocklib/hip/synth_source.hpp>
+#include <gnuradio/domain_adapter_remote.hpp>
 #include <gnuradio/flowgraph.hpp>
 #include <gnuradio/hip_buffer.hpp>
 #include <gnuradio/hip_context.hpp>
@@ -53,6 +55,29 @@ gr_complex synth_at(uint64_t i, uint64_t seed)
     return gr_complex((float)(int)(splitmix64(seed ^ g) >> 40) * (1.0f / 8388608.0f) - 1.0f,
                       (float)(int)(splitmix64(seed ^ (g + 1)) >> 40) * (1.0f / 8388608.0f) - 1.0f);
 }
+
+// Tail of a device ring's last `count` written items -> host.
+void ring_tail(const std::shared_ptr<hip_buffer>& r, int dev, int64_t count, float* out_host)
+{
+    if (count <= 0 || (size_t)count > r->capacity() / 2 || (uint64_t)count > r->total_written())
+        throw std::invalid_argument("tail: bad count");
+    const uint64_t start = r->total_written() - (uint64_t)count;
+    const char* src = (const char*)r->device_base() + (start % r->capacity()) * r->item_size();
+    void* s = nullptr;
+    hip::check(nsh_stream_create(dev, &s), "nsr: stream");
+    const int rc = nsh_memcpy_async(out_host, src, (size_t)count * r->item_size(), NSH_D2H, s);
+    const int rc2 = rc == 0 ? nsh_stream_sync(s) : rc;
+    nsh_stream_destroy(s);
+    hip::check(rc2, "nsr: tail copy");
+}
+
+struct c5_pipeline {
+    flowgraph::sptr fg;
+    std::shared_ptr<domain_adapter_remote_conf> da;
+    std::vector<hip::fir_filter_ccf::sptr> stages;
+    std::shared_ptr<hip_buffer> out_ring; // last group only
+    int dev = 0;
+};
 
 struct fir_bench {
     flowgraph::sptr fg;
@@ -145,22 +170,112 @@ int nsr_fir_bench_tail(void* handle, int64_t count, float* out_host)
 {
     return guarded([&] {
         auto b = static_cast<fir_bench*>(handle);
-        auto r = b->out_ring;
-        if (count <= 0 || (size_t)count > r->capacity() / 2) throw std::invalid_argument("nsr_fir_bench_tail: bad count");
-        const uint64_t end = r->total_written();
-        const uint64_t start = end - (uint64_t)count;
-        const char* src = (const char*)r->device_base() + (start % r->capacity()) * r->item_size();
-        void* s = nullptr;
-        hip::check(nsh_stream_create(b->dev, &s), "nsr: stream");
-        hip::check(nsh_memcpy_async(out_host, src, (size_t)count * r->item_size(), NSH_D2H, s), "nsr: tail copy");
-        hip::check(nsh_stream_sync(s), "nsr: tail copy");
-        nsh_stream_destroy(s);
+        ring_tail(b->out_ring, b->dev, count, out_host);
     });
 }
 
 int nsr_fir_bench_destroy(void* handle)
 {
     return guarded([&] { delete static_cast<fir_bench*>(handle); });
+}
+
+int nsr_c5_create(int group, int n_groups, int dev, const float* taps, int ntaps, int decim, int64_t n,
+                  uint64_t first_index, uint64_t seed, int base_port, const char* transport, size_t buf_bytes,
+                  void** handle)
+{
+    return guarded([&] {
+        const int n_stages = 4;
+        if (n_groups < 1 || n_stages % n_groups || group < 0 || group >= n_groups)
+            throw std::invalid_argument("nsr_c5_create: n_groups must divide 4 and 0 <= group < n_groups");
+        int64_t total_decim = 1;
+        for (int i = 0; i < n_stages; ++i) total_decim *= decim;
+        if (n <= 0 || n % total_decim) throw std::invalid_argument("nsr_c5_create: n must be a multiple of decim^4");
+        auto b = std::make_unique<c5_pipeline>();
+        b->dev = dev;
+        const size_t isz = sizeof(gr_complex);
+        const std::vector<float> h(taps, taps + ntaps);
+        auto src = hip::synth_source::make(first_index, (uint64_t)n, seed);
+        for (int i = 0; i < n_stages; ++i) b->stages.push_back(hip::fir_filter_ccf::make(h, decim));
+        auto snk = blocks::null_sink::make(isz);
+        b->fg = flowgraph::make();
+        b->fg->connect(src, 0, b->stages[0], 0);
+        for (int i = 1; i < n_stages; ++i) b->fg->connect(b->stages[i - 1], 0, b->stages[i], 0);
+        b->fg->connect(b->stages[n_stages - 1], 0, snk, 0);
+
+        // SPMD: every process builds the same graph and domain list; the domains of the
+        // other groups are remote_domain placeholders (domain_adapter_remote.hpp)
+        const int per = n_stages / n_groups;
+        std::vector<scheduler_sptr> scheds;
+        domain_conf_vec dc;
+        remote_edge_options o;
+        o.base_port = base_port;
+        o.transport = transport && *transport ? transport : "auto";
+        o.device = dev;
+        o.timeout_s = 120;
+        b->da = domain_adapter_remote_conf::make(o);
+        for (int g = 0; g < n_groups; ++g) {
+            scheduler_sptr sc;
+            if (g == group)
+                sc = schedulers::scheduler_hip::make("c5g" + std::to_string(g), dev, buf_bytes);
+            else
+                sc = remote_domain::make(g, "c5g" + std::to_string(g));
+            scheds.push_back(sc);
+            std::vector<node_sptr> blks;
+            if (g == 0) blks.push_back(src);
+            for (int i = g * per; i < (g + 1) * per; ++i) blks.push_back(b->stages[i]);
+            if (g == n_groups - 1) blks.push_back(snk);
+            dc.emplace_back(sc, blks, b->da);
+        }
+        b->fg->set_wait_spin_us(5000);
+        if (n_groups == 1) {
+            b->fg->set_scheduler(scheds[0]);
+            b->fg->validate();
+        } else {
+            b->fg->set_schedulers(scheds);
+            b->fg->partition(dc);
+        }
+        if (group == n_groups - 1) {
+            auto sh = std::dynamic_pointer_cast<schedulers::scheduler_hip>(scheds[group]);
+            b->out_ring = std::dynamic_pointer_cast<hip_buffer>(sh->buffers()->get_input_buffer(snk->input_stream_ports()[0]));
+            if (!b->out_ring) throw std::runtime_error("nsr_c5_create: the sink edge is not a hip_buffer");
+        }
+        *handle = b.release();
+    });
+}
+
+int nsr_c5_run(void* handle)
+{
+    return guarded([&] { static_cast<c5_pipeline*>(handle)->fg->run(); });
+}
+
+int nsr_c5_transport(void* handle, char* buf, int len)
+{
+    return guarded([&] {
+        auto b = static_cast<c5_pipeline*>(handle);
+        std::string t;
+        for (auto& a : b->da->adapters()) {
+            if (!t.empty()) t += ",";
+            t += (a->role() == remote_role::SEND ? "send" : "recv") + std::to_string(a->crossing()) + ":" +
+                 a->transport_kind();
+        }
+        if (len <= 0) throw std::invalid_argument("nsr_c5_transport: len");
+        std::strncpy(buf, t.c_str(), (size_t)len - 1);
+        buf[len - 1] = 0;
+    });
+}
+
+int nsr_c5_tail(void* handle, int64_t count, float* out_host)
+{
+    return guarded([&] {
+        auto b = static_cast<c5_pipeline*>(handle);
+        if (!b->out_ring) throw std::invalid_argument("nsr_c5_tail: this process does not own the sink");
+        ring_tail(b->out_ring, b->dev, count, out_host);
+    });
+}
+
+int nsr_c5_destroy(void* handle)
+{
+    return guarded([&] { delete static_cast<c5_pipeline*>(handle); });
 }
 
 int nsr_cpu_fir_run(const float* taps, int ntaps, const float* x, int64_t nx, int64_t n, size_t fixed_buf_size,

@@ -50,6 +50,13 @@ int nsh_device_info(int dev, int* n_cu, int* clock_khz, size_t* hbm_bytes, char*
     return 0;
 }
 
+int nsh_device_pci_id(int dev, char* buf, int len)
+{
+    if (!buf || len < 13) return ::nsh::fail(hipErrorInvalidValue, "nsh_device_pci_id: buffer too small");
+    NSH_CK(hipDeviceGetPCIBusId(buf, len, dev));
+    return 0;
+}
+
 int nsh_device_sync(void)
 {
     NSH_CK(hipDeviceSynchronize());

@@ -28,6 +28,7 @@ SIGNATURES = {
     "nsh_get_device_count": (_i, [C.POINTER(_i)]),
     "nsh_set_device": (_i, [_i]),
     "nsh_device_info": (_i, [_i, C.POINTER(_i), C.POINTER(_i), C.POINTER(_sz), C.c_char_p, _i]),
+    "nsh_device_pci_id": (_i, [_i, C.c_char_p, _i]),
     "nsh_device_sync": (_i, []),
     "nsh_stream_create": (_i, [_i, C.POINTER(_vp)]),
     "nsh_stream_destroy": (_i, [_vp]),

@@ -23,6 +23,12 @@ SIGNATURES = {
     "nsr_fir_bench_kernel": (C.c_char_p, [_vp]),
     "nsr_fir_bench_tail": (_i, [_vp, _i64, C.POINTER(C.c_float)]),
     "nsr_fir_bench_destroy": (_i, [_vp]),
+    "nsr_c5_create": (_i, [_i, _i, _i, C.POINTER(C.c_float), _i, _i, _i64, _u64, _u64, _i, C.c_char_p, _sz,
+                           C.POINTER(_vp)]),
+    "nsr_c5_run": (_i, [_vp]),
+    "nsr_c5_transport": (_i, [_vp, C.c_char_p, _i]),
+    "nsr_c5_tail": (_i, [_vp, _i64, C.POINTER(C.c_float)]),
+    "nsr_c5_destroy": (_i, [_vp]),
     "nsr_cpu_fir_run": (_i, [C.POINTER(C.c_float), _i, C.POINTER(C.c_float), _i64, _i64, _sz, C.POINTER(_d)]),
 }
 
@@ -81,6 +87,43 @@ class FirBench:
     def close(self):
         if getattr(self, "_h", None):
             lib().nsr_fir_bench_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class C5Pipeline:
+    """One process's share of the C5 decimating pipeline (see nsr_c5_create)."""
+
+    def __init__(self, taps, n, group=0, n_groups=1, device=0, decim=2, first_index=0, seed=0x6E736368,
+                 base_port=29700, transport="auto", buf_bytes=64 << 20):
+        t = np.ascontiguousarray(np.asarray(taps, np.float32))
+        h = C.c_void_p()
+        check(lib().nsr_c5_create(group, n_groups, device, _f32p(t), int(t.size), decim, int(n), first_index, seed,
+                                  base_port, transport.encode(), buf_bytes, C.byref(h)), "nsr_c5_create")
+        self._h = h
+        self.last = group == n_groups - 1
+
+    def run(self):
+        check(lib().nsr_c5_run(self._h), "nsr_c5_run")
+
+    def transport(self):
+        buf = C.create_string_buffer(512)
+        check(lib().nsr_c5_transport(self._h, buf, 512), "nsr_c5_transport")
+        return buf.value.decode()
+
+    def tail(self, count):
+        out = np.empty(count, np.complex64)
+        check(lib().nsr_c5_tail(self._h, count, _f32p(out.view(np.float32))), "nsr_c5_tail")
+        return out
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().nsr_c5_destroy(self._h)
             self._h = None
 
     def __del__(self):

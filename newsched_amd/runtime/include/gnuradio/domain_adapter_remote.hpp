@@ -35,6 +35,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <vector>
 
 namespace gr {
 
@@ -154,9 +155,19 @@ public:
     domain_adapter_sptr make_remote_adapter(port_sptr local_port, bool local_is_upstream, int crossing,
                                             const std::string& name) override;
     const remote_edge_options& options() const { return _opt; }
+    // The adapters this conf instantiated in this process (partition order), e.g. to
+    // report the transport each crossing negotiated.
+    std::vector<std::shared_ptr<domain_adapter_remote>> adapters() const
+    {
+        std::vector<std::shared_ptr<domain_adapter_remote>> v;
+        for (auto& w : _made)
+            if (auto a = w.lock()) v.push_back(a);
+        return v;
+    }
 
 private:
     remote_edge_options _opt;
+    std::vector<std::weak_ptr<domain_adapter_remote>> _made;
 };
 
 } // namespace gr

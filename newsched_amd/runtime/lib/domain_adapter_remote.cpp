@@ -39,6 +39,8 @@ struct hello {
     int32_t want;       // 0 auto, 1 rccl, 2 socket (sender's request)
     int32_t chosen;     // receiver's answer: 1 rccl, 2 socket
     int64_t max_chunk;  // receiver's answer: items per message
+    char pci[32];       // PCI bus id of `device` ("" for host rings): ordinals differ per
+                        // process under per-rank HIP_VISIBLE_DEVICES, bus ids do not
 };
 using clk = std::chrono::steady_clock;
 double since(clk::time_point t0) { return std::chrono::duration<double>(clk::now() - t0).count(); }
@@ -472,6 +474,7 @@ void domain_adapter_remote::buffer_ready()
         mine.is_device = dev_side ? 1 : 0;
         mine.device = _device;
         mine.want = _opt.transport == "rccl" ? 1 : _opt.transport == "socket" ? 2 : 0;
+        if (dev_side && _device >= 0) hip::check(nsh_device_pci_id(_device, mine.pci, (int)sizeof(mine.pci)), "remote edge: pci id");
         hello peer{};
         if (_role == remote_role::SEND) {
             _ch = connect_retry(_opt.host, _opt.base_port + _crossing, _opt.timeout_s, _closing);
@@ -498,7 +501,9 @@ void domain_adapter_remote::buffer_ready()
             buffer_info_t wi{};
             _buffer->write_info(wi);
             mine.max_chunk = wi.n_items;
-            const bool rccl_ok = dev_side && peer.is_device && peer.device != _device;
+            peer.pci[sizeof(peer.pci) - 1] = 0;
+            const bool rccl_ok = dev_side && peer.is_device && mine.pci[0] && peer.pci[0] &&
+                                 std::strncmp(peer.pci, mine.pci, sizeof(mine.pci)) != 0;
             const int want = peer.want ? peer.want : mine.want;
             if (want == 1 && !rccl_ok)
                 throw std::runtime_error("remote edge: rccl transport needs device rings on two different GPUs");
@@ -716,6 +721,7 @@ domain_adapter_sptr domain_adapter_remote_conf::make_remote_adapter(port_sptr lo
     auto a = domain_adapter_remote::make(local_is_upstream ? remote_role::SEND : remote_role::RECV, local_port,
                                          crossing, _opt);
     if (!name.empty()) a->set_alias(name);
+    _made.push_back(a);
     return a;
 }
 

@@ -12,7 +12,6 @@ import pytest
 
 from tests.conftest import ROOT
 
-pytestmark = pytest.mark.gpu
 
 ARGS = ["--steps", "3", "--warmup", "1", "--log2n", "22", "--out-buf-mib", "64", "--no-cpu"]
 
@@ -23,6 +22,34 @@ def _json_line(stdout):
     return json.loads(lines[0])
 
 
+def test_launcher_spawns_ranks_cpu():
+    """`bench.py --gpus 2` without torchrun starts two ranks itself (the driver's form);
+    n_gpus is what the process group counted (gloo here, no GPU touched)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--rank-check"], cwd=ROOT, capture_output=True,
+                         text=True, timeout=120, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    assert _json_line(out.stdout) == {"n_gpus": 2, "world": 2}
+
+
+def test_launcher_rejects_mismatched_world():
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--rank-check"], cwd=ROOT, capture_output=True,
+                         text=True, timeout=120, env=env)
+    assert out.returncode != 0 and "WORLD_SIZE" in out.stderr
+
+
+def test_c5_layout():
+    import bench
+
+    assert bench.c5_layout(2) == (2, 1)
+    assert bench.c5_layout(4) == (4, 1)
+    assert bench.c5_layout(8) == (4, 2)
+    assert bench.c5_layout(1) == (1, 1)
+    assert bench.c5_layout(6) == (2, 3)
+
+
+@pytest.mark.gpu
 def test_bench_one_gpu(torch_cuda):
     out = subprocess.run([sys.executable, "bench.py"] + ARGS, cwd=ROOT, capture_output=True, text=True, timeout=240)
     assert out.returncode == 0, out.stderr[-3000:]
@@ -36,6 +63,7 @@ def test_bench_one_gpu(torch_cuda):
     assert d["config"]["workload"].startswith("C3")
 
 
+@pytest.mark.gpu
 def test_bench_two_ranks_rehearsal(torch_cuda):
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -49,3 +77,47 @@ def test_bench_two_ranks_rehearsal(torch_cuda):
     assert d["n_gpus"] == 2
     assert d["parity"]["ok"], d["parity"]  # both shards' tails (rank 1 starts at sample 2^22)
     assert "2" in d["config"]["parallelism"]
+
+
+@pytest.mark.gpu
+def test_bench_spawns_ranks_and_c5_leg(torch_cuda):
+    """The driver's N>1 form without torchrun: bench.py starts the ranks itself; both shards'
+    tails pass; the C5 pipeline leg ({1,2}|{3,4} over domain_adapter_remote; two ranks on one
+    GPU negotiate the staged socket transport, RCCL needs two GPUs) is parity-green."""
+    env = dict(os.environ, NSH_BENCH_BACKEND="gloo")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    out = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--c5-log2n", "20"] + ARGS, cwd=ROOT,
+                         capture_output=True, text=True, timeout=300, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    d = _json_line(out.stdout)
+    assert d["n_gpus"] == 2 and d["parity"]["ok"], d
+    c5 = d["c5_pipeline"]
+    assert c5["ok"] and c5["parity"]["ok"], c5
+    assert c5["value"] > 0
+    assert "socket" in c5["transports"]["0"] and "socket" in c5["transports"]["1"], c5
+
+
+@pytest.mark.gpu
+def test_bench_c5_single_gpu(torch_cuda):
+    """C5 at G = 1 (all four stages in one scheduler_hip domain) through the same leg."""
+    out = subprocess.run([sys.executable, "bench.py", "--c5", "on", "--c5-log2n", "22"] + ARGS, cwd=ROOT,
+                         capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-3000:]
+    c5 = _json_line(out.stdout)["c5_pipeline"]
+    assert c5["ok"] and c5["parity"]["ok"], c5
+
+
+@pytest.mark.gpu
+def test_bench_c5_rccl_two_gpus(torch_cuda):
+    """The RCCL edge transport (domain_adapter_remote rccl_transport) end to end: needs two
+    GPUs, so it is skipped on the 1-GPU test box and runs on the first multi-GPU lease."""
+    if torch_cuda.cuda.device_count() < 2:
+        pytest.skip("RCCL edges need two GPUs")
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "NSH_BENCH_BACKEND")}
+    out = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--c5-log2n", "22", "--c5-transport", "rccl"]
+                         + ARGS, cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    c5 = _json_line(out.stdout)["c5_pipeline"]
+    assert c5["ok"] and c5["parity"]["ok"], c5
+    assert all("rccl" in t for t in c5["transports"].values()), c5
