@@ -211,6 +211,7 @@ int nsh_fir_plan_destroy(void* plan)
     if (p->frag_dev) (void)hipFree(p->frag_dev);
     if (p->frag16_dev) (void)hipFree(p->frag16_dev);
     if (p->frag8_dev) (void)hipFree(p->frag8_dev);
+    if (p->frag12_dev) (void)hipFree(p->frag12_dev);
     if (p->fragd_dev) (void)hipFree(p->fragd_dev);
     if (p->fragd8_dev) (void)hipFree(p->fragd8_dev);
     delete p;

@@ -1389,6 +1389,204 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma9(const float2* __restrict__
     if (ch <= c_last) step(vb, vc, va, ch);
 }
 
+// ---- k_fir_mfma12: one chunk per workgroup, in address order per XCD -------------------------
+// k_fir_mfma9's numerics (fp16x2 split at a per-chunk power-of-two scale, three products, the
+// fp32 direct form for chunks that need it) with the access shape that copies at the HBM
+// ceiling (tools/probe/shape_probe.hip, profiles/r02b_shape_probe28_runs.log): short-lived
+// workgroups, each filtering ONE 2048-sample chunk, dispatched in address order with the
+// chunk index remapped so that XCD x (workgroup ids x, x+8, ...) walks its own contiguous
+// eighth of the stream -- 6.55 TB/s for the copy of that shape vs 5.6-5.7 TB/s for v9's
+// contiguous per-workgroup ranges. Each workgroup re-reads its 32(Q-1)-sample halo (the
+// previous chunk's tail, just read by the previous workgroup of the same XCD: an L2 hit) with
+// the default cache policy; the probe measured no cost for it.
+// Taps: v9 kept 2 x 2Q B fragments in VGPRs (80 registers, 20 KiB per wave from L2 at every
+// workgroup start -- in the probe, 20 KiB of such loads per chunk cost 10-40 %). Here the
+// fragments come from LDS: the scaled taps reversed, R[m] = h[32Q - 1 - m], hi and lo fp16
+// planes, stored as 8 copies shifted by 0..7 elements, so the 8 consecutive taps a lane needs
+// for one k-step (R[m0 .. m0 + 8)) are one aligned ds_read_b128 from copy m0 mod 8. Copy pitch
+// = 32 mod 64 bytes: the 16 lanes of a read group hit 16 distinct 16-B slots. The image
+// (2 x 8 x (32Q + 24) fp16, 6 KiB at Q = 5) is prepared on the host and loaded per workgroup
+// (L1/L2 hits: every workgroup reads the same bytes).
+// Scale and exact-path test cover the chunk and its halo. Results match v9 to within the
+// split's rounding (v9's scale also covered the whole previous chunk), not bit for bit.
+template <int Q>
+struct geom12 {
+    static constexpr int NT = 256;
+    static constexpr int CHUNK = 2048;
+    static constexpr int H = 32 * (Q - 1);
+    static constexpr int HP = H / 2;
+    static constexpr int NB = (CHUNK + H) / 32;
+    static constexpr int PLANE = (NB * 80 + 255) / 256 * 256;
+    static constexpr int BUF = 4 * PLANE;
+    static constexpr int TW = 32 * Q + 24;                           // fp16 per shifted copy
+    static constexpr int COPY = ((2 * TW + 31) / 64) * 64 + 32;      // bytes, = 32 mod 64, >= 2 TW
+    static constexpr int TAPS = 2 * 8 * COPY;                        // [plane][shift] copies
+    static constexpr int IMG_UNITS = 2 * 8 * TW / 8;                 // 16-B units of the global image
+    static constexpr int SLOTS = BUF + TAPS;                         // u32 max[4], mnz[4]
+    static constexpr int LDS = SLOTS + 32;
+    static_assert(COPY >= 2 * TW && COPY % 64 == 32, "copy pitch");
+    static_assert((HP + 4 * NT) * 16 <= BUF, "a raw fp32 chunk + halo fits the plane buffer");
+    static_assert(HP <= NT, "halo pairs: one per thread");
+};
+
+template <int Q, int CPW>
+__global__ __launch_bounds__(256) void k_fir_mfma12(const float2* __restrict__ in,
+                                                    const float2* __restrict__ hist_in,
+                                                    float2* __restrict__ hist_out,
+                                                    float2* __restrict__ out,
+                                                    const uint4* __restrict__ timg, // [2][8][TW/8]
+                                                    const float* __restrict__ taps,
+                                                    int L,
+                                                    int sh,
+                                                    int64_t n_out,
+                                                    int64_t per_x)
+{
+    using G = geom12<Q>;
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    unsigned char* tl = lds + G::BUF;
+    unsigned* slot_max = reinterpret_cast<unsigned*>(lds + G::SLOTS);
+    unsigned* slot_mnz = slot_max + 4;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int64_t n_in = n_out;
+    const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
+    const int64_t c_first = ((int64_t)(blockIdx.x & 7) * per_x + (blockIdx.x >> 3)) * CPW;
+    if (c_first >= nchunks) return; // whole workgroup: before any barrier
+    const int n_my = (int)(nchunks - c_first < CPW ? nchunks - c_first : CPW);
+
+    // chunk ch -> registers (nontemporal) and its halo (default policy: the previous chunk's
+    // tail was just read by this or the previous workgroup of this XCD). Branch-free: the halo
+    // comes through one buffer resource, over `in` (ch > 0) or over hist_in (ch = 0; out-of-range
+    // lanes and a null history read zeros), so no wait sits between the loads.
+    auto load = [&](int64_t ch, float4 (&v)[4], float4& hv) {
+        load_chunk9(v, in, ch, n_in);
+        __amdgpu_buffer_rsrc_t hr;
+        int off;
+        if (ch > 0) {
+            hr = chunk_rsrc<G::H>(in + ch * G::CHUNK - G::H, 0, G::H);
+            off = 16 * tid;
+        } else {
+            hr = chunk_rsrc<1 << 20>(hist_in, 0, hist_in ? L - 1 : 0);
+            const int e = 2 * tid - G::H + (L - 1); // history element of the lane's first sample
+            off = e >= 0 ? 8 * e : 1 << 30;          // past num_records -> zeros
+        }
+        hv = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (tid < G::HP) {
+            const nsh::buf_f4 t = __builtin_bit_cast(nsh::buf_f4, __builtin_amdgcn_raw_buffer_load_b128(hr, off, 0, 0));
+            hv = make_float4(t.x, t.y, t.z, t.w);
+        }
+    };
+    float4 va[4], vb[4], ha, hb;
+    load(c_first, va, ha);
+    uint4 ti[2];
+    {   // the tap image (L1/L2 hits), both units per lane issued before any wait
+        const __amdgpu_buffer_rsrc_t tr = __builtin_amdgcn_make_buffer_rsrc((void*)timg, (short)0, G::IMG_UNITS * 16, 0x00020000);
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+            ti[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(tr, 16 * (tid + G::NT * k), 0, 0));
+    }
+    if (CPW > 1 && n_my > 1) load(c_first + 1, vb, hb);
+    {   // tap image -> LDS at the padded copy pitch (once per workgroup)
+        constexpr int UPC = G::TW / 8; // units per copy
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int u = tid + G::NT * k;
+            if (u < G::IMG_UNITS) *reinterpret_cast<uint4*>(tl + (u / UPC) * G::COPY + 16 * (u % UPC)) = ti[k];
+        }
+    }
+
+    const int rho = lane & 31;
+    const int h = lane >> 5;
+    const int phase = rho;
+    auto process = [&](int64_t ch, const float4 (&v)[4], const float4& hv) {
+        {   // chunk + halo range -> workgroup scale and exact-path decision
+            float mf = max_abs4(hv);
+            unsigned z = min_nz1(hv);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                mf = __builtin_elementwise_maximum(mf, max_abs4(v[u]));
+                z = min(z, min_nz1(v[u]));
+            }
+            const unsigned m = wave_max(__float_as_uint(mf));
+            z = wave_min(z);
+            if (lane == 0) {
+                slot_max[wave] = m;
+                slot_mnz[wave] = z;
+            }
+        }
+        nsh::lds_barrier(); // also: every wave is done with the previous chunk's planes
+        const unsigned m = max(max(slot_max[0], slot_max[1]), max(slot_max[2], slot_max[3]));
+        const unsigned z = min(min(slot_mnz[0], slot_mnz[1]), min(slot_mnz[2], slot_mnz[3]));
+        const int s = scale_of(m);
+        const bool exact = chunk_needs_exact(m, z, s);
+        if (exact) {
+            float4* r = reinterpret_cast<float4*>(lds);
+            if (tid < G::HP) r[tid] = hv;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) r[G::HP + tid + G::NT * u] = v[u];
+        } else {
+            if (tid < G::HP) store_pair9<Q>(hv, lds, 2 * tid, s);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) store_pair9<Q>(v[u], lds, G::H + 2 * (tid + G::NT * u), s);
+        }
+        nsh::lds_barrier();
+        nf2 o[8];
+        if (exact) {
+            direct_tile9<Q>(lds, taps, L, wave, h, phase, o);
+        } else {
+            const int b = rho & 15, c = rho >> 4;
+            const int a_base = c * 2 * G::PLANE + ((Q - 1) + 16 * wave + b) * 80 + 16 * h;
+            f32x16 acc_hi = {};
+            f32x16 acc_lo = {};
+#pragma unroll
+            for (int st = 0; st < 2 * Q; ++st) {
+                const int off = a_base - (st >> 1) * 80 + 32 * (st & 1);
+                const f16x8 A0 = *reinterpret_cast<const f16x8*>(lds + off);
+                const f16x8 A1 = *reinterpret_cast<const f16x8*>(lds + off + G::PLANE);
+                // taps h[t0 - j], t0 = i - 16 (st & 1) - 8 h + 32 (st >> 1): R[m0 + j], m0 = 32Q - 1 - t0
+                const int m0 = 32 * Q - 1 - rho + 16 * (st & 1) + 8 * h - 32 * (st >> 1);
+                const int tb = (m0 & 7) * G::COPY + 2 * (m0 & ~7);
+                const f16x8 B0 = *reinterpret_cast<const f16x8*>(tl + tb);
+                const f16x8 B1 = *reinterpret_cast<const f16x8*>(tl + 8 * G::COPY + tb);
+                acc_hi = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, B0, acc_hi, 0, 0, 0);
+                acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, B1, acc_lo, 0, 0, 0);
+                acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, B0, acc_lo, 0, 0, 0);
+            }
+            const f32x16 sum = acc_hi + acc_lo;
+            const int unscale = -(s + sh);
+            if (unscale >= -126 && unscale <= 127) {
+                const nf2 f = nf2{ __builtin_bit_cast(float, (unscale + 127) << 23), __builtin_bit_cast(float, (unscale + 127) << 23) };
+#pragma unroll
+                for (int reg = 0; reg < 8; ++reg) o[reg] = nf2{ sum[reg], sum[reg + 8] } * f;
+            } else {
+#pragma unroll
+                for (int reg = 0; reg < 8; ++reg) o[reg] = nf2{ __builtin_ldexpf(sum[reg], unscale), __builtin_ldexpf(sum[reg + 8], unscale) };
+            }
+        }
+        const __amdgpu_buffer_rsrc_t r = chunk_rsrc<2048>(out, ch, n_out);
+        const int base = wave * TILE + phase;
+#pragma unroll
+        for (int reg = 0; reg < 8; ++reg) buf_store_f2(r, (base + 32 * ((reg & 3) + 8 * (reg >> 2) + 4 * h)) * 8, o[reg]);
+    };
+    if (CPW == 1) {
+        process(c_first, va, ha);
+    } else {
+        // two register sets: chunk i+1 is in flight while chunk i is filtered
+        for (int i = 0; i < n_my; i += 2) {
+            process(c_first + i, va, ha);
+            if (i + 2 < n_my) load(c_first + i + 2, va, ha);
+            if (i + 1 < n_my) {
+                process(c_first + i + 1, vb, hb);
+                if (i + 3 < n_my) load(c_first + i + 3, vb, hb);
+            }
+        }
+    }
+    if (c_first == 0) // the last L-1 inputs for the next call (after this workgroup's stores)
+        for (int j = tid; j < L - 1; j += G::NT) hist_out[j] = virt(in, hist_in, n_in - (L - 1) + j, n_in, L);
+}
+
 typedef __attribute__((ext_vector_type(4))) _Float16 f16x4;
 
 // ---- k_fir_mfma11: decimating polyphase FIR (D = 2, 4) on the fp16x2 split -----------------
@@ -2393,10 +2591,37 @@ int launch_v9(const nsh_fir_plan* p, const float2* in, const float2* hin, float2
 }
 
 
+template <int Q, int CPW>
+int launch_v12(const nsh_fir_plan* p, const float2* in, const float2* hin, float2* hout, float2* out, int64_t n_out,
+               hipStream_t s)
+{
+    using G = geom12<Q>;
+    static bool attr_set = false;
+    if (!attr_set) {
+        NSH_CK(hipFuncSetAttribute((const void*)k_fir_mfma12<Q, CPW>, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
+        attr_set = true;
+    }
+    const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
+    const int64_t nwg = (nchunks + CPW - 1) / CPW;
+    const int64_t per_x = (nwg + 7) / 8; // workgroups per XCD
+    const int64_t grid = per_x * 8;
+    if (grid > 0x7fffffff) return nsh::fail_msg("nsh_fir_ccf(mfma v12): stream too long for one launch");
+    hipLaunchKernelGGL((k_fir_mfma12<Q, CPW>), dim3((unsigned)grid), dim3(G::NT), G::LDS, s, in, hin, hout, out,
+                       (const uint4*)p->frag12_dev, (const float*)p->taps_dev, p->L, p->sh8, n_out, per_x);
+    NSH_CK_LAUNCH("nsh_fir_ccf(mfma fp16x2 v12)");
+    return 0;
+}
+
 // Tuning variants (selected by NSH_FIR_MFMA_VARIANT for A/B runs; default = measured best).
 template <int Q>
 int launch_q(const nsh_fir_plan* p, const float2* in, const float2* hin, float2* hout, float2* out, int64_t n_out, hipStream_t s)
 {
+    if (p->frag12_dev && !p->force_x3 && (p->variant == 0 || p->variant == 12))
+        return launch_v12<Q, 1>(p, in, hin, hout, out, n_out, s); // default
+    if (p->frag12_dev && !p->force_x3 && p->variant == 13)
+        return launch_v12<Q, 2>(p, in, hin, hout, out, n_out, s);
+    if (p->frag12_dev && !p->force_x3 && p->variant == 14)
+        return launch_v12<Q, 4>(p, in, hin, hout, out, n_out, s);
     if (p->frag8_dev && !p->force_x3 && p->variant != 6 && p->variant != 7)
         return launch_v9<Q>(p, in, hin, hout, out, n_out, s);
     switch (p->variant) {
@@ -2574,6 +2799,19 @@ int nsh_fir_mfma_prepare(nsh_fir_plan* p)
                         f8[(((size_t)1 * S + st) * 64 + lane) * 8 + j] = h1;
                     }
             p->sh8 = sh;
+            // v12 tap image: R[m] = h[32Q - 1 - m] (scaled, hi/lo fp16), copy k holds R[k .. k + TW)
+            const int TW = 32 * Q + 24;
+            std::vector<_Float16> f12((size_t)2 * 8 * TW, (_Float16)0.f);
+            for (int k = 0; k < 8; ++k)
+                for (int e = 0; e < TW; ++e) {
+                    const int t = 32 * Q - 1 - (e + k);
+                    const float hs = (t >= 0 && t < p->L) ? std::ldexp(p->taps_host[t], sh) : 0.f;
+                    const _Float16 h0 = (_Float16)hs;
+                    f12[(size_t)(0 * 8 + k) * TW + e] = h0;
+                    f12[(size_t)(1 * 8 + k) * TW + e] = (_Float16)(hs - (float)h0);
+                }
+            NSH_CK(hipMalloc(&p->frag12_dev, f12.size() * sizeof(_Float16)));
+            NSH_CK(hipMemcpy(p->frag12_dev, f12.data(), f12.size() * sizeof(_Float16), hipMemcpyHostToDevice));
             NSH_CK(hipMalloc(&p->frag8_dev, f8.size() * sizeof(_Float16)));
             NSH_CK(hipMemcpy(p->frag8_dev, f8.data(), f8.size() * sizeof(_Float16), hipMemcpyHostToDevice));
         }
@@ -2629,6 +2867,8 @@ std::string nsh_fir_mfma_kernel_name(const nsh_fir_plan* p)
     };
     if (p->algo == NSH_FIR_MFMA16) return t("k_fir_mfma5", p->QH, p->variant == 20 ? 2 : 1);
     if (p->D > 1) return t(p->fragd8_dev && p->variant != 7 ? "k_fir_mfma11" : "k_fir_mfma7", p->D, p->QHD);
+    if (p->frag12_dev && !p->force_x3 && (p->variant == 0 || (p->variant >= 12 && p->variant <= 14)))
+        return t("k_fir_mfma12", p->Q, p->variant == 13 ? 2 : p->variant == 14 ? 4 : 1);
     if (p->frag8_dev && !p->force_x3 && p->variant != 6 && p->variant != 7) return t("k_fir_mfma9", p->Q);
     if (p->variant >= 20) return t("k_fir_mfma5", p->QH, p->variant == 20 ? 2 : 1);
     return t("k_fir_mfma2", p->Q, p->variant == 6 ? 1 : 2);

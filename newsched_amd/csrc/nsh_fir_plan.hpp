@@ -29,6 +29,9 @@ struct nsh_fir_plan {
     // scaled fp16x2 form (decim 1, default): taps * 2^sh8 split into two fp16 terms,
     // [part(2)][kstep(S)][lane(64)][8]; null when the taps' range does not allow it.
     void* frag8_dev = nullptr;
+    // k_fir_mfma12: the same scaled fp16x2 taps reversed, as 8 shifted copies per plane,
+    // [part(2)][shift(8)][32Q + 24] fp16 (a lane's 8 taps of a k-step = one aligned 16-B read)
+    void* frag12_dev = nullptr;
     int sh8 = 0;
     bool force_x3 = false; // NSH_FIR_MFMA_BF16X3: always the bf16x3 six-product kernel
     int variant = 0;      // MFMA kernel tuning variant (0 = default)

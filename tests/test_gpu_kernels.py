@@ -129,12 +129,12 @@ def test_mul_const_vcc_bitexact(torch_cuda, vlen, nitems):
     np.testing.assert_array_equal(host(dy)[: nitems * vlen], orc.mul_cc(x, np.tile(k, nitems)))
 
 
-# "mfma" is the default matrix-core kernel (decim 1: per-chunk scaled fp16x2, k_fir_mfma9),
+# "mfma" is the default matrix-core kernel (decim 1: per-chunk scaled fp16x2, k_fir_mfma12),
 # "mfma_x3" forces the bf16x3 six-product kernel (k_fir_mfma2), "mfma16" the 16-sample form.
-ALGOS = [("direct", nsh.FIR_DIRECT), ("mfma", nsh.FIR_MFMA), ("mfma_x3", nsh.FIR_MFMA_BF16X3),
-         ("mfma16", nsh.FIR_MFMA16)]
-MAX_TAPS = {"direct": 4096, "mfma": 161, "mfma_x3": 161, "mfma16": 145}
-VARIANT = {}  # name -> NSH_FIR_MFMA_VARIANT for tuning variants under test (none at present)
+ALGOS = [("direct", nsh.FIR_DIRECT), ("mfma", nsh.FIR_MFMA), ("mfma_v9", nsh.FIR_MFMA),
+         ("mfma_x3", nsh.FIR_MFMA_BF16X3), ("mfma16", nsh.FIR_MFMA16)]
+MAX_TAPS = {"direct": 4096, "mfma": 161, "mfma_v9": 161, "mfma_x3": 161, "mfma16": 145}
+VARIANT = {"mfma_v9": "9"}  # name -> NSH_FIR_MFMA_VARIANT for tuning variants under test
 
 
 def make_plan(name, taps, decim, algo):
@@ -192,7 +192,7 @@ def test_fir127_golden(torch_cuda, golden, name, algo):
     plan = make_plan(name, g["taps"], 1, algo)
     assert plan.algo == algo
     if name == "mfma":
-        assert plan.kernel == "k_fir_mfma9<5>", plan.kernel
+        assert plan.kernel == "k_fir_mfma12<5,1>", plan.kernel
     y, hist = run_fir(torch, plan, g["x"], g["x"].size)
     ok, err, scale = orc.tol_ok(y, g["y"])
     assert ok, (name, err, scale)
@@ -397,16 +397,20 @@ def _assert_nonfinite_pattern(y, ref):
     np.testing.assert_array_equal(np.sign(y.imag[inf]), np.sign(ref.imag[inf]))
 
 
-@pytest.fixture
-def v8_form(monkeypatch):
-    """The fp16x2 kernel (k_fir_mfma9, default): no tuning variant set."""
-    monkeypatch.delenv("NSH_FIR_MFMA_VARIANT", raising=False)
-    return "v9"
+@pytest.fixture(params=["v12", "v9"])
+def v8_form(request, monkeypatch):
+    """The fp16x2 kernels: k_fir_mfma12 (default: one chunk per workgroup) and k_fir_mfma9
+    (contiguous per-workgroup ranges, NSH_FIR_MFMA_VARIANT=9)."""
+    if request.param == "v9":
+        monkeypatch.setenv("NSH_FIR_MFMA_VARIANT", "9")
+    else:
+        monkeypatch.delenv("NSH_FIR_MFMA_VARIANT", raising=False)
+    return request.param
 
 
 def _v8_plan(h, form):
     plan = nsh.FirPlan(h, 1, nsh.FIR_MFMA)
-    assert plan.kernel == "k_fir_mfma9<5>", plan.kernel
+    assert plan.kernel == ("k_fir_mfma12<5,1>" if form == "v12" else "k_fir_mfma9<5>"), plan.kernel
     return plan
 
 
@@ -487,7 +491,7 @@ def test_fir_mfma_taps_far_below_max(torch_cuda):
     h[5] = np.float32(h.max() * 2.0 ** -40)
     x = orc.synth(30_000, 4)
     plan = nsh.FirPlan(h, 1, nsh.FIR_MFMA)
-    assert plan.kernel == "k_fir_mfma9<5>", plan.kernel
+    assert plan.kernel == "k_fir_mfma12<5,1>", plan.kernel
     y, _ = run_fir(torch, plan, x, x.size)
     ok, err, scale = orc.tol_ok(y, orc.fir_ccf(x, h))
     assert ok, (err, scale)
@@ -496,15 +500,15 @@ def test_fir_mfma_taps_far_below_max(torch_cuda):
 def test_fir_plan_kernels():
     """Which kernel each algorithm runs (no silent fallback between the MFMA forms)."""
     h = _firwin127()
-    assert nsh.FirPlan(h, 1, nsh.FIR_MFMA).kernel == "k_fir_mfma9<5>"
-    assert nsh.FirPlan(h, 1, nsh.FIR_AUTO).kernel == "k_fir_mfma9<5>"
+    assert nsh.FirPlan(h, 1, nsh.FIR_MFMA).kernel == "k_fir_mfma12<5,1>"
+    assert nsh.FirPlan(h, 1, nsh.FIR_AUTO).kernel == "k_fir_mfma12<5,1>"
     assert nsh.FirPlan(h, 1, nsh.FIR_MFMA_BF16X3).kernel == "k_fir_mfma2<5,2>"
     assert nsh.FirPlan(h, 1, nsh.FIR_MFMA16).kernel == "k_fir_mfma5<9,1>"
     assert nsh.FirPlan(h, 1, nsh.FIR_DIRECT).kernel == "k_fir_direct<1,8>"
     assert nsh.FirPlan(h, 2, nsh.FIR_MFMA).kernel == "k_fir_mfma11<2,5>"
     assert nsh.FirPlan(h, 4, nsh.FIR_MFMA).kernel == "k_fir_mfma11<4,3>"
     for L in (1, 17, 33, 65, 97, 129, 161):
-        assert nsh.FirPlan(np.ones(L, np.float32), 1, nsh.FIR_MFMA).kernel == "k_fir_mfma9<%d>" % ((L + 30) // 32 + 1)
+        assert nsh.FirPlan(np.ones(L, np.float32), 1, nsh.FIR_MFMA).kernel == "k_fir_mfma12<%d,1>" % ((L + 30) // 32 + 1)
 
 
 def test_fft_golden(torch_cuda, golden):
