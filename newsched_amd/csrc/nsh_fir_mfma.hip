@@ -1463,19 +1463,22 @@ __global__ __launch_bounds__(256) void k_fir_mfma12(const float2* __restrict__ i
     auto load = [&](int64_t ch, float4 (&v)[4], float4& hv) {
         load_chunk9(v, in, ch, n_in);
         __amdgpu_buffer_rsrc_t hr;
-        int off;
+        int off0, off1; // per sample: with an odd history length a pair straddles its start
         if (ch > 0) {
             hr = chunk_rsrc<G::H>(in + ch * G::CHUNK - G::H, 0, G::H);
-            off = 16 * tid;
+            off0 = 16 * tid;
+            off1 = off0 + 8;
         } else {
             hr = chunk_rsrc<1 << 20>(hist_in, 0, hist_in ? L - 1 : 0);
             const int e = 2 * tid - G::H + (L - 1); // history element of the lane's first sample
-            off = e >= 0 ? 8 * e : 1 << 30;          // past num_records -> zeros
+            off0 = e >= 0 ? 8 * e : 1 << 30;         // past num_records -> zeros
+            off1 = e + 1 >= 0 ? 8 * (e + 1) : 1 << 30;
         }
         hv = make_float4(0.f, 0.f, 0.f, 0.f);
         if (tid < G::HP) {
-            const nsh::buf_f4 t = __builtin_bit_cast(nsh::buf_f4, __builtin_amdgcn_raw_buffer_load_b128(hr, off, 0, 0));
-            hv = make_float4(t.x, t.y, t.z, t.w);
+            const nsh::buf_f2 a = __builtin_bit_cast(nsh::buf_f2, __builtin_amdgcn_raw_buffer_load_b64(hr, off0, 0, 0));
+            const nsh::buf_f2 b = __builtin_bit_cast(nsh::buf_f2, __builtin_amdgcn_raw_buffer_load_b64(hr, off1, 0, 0));
+            hv = make_float4(a.x, a.y, b.x, b.y);
         }
     };
     float4 va[4], vb[4], ha, hb;
