@@ -66,6 +66,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t chunk_rsrc(const float2* base,
 }
 constexpr int AUX_NT = 2; // gfx950 cache policy bits: nt (streaming)
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef float buf_f4 __attribute__((ext_vector_type(4)));
 typedef float buf_f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ float4 buf_load_f4(__amdgpu_buffer_rsrc_t r, int byte_off)

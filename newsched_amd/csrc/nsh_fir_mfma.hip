@@ -1429,7 +1429,7 @@ struct geom12 {
     static_assert(HP <= NT, "halo pairs: one per thread");
 };
 
-template <int Q, int CPW>
+template <int Q>
 __global__ __launch_bounds__(256) void k_fir_mfma12(const float2* __restrict__ in,
                                                     const float2* __restrict__ hist_in,
                                                     float2* __restrict__ hist_out,
@@ -1452,9 +1452,8 @@ __global__ __launch_bounds__(256) void k_fir_mfma12(const float2* __restrict__ i
     const int wave = tid >> 6;
     const int64_t n_in = n_out;
     const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
-    const int64_t c_first = ((int64_t)(blockIdx.x & 7) * per_x + (blockIdx.x >> 3)) * CPW;
+    const int64_t c_first = (int64_t)(blockIdx.x & 7) * per_x + (blockIdx.x >> 3);
     if (c_first >= nchunks) return; // whole workgroup: before any barrier
-    const int n_my = (int)(nchunks - c_first < CPW ? nchunks - c_first : CPW);
 
     // chunk ch -> registers (nontemporal) and its halo (default policy: the previous chunk's
     // tail was just read by this or the previous workgroup of this XCD). Branch-free: the halo
@@ -1481,29 +1480,34 @@ __global__ __launch_bounds__(256) void k_fir_mfma12(const float2* __restrict__ i
             hv = make_float4(a.x, a.y, b.x, b.y);
         }
     };
-    float4 va[4], vb[4], ha, hb;
+    float4 va[4], ha;
     load(c_first, va, ha);
-    uint4 ti[2];
+    constexpr int UPC = G::TW / 8; // 16-B units per copy
+    uint4 ti[2] = {};
+#if !(NSH_FIR_ABLATE & 4096) // timing only: no tap image loads
     {   // the tap image (L1/L2 hits), both units per lane issued before any wait
         const __amdgpu_buffer_rsrc_t tr = __builtin_amdgcn_make_buffer_rsrc((void*)timg, (short)0, G::IMG_UNITS * 16, 0x00020000);
 #pragma unroll
         for (int k = 0; k < 2; ++k)
             ti[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(tr, 16 * (tid + G::NT * k), 0, 0));
     }
-    if (CPW > 1 && n_my > 1) load(c_first + 1, vb, hb);
-    {   // tap image -> LDS at the padded copy pitch (once per workgroup)
-        constexpr int UPC = G::TW / 8; // units per copy
+#endif
+    // tap image -> LDS at the padded copy pitch
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const int u = tid + G::NT * k;
-            if (u < G::IMG_UNITS) *reinterpret_cast<uint4*>(tl + (u / UPC) * G::COPY + 16 * (u % UPC)) = ti[k];
-        }
+    for (int k = 0; k < 2; ++k) {
+        const int u = tid + G::NT * k;
+        if (u < G::IMG_UNITS) *reinterpret_cast<uint4*>(tl + (u / UPC) * G::COPY + 16 * (u % UPC)) = ti[k];
     }
 
     const int rho = lane & 31;
     const int h = lane >> 5;
     const int phase = rho;
     auto process = [&](int64_t ch, const float4 (&v)[4], const float4& hv) {
+#if NSH_FIR_ABLATE & 8192 // timing only: fixed scale, no reductions, no first barrier
+        const int s = 0;
+        const bool exact = false;
+        if (ch < 0) slot_max[0] = 0;
+#else
         {   // chunk + halo range -> workgroup scale and exact-path decision
             float mf = max_abs4(hv);
             unsigned z = min_nz1(hv);
@@ -1524,6 +1528,7 @@ __global__ __launch_bounds__(256) void k_fir_mfma12(const float2* __restrict__ i
         const unsigned z = min(min(slot_mnz[0], slot_mnz[1]), min(slot_mnz[2], slot_mnz[3]));
         const int s = scale_of(m);
         const bool exact = chunk_needs_exact(m, z, s);
+#endif
         if (exact) {
             float4* r = reinterpret_cast<float4*>(lds);
             if (tid < G::HP) r[tid] = hv;
@@ -1553,6 +1558,10 @@ __global__ __launch_bounds__(256) void k_fir_mfma12(const float2* __restrict__ i
                 const int tb = (m0 & 7) * G::COPY + 2 * (m0 & ~7);
                 const f16x8 B0 = *reinterpret_cast<const f16x8*>(tl + tb);
                 const f16x8 B1 = *reinterpret_cast<const f16x8*>(tl + 8 * G::COPY + tb);
+#if NSH_FIR_ABLATE & 256 // timing only: LDS fragment reads kept, no matrix work
+                acc_hi[st & 15] += (float)A0[0] + (float)A1[1] + (float)B0[2] + (float)B1[3];
+                continue;
+#endif
                 acc_hi = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, B0, acc_hi, 0, 0, 0);
                 acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, B1, acc_lo, 0, 0, 0);
                 acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, B0, acc_lo, 0, 0, 0);
@@ -1569,23 +1578,19 @@ __global__ __launch_bounds__(256) void k_fir_mfma12(const float2* __restrict__ i
             }
         }
         const __amdgpu_buffer_rsrc_t r = chunk_rsrc<2048>(out, ch, n_out);
+#if NSH_FIR_ABLATE & 16384 // timing only: four contiguous 16-B stores per lane (a copy's store shape)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const nf2 a = o[2 * u], bb = o[2 * u + 1];
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(nsh::u32x4, nf4{ a.x, a.y, bb.x, bb.y }), r, (tid + G::NT * u) * 16, 0, AUX_NT);
+        }
+        return;
+#endif
         const int base = wave * TILE + phase;
 #pragma unroll
         for (int reg = 0; reg < 8; ++reg) buf_store_f2(r, (base + 32 * ((reg & 3) + 8 * (reg >> 2) + 4 * h)) * 8, o[reg]);
     };
-    if (CPW == 1) {
-        process(c_first, va, ha);
-    } else {
-        // two register sets: chunk i+1 is in flight while chunk i is filtered
-        for (int i = 0; i < n_my; i += 2) {
-            process(c_first + i, va, ha);
-            if (i + 2 < n_my) load(c_first + i + 2, va, ha);
-            if (i + 1 < n_my) {
-                process(c_first + i + 1, vb, hb);
-                if (i + 3 < n_my) load(c_first + i + 3, vb, hb);
-            }
-        }
-    }
+    process(c_first, va, ha);
     if (c_first == 0) // the last L-1 inputs for the next call (after this workgroup's stores)
         for (int j = tid; j < L - 1; j += G::NT) hist_out[j] = virt(in, hist_in, n_in - (L - 1) + j, n_in, L);
 }
@@ -2594,22 +2599,21 @@ int launch_v9(const nsh_fir_plan* p, const float2* in, const float2* hin, float2
 }
 
 
-template <int Q, int CPW>
+template <int Q>
 int launch_v12(const nsh_fir_plan* p, const float2* in, const float2* hin, float2* hout, float2* out, int64_t n_out,
                hipStream_t s)
 {
     using G = geom12<Q>;
     static bool attr_set = false;
     if (!attr_set) {
-        NSH_CK(hipFuncSetAttribute((const void*)k_fir_mfma12<Q, CPW>, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
+        NSH_CK(hipFuncSetAttribute((const void*)k_fir_mfma12<Q>, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
         attr_set = true;
     }
     const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
-    const int64_t nwg = (nchunks + CPW - 1) / CPW;
-    const int64_t per_x = (nwg + 7) / 8; // workgroups per XCD
+    const int64_t per_x = (nchunks + 7) / 8; // workgroups (= chunks) per XCD
     const int64_t grid = per_x * 8;
     if (grid > 0x7fffffff) return nsh::fail_msg("nsh_fir_ccf(mfma v12): stream too long for one launch");
-    hipLaunchKernelGGL((k_fir_mfma12<Q, CPW>), dim3((unsigned)grid), dim3(G::NT), G::LDS, s, in, hin, hout, out,
+    hipLaunchKernelGGL((k_fir_mfma12<Q>), dim3((unsigned)grid), dim3(G::NT), G::LDS, s, in, hin, hout, out,
                        (const uint4*)p->frag12_dev, (const float*)p->taps_dev, p->L, p->sh8, n_out, per_x);
     NSH_CK_LAUNCH("nsh_fir_ccf(mfma fp16x2 v12)");
     return 0;
@@ -2620,11 +2624,7 @@ template <int Q>
 int launch_q(const nsh_fir_plan* p, const float2* in, const float2* hin, float2* hout, float2* out, int64_t n_out, hipStream_t s)
 {
     if (p->frag12_dev && !p->force_x3 && (p->variant == 0 || p->variant == 12))
-        return launch_v12<Q, 1>(p, in, hin, hout, out, n_out, s); // default
-    if (p->frag12_dev && !p->force_x3 && p->variant == 13)
-        return launch_v12<Q, 2>(p, in, hin, hout, out, n_out, s);
-    if (p->frag12_dev && !p->force_x3 && p->variant == 14)
-        return launch_v12<Q, 4>(p, in, hin, hout, out, n_out, s);
+        return launch_v12<Q>(p, in, hin, hout, out, n_out, s); // default
     if (p->frag8_dev && !p->force_x3 && p->variant != 6 && p->variant != 7)
         return launch_v9<Q>(p, in, hin, hout, out, n_out, s);
     switch (p->variant) {
@@ -2870,8 +2870,7 @@ std::string nsh_fir_mfma_kernel_name(const nsh_fir_plan* p)
     };
     if (p->algo == NSH_FIR_MFMA16) return t("k_fir_mfma5", p->QH, p->variant == 20 ? 2 : 1);
     if (p->D > 1) return t(p->fragd8_dev && p->variant != 7 ? "k_fir_mfma11" : "k_fir_mfma7", p->D, p->QHD);
-    if (p->frag12_dev && !p->force_x3 && (p->variant == 0 || (p->variant >= 12 && p->variant <= 14)))
-        return t("k_fir_mfma12", p->Q, p->variant == 13 ? 2 : p->variant == 14 ? 4 : 1);
+    if (p->frag12_dev && !p->force_x3 && (p->variant == 0 || p->variant == 12)) return t("k_fir_mfma12", p->Q);
     if (p->frag8_dev && !p->force_x3 && p->variant != 6 && p->variant != 7) return t("k_fir_mfma9", p->Q);
     if (p->variant >= 20) return t("k_fir_mfma5", p->QH, p->variant == 20 ? 2 : 1);
     return t("k_fir_mfma2", p->Q, p->variant == 6 ? 1 : 2);
