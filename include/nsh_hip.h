@@ -109,23 +109,25 @@ int nsh_synth_cf32(float* out, int64_t n, uint64_t first_index, uint64_t seed, v
  *              which saves the stream-start memset)
  *   hist_out : receives the ntaps-1 samples that precede the NEXT call's in[0]
  *              (must not alias hist_in -- ping-pong two buffers)
- * algo: NSH_FIR_AUTO picks by measurement; NSH_FIR_DIRECT is the fp32 VALU
- * direct form; NSH_FIR_MFMA is the split-precision Toeplitz form on the matrix cores
- * (decim 1: 32-sample blocks, ntaps <= 161, per-chunk scaled fp16x2 with three products,
- * or bf16x3 with six when the taps span more than 2^28; decim 2/4: polyphase bf16x3);
- * NSH_FIR_MFMA16 is the bf16x3 form on 16-sample blocks (decim 1, ntaps <= 145);
- * NSH_FIR_MFMA_BF16X3 is NSH_FIR_MFMA with the bf16x3 kernel forced for decim 1. */
+ * algo: NSH_FIR_AUTO picks by measurement (MFMA for decim 1, 2, 4 with finite
+ * taps, else DIRECT); NSH_FIR_DIRECT is the fp32 VALU direct form (any decim; the only form
+ * for decim 8 and above); NSH_FIR_MFMA is the split-precision Toeplitz form on the matrix
+ * cores: decim 1 on 32-sample blocks, ntaps <= 161, fp16x2 at a per-chunk power-of-two scale
+ * with three products (k_fir_mfma12; chunks holding non-finite or fp16-subnormal-range
+ * samples take the fp32 direct form inside the same launch); decim 2 and 4 as the polyphase
+ * fp16x2 form (k_fir_mfma11); NSH_FIR_MFMA16 is the bf16x3 form on 16-sample blocks (decim 1,
+ * ntaps <= 145); NSH_FIR_MFMA_BF16X3 forces the bf16x3 six-product kernel for decim 1. */
 enum nsh_fir_algo { NSH_FIR_AUTO = 0, NSH_FIR_DIRECT = 1, NSH_FIR_MFMA = 2, NSH_FIR_MFMA16 = 3, NSH_FIR_MFMA_BF16X3 = 4 };
 int nsh_fir_plan_create(int dev, const float* taps_host, int ntaps, int decim, int algo, void** plan);
 int nsh_fir_plan_destroy(void* plan);
 int nsh_fir_plan_algo(void* plan);          /* the algorithm AUTO resolved to */
-const char* nsh_fir_plan_kernel(void* plan); /* the kernel nsh_fir_ccf launches, e.g. "k_fir_mfma9<5>" */
+const char* nsh_fir_plan_kernel(void* plan); /* the kernel nsh_fir_ccf launches, e.g. "k_fir_mfma12<5>" */
 int nsh_fir_ccf(void* plan, const float* in, const float* hist_in, float* hist_out,
                 float* out, int64_t n_out, void* stream);
 
 /* Two decimate-by-2 FIRs in one pass (the fused form of fir_filter_ccf(h1, 2) ->
- * fir_filter_ccf(h2, 2), what scheduler_hip's fusion pass turns such a pair into; replaces
- * two nsh_fir_ccf calls): y1[i] = sum_k h1[k] x[2i - k], y2[m] = sum_k h2[k] y1[2m - k].
+ * fir_filter_ccf(h2, 2); replaces two nsh_fir_ccf calls; scheduler_hip's fusion pass does not
+ * use it: it measured no faster than the two launches): y1[i] = sum_k h1[k] x[2i - k], y2[m] = sum_k h2[k] y1[2m - k].
  * plan1/plan2 are decim-2 NSH_FIR_MFMA (or AUTO-resolved MFMA) plans on the same device;
  * in = 4 n_out samples; hist1 = ntaps1-1 x samples, hist2 = ntaps2-1 y1 samples, each an
  * in/out pair as for nsh_fir_ccf (no aliasing). Outputs within the fp16x2 MFMA tolerance of

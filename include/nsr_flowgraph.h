@@ -34,7 +34,7 @@ int nsr_fir_bench_run(void* handle); /* one run (start + wait); rethrown work() 
 /* Over the last run: summed FIR kernel time from HIP events around each launch on the
  * partition stream, FIR launches, samples, and the algorithm the plan resolved to. */
 int nsr_fir_bench_stats(void* handle, double* kernel_ms, uint64_t* launches, uint64_t* samples, int* algo);
-/* The FIR kernel the bench's block launches (after its first run), e.g. "k_fir_mfma8<5>". */
+/* The FIR kernel the bench's block launches (after its first run), e.g. "k_fir_mfma12<5>". */
 const char* nsr_fir_bench_kernel(void* handle);
 /* The last `count` FIR outputs of the last run (interleaved re,im fp32) -> host. */
 int nsr_fir_bench_tail(void* handle, int64_t count, float* out_host);

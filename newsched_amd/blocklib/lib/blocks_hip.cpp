@@ -19,9 +19,10 @@ namespace hip {
 work_return_code_t copy::work(std::vector<block_work_input>& in, std::vector<block_work_output>& out)
 {
     const size_t n = (size_t)out[0].n_items;
-    check(nsh_copy(in[0].buffer->read_ptr(), out[0].buffer->write_ptr(), n * d_batch_size * sizeof(gr_complex),
-                   current_stream()),
-          "hip::copy");
+    for (size_t l = 0; l < d_load; ++l)
+        check(nsh_copy(in[0].buffer->read_ptr(), out[0].buffer->write_ptr(), n * d_batch_size * sizeof(gr_complex),
+                       current_stream()),
+              "hip::copy");
     out[0].n_produced = out[0].n_items;
     return work_return_code_t::WORK_OK;
 }

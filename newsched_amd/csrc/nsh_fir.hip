@@ -15,8 +15,9 @@
 //    are padded by one sample every R*D samples so the per-lane ds_read_b64 of the window
 //    is bank-conflict-free. Exact fp32 products, fp32 accumulation in tap order.
 //  * MFMA / MFMA16 / MFMA_BF16X3 -- split-precision Toeplitz MFMA (nsh_fir_mfma.hip):
-//    decim 1 on 32-sample blocks as scaled fp16x2 (default) or bf16x3, on 16-sample blocks
-//    as bf16x3; decim 2 and 4 as a polyphase bf16x3 form.
+//    decim 1 on 32-sample blocks as scaled fp16x2 (default, k_fir_mfma12; k_fir_mfma9 as
+//    NSH_FIR_MFMA_VARIANT=9) or bf16x3, on 16-sample blocks as bf16x3; decim 2 and 4 as the
+//    polyphase fp16x2 form (k_fir_mfma11). Decim 8 and above: DIRECT.
 #include "nsh_common.hpp"
 
 #include <algorithm>
@@ -150,6 +151,7 @@ int nsh_fir_plan_create(int dev, const float* taps_host, int ntaps, int decim, i
     NSH_CK(hipSetDevice(dev));
     auto* p = new nsh_fir_plan();
     p->dev = dev;
+    if (hipDeviceGetAttribute(&p->n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) p->n_cu = 256;
     p->L = ntaps;
     p->D = decim;
     p->Lp = (ntaps + 7) / 8 * 8;

@@ -35,6 +35,9 @@
 #include "nsh_common.hpp"
 
 #include <algorithm>
+#include <mutex>
+#include <set>
+#include <utility>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -53,15 +56,21 @@
 
 namespace {
 
-// CUs of the plan's device: one attribute query per plan instead of one per launch
-int plan_cus(const nsh_fir_plan* p)
+// CUs of the plan's device (queried once, at plan creation: a plan is read-only afterwards and
+// may be shared by concurrent launches)
+int plan_cus(const nsh_fir_plan* p) { return p->n_cu > 0 ? p->n_cu : 256; }
+
+// The dynamic-LDS limit of a kernel, set once per (kernel, device): hipFuncSetAttribute acts on
+// the current device, so a process-wide flag would leave a second device's launches unset.
+hipError_t set_lds_attr(const void* fn, int bytes, int dev)
 {
-    if (p->n_cu <= 0) {
-        int n = 256;
-        (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, p->dev);
-        const_cast<nsh_fir_plan*>(p)->n_cu = n;
-    }
-    return p->n_cu;
+    static std::mutex m;
+    static std::set<std::pair<const void*, int>> done;
+    std::lock_guard<std::mutex> g(m);
+    if (done.count({ fn, dev })) return hipSuccess;
+    const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (e == hipSuccess) done.insert({ fn, dev });
+    return e;
 }
 
 using nsh::AUX_NT;
@@ -719,11 +728,7 @@ int launch_v5(const nsh_fir_plan* p, const float2* in, const float2* hin, float2
               hipStream_t s, int wg_per_cu)
 {
     using G = geom5<QH>;
-    static bool attr_set = false;
-    if (!attr_set) {
-        NSH_CK(hipFuncSetAttribute((const void*)k_fir_mfma5<QH, DEPTH>, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
-        attr_set = true;
-    }
+    NSH_CK(set_lds_attr((const void*)k_fir_mfma5<QH, DEPTH>, G::LDS, p->dev));
     const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
     const int n_cu = plan_cus(p);
     const int64_t max_grid = (int64_t)n_cu * wg_per_cu;
@@ -1937,11 +1942,7 @@ int launch_v7(const nsh_fir_plan* p, const float2* in, const float2* hin, float2
               hipStream_t s)
 {
     using G = geom7<D, QH>;
-    static bool attr_set = false;
-    if (!attr_set) {
-        NSH_CK(hipFuncSetAttribute((const void*)k_fir_mfma7<D, QH>, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
-        attr_set = true;
-    }
+    NSH_CK(set_lds_attr((const void*)k_fir_mfma7<D, QH>, G::LDS, p->dev));
     const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
     const int n_cu = plan_cus(p);
     const int wg_per_cu = (160 * 1024) / G::LDS >= 3 ? 3 : 2; // LDS-bound residency (VGPRs allow 3)
@@ -1958,11 +1959,7 @@ int launch_v11(const nsh_fir_plan* p, const float2* in, const float2* hin, float
                hipStream_t s)
 {
     using G = geom11<D, QH>;
-    static bool attr_set = false;
-    if (!attr_set) {
-        NSH_CK(hipFuncSetAttribute((const void*)k_fir_mfma11<D, QH>, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
-        attr_set = true;
-    }
+    NSH_CK(set_lds_attr((const void*)k_fir_mfma11<D, QH>, G::LDS, p->dev));
     const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
     const int n_cu = plan_cus(p);
     const int64_t max_grid = (int64_t)n_cu * 2; // launch_v9's longer grids measured 4-7 % slower here
@@ -2498,11 +2495,7 @@ int launch_casc2(const nsh_fir_plan* p1, const nsh_fir_plan* p2, const float2* i
                  const float2* h2i, float2* h2o, float2* out, int64_t n_out, hipStream_t s)
 {
     using C = geomcasc<QH1, QH2>;
-    static bool attr_set = false;
-    if (!attr_set) {
-        NSH_CK(hipFuncSetAttribute((const void*)k_fir_casc2<QH1, QH2>, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS));
-        attr_set = true;
-    }
+    NSH_CK(set_lds_attr((const void*)k_fir_casc2<QH1, QH2>, C::LDS, p1->dev));
     const int64_t nchunks = (2 * n_out + 1023) / 1024;
     const int n_cu = plan_cus(p1);
     const int64_t max_grid = (int64_t)n_cu * 2;
@@ -2549,11 +2542,7 @@ int launch_v2(const nsh_fir_plan* p, const float2* in, const float2* hin, float2
               hipStream_t s, int wg_per_cu)
 {
     using G = geom2<Q>;
-    static bool attr_set = false;
-    if (!attr_set) {
-        NSH_CK(hipFuncSetAttribute((const void*)k_fir_mfma2<Q, DEPTH>, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
-        attr_set = true;
-    }
+    NSH_CK(set_lds_attr((const void*)k_fir_mfma2<Q, DEPTH>, G::LDS, p->dev));
     const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
     const int n_cu = plan_cus(p);
     const int64_t max_grid = (int64_t)n_cu * wg_per_cu;
@@ -2571,11 +2560,7 @@ int launch_v9(const nsh_fir_plan* p, const float2* in, const float2* hin, float2
               hipStream_t s)
 {
     using G = geom8<Q>;
-    static bool attr_set = false;
-    if (!attr_set) {
-        NSH_CK(hipFuncSetAttribute((const void*)k_fir_mfma9<Q>, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
-        attr_set = true;
-    }
+    NSH_CK(set_lds_attr((const void*)k_fir_mfma9<Q>, G::LDS, p->dev));
     const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
     const int n_cu = plan_cus(p);
     // Workgroups over the whole launch (2 resident per CU at a time): 16 chunks each from 2^26
@@ -2604,11 +2589,7 @@ int launch_v12(const nsh_fir_plan* p, const float2* in, const float2* hin, float
                hipStream_t s)
 {
     using G = geom12<Q>;
-    static bool attr_set = false;
-    if (!attr_set) {
-        NSH_CK(hipFuncSetAttribute((const void*)k_fir_mfma12<Q>, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
-        attr_set = true;
-    }
+    NSH_CK(set_lds_attr((const void*)k_fir_mfma12<Q>, G::LDS, p->dev));
     const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
     const int64_t per_x = (nchunks + 7) / 8; // workgroups (= chunks) per XCD
     const int64_t grid = per_x * 8;

@@ -32,6 +32,17 @@ struct fusion_result {
     flat_graph_sptr graph;            // the rewritten partition (== input if nothing fused)
     std::vector<block_sptr> fused;    // the blocks that replaced chains
     std::vector<std::vector<block_sptr>> chains; // fused[i] replaced chains[i]
+    // Port links the pass changed on the user's blocks (directed: first->connect/disconnect
+    // (second)); undo() restores the graph's original links, so the same flowgraph can be
+    // initialized again (validate, partition) with or without fusion.
+    std::vector<std::pair<port_sptr, port_sptr>> cut, added;
+    void undo()
+    {
+        for (auto it = added.rbegin(); it != added.rend(); ++it) it->first->disconnect(it->second);
+        for (auto it = cut.rbegin(); it != cut.rend(); ++it) it->first->connect(it->second);
+        added.clear();
+        cut.clear();
+    }
 };
 
 // Stages per fused block (the fused kernel's limit); longer chains become several blocks.

@@ -30,8 +30,16 @@ namespace {
 // Replace each chain (a path of blocks joined by single edges) by one block with the head's
 // input port and the tail's output port; shared by the passes.
 flat_graph_sptr rewrite_chains(flat_graph_sptr fg, const std::vector<std::vector<block_sptr>>& chains,
-                               const std::vector<block_sptr>& fused)
+                               const std::vector<block_sptr>& fused, fusion_result& r)
 {
+    auto cut = [&r](const port_sptr& a, const port_sptr& b) {
+        a->disconnect(b);
+        r.cut.emplace_back(a, b);
+    };
+    auto link = [&r](const port_sptr& a, const port_sptr& b) {
+        a->connect(b);
+        r.added.emplace_back(a, b);
+    };
     auto as_block = [](const node_sptr& n) { return std::dynamic_pointer_cast<block>(n); };
     std::map<block*, std::pair<size_t, block_sptr>> owner;
     for (size_t i = 0; i < chains.size(); ++i)
@@ -46,22 +54,24 @@ flat_graph_sptr rewrite_chains(flat_graph_sptr fg, const std::vector<std::vector
             g->edges().push_back(e);
             continue;
         }
-        e->src().port()->disconnect(e->dst().port());
-        e->dst().port()->disconnect(e->src().port());
+        cut(e->src().port(), e->dst().port());
+        cut(e->dst().port(), e->src().port());
         if (so != owner.end() && dn != owner.end() && so->second.first == dn->second.first) continue; // interior
         auto src = so == owner.end() ? e->src()
                                      : node_endpoint(so->second.second, so->second.second->output_stream_ports()[0]);
         auto dst = dn == owner.end() ? e->dst()
                                      : node_endpoint(dn->second.second, dn->second.second->input_stream_ports()[0]);
-        auto ne = g->connect(src, dst);
+        auto ne = g->connect(src, dst); // links src.port <-> dst.port
+        r.added.emplace_back(src.port(), dst.port());
+        r.added.emplace_back(dst.port(), src.port());
         if (e->has_custom_buffer()) ne->set_custom_buffer(e->buffer_factory(), e->buf_properties());
     }
-    auto move_links = [](const port_sptr& from, const port_sptr& to) {
+    auto move_links = [&](const port_sptr& from, const port_sptr& to) {
         for (auto& peer : from->connected_ports()) {
-            peer->disconnect(from);
-            from->disconnect(peer);
-            peer->connect(to);
-            to->connect(peer);
+            cut(peer, from);
+            cut(from, peer);
+            link(peer, to);
+            link(to, peer);
         }
     };
     for (size_t i = 0; i < chains.size(); ++i) {
@@ -163,7 +173,7 @@ fusion_result fuse_elementwise_cc(flat_graph_sptr fg)
     // when one segment of a split chain feeds the next). Links that are not edges of this
     // partition (an in-process domain crossing keeps the original cross-domain port pair
     // connected for notifications) move to the fused block.
-    auto g = rewrite_chains(fg, chains, r.fused);
+    auto g = rewrite_chains(fg, chains, r.fused, r);
     r.chains = std::move(chains);
     r.graph = g;
     return r;
@@ -209,7 +219,7 @@ fusion_result fuse_channelizer(flat_graph_sptr fg)
         used.insert(f2.get());
     }
     if (r.fused.empty()) return r;
-    r.graph = rewrite_chains(fg, r.chains, r.fused);
+    r.graph = rewrite_chains(fg, r.chains, r.fused, r);
     return r;
 }
 

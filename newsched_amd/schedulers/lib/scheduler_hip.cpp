@@ -31,6 +31,7 @@ void scheduler_hip::release_fused()
     // fused blocks are owned here; their ports point at this scheduler's threads
     for (auto& f : _plan.fused)
         for (auto& p : f->all_ports()) p->set_parent_intf(nullptr);
+    _plan.undo(); // the user's blocks get their original port links back
     _plan = hip::fusion_result();
 }
 
@@ -45,6 +46,8 @@ void scheduler_hip::initialize(flat_graph_sptr fg, flowgraph_monitor_sptr fgmon,
         _plan.graph = ch.graph;
         _plan.fused.insert(_plan.fused.end(), ch.fused.begin(), ch.fused.end());
         _plan.chains.insert(_plan.chains.end(), ch.chains.begin(), ch.chains.end());
+        _plan.cut.insert(_plan.cut.end(), ch.cut.begin(), ch.cut.end());
+        _plan.added.insert(_plan.added.end(), ch.added.begin(), ch.added.end());
         fg = _plan.graph;
     }
     scheduler_mt::initialize(fg, fgmon, nbr);

@@ -242,3 +242,44 @@ TEST(Fusion, ChannelizerBoundaries)
     EXPECT_TRUE(run(2) == 0u); // spectrum fans out
     EXPECT_TRUE(run(3) == 0u); // ifft -> w -> fft
 }
+
+// fusion_result::undo() (scheduler_hip::release_fused) gives the user's blocks their original
+// port links back, so the same flowgraph can be initialized (and fused) again.
+TEST(Fusion, UndoRestoresPortLinks)
+{
+    auto src = blocks::vector_source_c::make(std::vector<gr_complex>(16));
+    auto m0 = multiply_const_cc::make(K(0));
+    auto m1 = multiply_const_cc::make(K(1));
+    auto m2 = multiply_const_cc::make(K(2));
+    auto snk = blocks::null_sink::make(sizeof(gr_complex));
+    auto fg = flowgraph::make();
+    fg->connect(src, 0, m0, 0)->set_custom_buffer(HIP_BUFFER_ARGS_H2D);
+    fg->connect(m0, 0, m1, 0);
+    fg->connect(m1, 0, m2, 0);
+    fg->connect(m2, 0, snk, 0)->set_custom_buffer(HIP_BUFFER_ARGS_D2H);
+    auto remote = blocks::null_sink::make(sizeof(gr_complex)); // a crossing's extra link
+    auto xin = remote->input_stream_ports()[0];
+    m2->output_stream_ports()[0]->connect(xin);
+    xin->connect(m2->output_stream_ports()[0]);
+    const std::vector<block_sptr> blks{ src, m0, m1, m2, snk, remote };
+    auto snapshot = [&] {
+        std::vector<std::vector<port_sptr>> v;
+        for (auto& b : blks)
+            for (auto& p : b->all_ports()) {
+                auto c = p->connected_ports(); // as a set: restored links may come back in another order
+                std::sort(c.begin(), c.end());
+                v.push_back(c);
+            }
+        return v;
+    };
+    const auto before = snapshot();
+    for (int round = 0; round < 2; ++round) {
+        auto r = hip::fuse_elementwise_cc(flat(fg));
+        ASSERT_TRUE(r.fused.size() == 1u);
+        EXPECT_TRUE(connected(xin, r.fused[0]->output_stream_ports()[0]));
+        EXPECT_FALSE(connected(m0->output_stream_ports()[0], m1->input_stream_ports()[0]));
+        r.undo();
+        EXPECT_TRUE(snapshot() == before);
+        EXPECT_FALSE(connected(xin, r.fused[0]->output_stream_ports()[0]));
+    }
+}

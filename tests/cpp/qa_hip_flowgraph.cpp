@@ -16,6 +16,7 @@
 #include <gnuradio/blocklib/blocks/multiply_const.hpp>
 #include <gnuradio/blocklib/blocks/nop.hpp>
 #include <gnuradio/blocklib/blocks/null_sink.hpp>
+#include <gnuradio/blocklib/blocks/null_source.hpp>
 #include <gnuradio/blocklib/blocks/vector_sink.hpp>
 #include <gnuradio/blocklib/blocks/vector_source.hpp>
 #include <gnuradio/blocklib/hip/arith.hpp>
@@ -29,6 +30,7 @@
 #include <gnuradio/hip_buffer.hpp>
 #include <gnuradio/schedulers/hip/scheduler_hip.hpp>
 #include <gnuradio/schedulers/mt/scheduler_mt.hpp>
+#include <gnuradio/vmcircbuf.hpp>
 
 using namespace gr;
 
@@ -58,6 +60,36 @@ static void cuda_copy_case(bool one_group)
 }
 TEST(SchedulerMTTest, CudaCopyBasic) { cuda_copy_case(true); }
 TEST(SchedulerMTTest, CudaCopyMultiThreaded) { cuda_copy_case(false); }
+
+// The reference's CUDA copy benchmark flowgraph (schedulers/mt/bench/cuda/bm_copy.cpp:55-100),
+// mem_model 0, with hip::copy::make(batch_size, load) and the HIP_BUFFER_ARGS_* edges:
+// null_source -> head -[H2D]-> copy x nblocks -[D2D]...-[D2H]-> null_sink, one scheduler_mt
+// with vmcirc default buffers of 2 items. Every sample must arrive; with load > 1 each copy
+// block repeats its pass (and is not fused).
+static void bm_copy_case(int nblocks, int load, int batch_size, uint64_t samples)
+{
+    std::vector<hip::copy::sptr> copy_blks(nblocks);
+    for (int i = 0; i < nblocks; i++) copy_blks[i] = hip::copy::make(batch_size, load);
+    auto src = blocks::null_source::make(sizeof(gr_complex) * batch_size);
+    auto snk = blocks::null_sink::make(sizeof(gr_complex) * batch_size);
+    auto head = blocks::head::make(sizeof(gr_complex) * batch_size, samples / batch_size);
+    auto fg = flowgraph::make();
+    fg->connect(src, 0, head, 0)->set_custom_buffer(VMCIRC_BUFFER_ARGS);
+    auto sched = schedulers::scheduler_mt::make("sched", sizeof(gr_complex) * batch_size * 2);
+    sched->set_default_buffer_factory(VMCIRC_BUFFER_ARGS);
+    fg->set_scheduler(sched);
+    fg->connect(head, 0, copy_blks[0], 0)->set_custom_buffer(HIP_BUFFER_ARGS_H2D);
+    for (int i = 0; i < nblocks - 1; i++)
+        fg->connect(copy_blks[i], 0, copy_blks[i + 1], 0)->set_custom_buffer(HIP_BUFFER_ARGS_D2D);
+    fg->connect(copy_blks[nblocks - 1], 0, snk, 0)->set_custom_buffer(HIP_BUFFER_ARGS_D2H);
+    fg->validate();
+    fg->start();
+    fg->wait();
+    EXPECT_EQ(snk->consumed(), samples / batch_size);
+    EXPECT_EQ(copy_blks[0]->load(), (size_t)load);
+}
+TEST(SchedulerMTTest, BmCopyFlowgraph) { bm_copy_case(4, 1, 1024, 1500000); }
+TEST(SchedulerMTTest, BmCopyFlowgraphLoad) { bm_copy_case(4, 3, 1024, 500000); }
 
 // ---- GPU scheduler domain ---------------------------------------------------------------
 TEST(HipDomain, FirMatchesCpuAndReruns)
@@ -206,6 +238,43 @@ TEST(HipDomain, FusionAcrossDomainsAndFanOut)
             EXPECT_TRUE(s2->data() == r2);
         }
     }
+}
+
+// A fused, domain-partitioned flowgraph initialized twice (partition() again after a run):
+// the second fusion pass must start from the user's original port links (ADVICE r1:
+// release_fused() restores them), and the crossing notifications must reach the new fused
+// block -- the run completes with the same, bit-exact output.
+TEST(HipDomain, FusedPartitionInitializedTwice)
+{
+    const size_t n = 1u << 20;
+    auto src = hip::synth_source::make(0, n);
+    auto m0 = hip::multiply_const_cc::make(gr_complex(0.5f, 0.25f));
+    auto m1 = hip::multiply_const_cc::make(gr_complex(-1.0f, 2.0f));
+    auto cp = hip::copy::make(1);
+    auto snk = blocks::vector_sink_c::make(1, n);
+    auto fg = flowgraph::make();
+    fg->connect(src, 0, m0, 0);
+    fg->connect(m0, 0, m1, 0);
+    fg->connect(m1, 0, cp, 0);
+    fg->connect(cp, 0, snk, 0)->set_custom_buffer(HIP_BUFFER_ARGS_D2H);
+    auto s0 = schedulers::scheduler_hip::make("hip0", 0, 1u << 20);
+    auto s1 = schedulers::scheduler_mt::make("mt", 32768);
+    fg->set_schedulers({ s0, s1 });
+    auto da = domain_adapter_direct_conf::make(buffer_preference_t::UPSTREAM);
+    std::vector<gr_complex> first;
+    for (int round = 0; round < 2; ++round) {
+        domain_conf_vec dc{ domain_conf(s0, { src, m0, m1, cp }, da), domain_conf(s1, { snk }, da) };
+        fg->partition(dc);
+        fg->run();
+        EXPECT_EQ(s0->fusion_plan().fused.size(), 1u);
+        if (round == 0)
+            first = snk->data();
+        else
+            EXPECT_TRUE(snk->data() == first);
+    }
+    auto x = synth(n);
+    for (auto& v : x) v = (v * gr_complex(0.5f, 0.25f)) * gr_complex(-1.0f, 2.0f);
+    EXPECT_TRUE(first == x);
 }
 
 TEST(HipDomain, ChannelizerC4)
