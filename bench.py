@@ -192,6 +192,46 @@ def run_c5(a, dist, backend, rank, world, device, torch, orc, nsr):
     return res
 
 
+def run_fp32_leg(a, n, taps, first, device, barrier, dist, tdev, torch, orc, nsr, nsh):
+    """The same C3 flowgraph with the exact-fp32 matrix form (NSH_FIR_MFMA_F32: no operand
+    split, fp32 products and sums) -- what the ceiling is without split precision."""
+    fb = nsr.FirBench(taps, n, device=device, algo=nsh.FIR_MFMA_F32, first_index=first,
+                      out_buf_bytes=a.out_buf_mib << 20)
+    steps = max(5, a.steps // 4)
+    for _ in range(max(3, a.warmup // 2)):
+        fb.run()
+    barrier()
+    l0 = fb.stats()["launches"]
+    kms, samples = 0.0, 0
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fb.run()
+        st = fb.stats()
+        kms += st["kernel_ms"]
+        samples += st["samples"]
+    barrier()
+    el = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([el], dtype=torch.float64, device=tdev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    st = fb.stats()
+    launches = st["launches"] - l0
+    avg_ms = kms / launches
+    m = 4096
+    y = fb.tail(m)
+    lo = first + n - m - (taps.size - 1)
+    xw = orc.synth(m + taps.size - 1, lo)
+    ok, err, _ = orc.tol_ok(y, orc.fir_ccf(xw[taps.size - 1:], taps, hist=xw[: taps.size - 1]))
+    fb.close()
+    achieved = BYTES_PER_SAMPLE * (samples / launches) / (avg_ms * 1e-3) / 1e9
+    world = dist.get_world_size() if dist is not None else 1
+    return {"kernel": st["kernel"], "steps": steps, "value": round(world * n * steps / el / 1e6, 1), "unit": "MSamples/s",
+            "avg_launch_us": round(avg_ms * 1e3, 2), "achieved_GBs": round(achieved, 1),
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "parity": {"max_abs_err": err, "ok": bool(ok)}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -200,7 +240,9 @@ def main():
     ap.add_argument("--min-warmup-s", type=float, default=1.0,
                     help="keep warming up (untimed runs) until this long has passed: clocks settle")
     ap.add_argument("--log2n", type=int, default=28)
-    ap.add_argument("--algo", default="auto", choices=["auto", "mfma", "mfma_x3", "mfma16", "direct"])
+    ap.add_argument("--algo", default="auto", choices=["auto", "mfma", "mfma_x3", "mfma16", "mfma_f32", "direct"])
+    ap.add_argument("--fp32-leg", choices=["on", "off"], default="on",
+                    help="also time the exact-fp32 matrix form (NSH_FIR_MFMA_F32) on the same flowgraph")
     ap.add_argument("--out-buf-mib", type=int, default=2048, help="FIR output hip_buffer (default: one launch per 2^28-sample step)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-log2n", type=int, default=28, help="CPU baseline sample (default: the full stream)")
@@ -257,7 +299,7 @@ def main():
     from oracle import oracle as orc  # checker only: tail parity + CPU-baseline inputs
 
     algo = {"auto": nsh.FIR_AUTO, "mfma": nsh.FIR_MFMA, "mfma16": nsh.FIR_MFMA16, "mfma_x3": nsh.FIR_MFMA_BF16X3,
-            "direct": nsh.FIR_DIRECT}[a.algo]
+            "mfma_f32": nsh.FIR_MFMA_F32, "direct": nsh.FIR_DIRECT}[a.algo]
     n = 1 << a.log2n
     taps = firwin(127, 0.2)
     first = rank * n  # this rank's time shard
@@ -293,7 +335,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     st = fb.stats()
-    algo_used = {1: "direct", 2: "mfma", 3: "mfma16", 4: "mfma_x3"}.get(st["algo"], str(st["algo"]))
+    algo_used = {1: "direct", 2: "mfma", 3: "mfma16", 4: "mfma_x3", 5: "mfma_f32"}.get(st["algo"], str(st["algo"]))
     kernel = st["kernel"]
     timed_launches = st["launches"] - launches0
     launches_per_run = timed_launches / a.steps
@@ -360,6 +402,9 @@ def main():
         out["roofline"]["traffic_source"] = ("HBM B/sample from separate rocprofv3 --pmc passes (%s), scaled to this "
                                              "launch size; not measured in this run" % src)
     fb.close()
+
+    if a.fp32_leg == "on" and a.algo == "auto":
+        out["fp32_exact"] = run_fp32_leg(a, n, taps, first, device, barrier, dist, tdev, torch, orc, nsr, nsh)
 
     if a.c5 == "on" or (a.c5 == "auto" and world > 1):
         out["c5_pipeline"] = run_c5(a, dist, backend, rank, world, device, torch, orc, nsr)

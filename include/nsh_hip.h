@@ -116,8 +116,18 @@ int nsh_synth_cf32(float* out, int64_t n, uint64_t first_index, uint64_t seed, v
  * with three products (k_fir_mfma12; chunks holding non-finite or fp16-subnormal-range
  * samples take the fp32 direct form inside the same launch); decim 2 and 4 as the polyphase
  * fp16x2 form (k_fir_mfma11); NSH_FIR_MFMA16 is the bf16x3 form on 16-sample blocks (decim 1,
- * ntaps <= 145); NSH_FIR_MFMA_BF16X3 forces the bf16x3 six-product kernel for decim 1. */
-enum nsh_fir_algo { NSH_FIR_AUTO = 0, NSH_FIR_DIRECT = 1, NSH_FIR_MFMA = 2, NSH_FIR_MFMA16 = 3, NSH_FIR_MFMA_BF16X3 = 4 };
+ * ntaps <= 145); NSH_FIR_MFMA_BF16X3 forces the bf16x3 six-product kernel for decim 1;
+ * NSH_FIR_MFMA_F32 is the exact-fp32 Toeplitz form on the fp32-input matrix instructions
+ * (decim 1, ntaps <= 257, finite taps; no operand split: fp32 products and sums, chunks with
+ * inf/NaN through the fp32 direct form in the same launch). */
+enum nsh_fir_algo {
+    NSH_FIR_AUTO = 0,
+    NSH_FIR_DIRECT = 1,
+    NSH_FIR_MFMA = 2,
+    NSH_FIR_MFMA16 = 3,
+    NSH_FIR_MFMA_BF16X3 = 4,
+    NSH_FIR_MFMA_F32 = 5
+};
 int nsh_fir_plan_create(int dev, const float* taps_host, int ntaps, int decim, int algo, void** plan);
 int nsh_fir_plan_destroy(void* plan);
 int nsh_fir_plan_algo(void* plan);          /* the algorithm AUTO resolved to */

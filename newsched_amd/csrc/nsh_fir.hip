@@ -164,7 +164,7 @@ int nsh_fir_plan_create(int dev, const float* taps_host, int ntaps, int decim, i
         delete p;
         return nsh::fail(e, "nsh_fir_plan_create: taps upload");
     }
-    if (algo < NSH_FIR_AUTO || algo > NSH_FIR_MFMA_BF16X3) {
+    if (algo < NSH_FIR_AUTO || algo > NSH_FIR_MFMA_F32) {
         (void)hipFree(p->taps_dev);
         delete p;
         return nsh::fail_msg("nsh_fir_plan_create: unknown algorithm");
@@ -179,6 +179,16 @@ int nsh_fir_plan_create(int dev, const float* taps_host, int ntaps, int decim, i
         (void)hipFree(p->taps_dev);
         delete p;
         return nsh::fail_msg("nsh_fir_plan_create: MFMA16 form needs decim 1, finite taps and ntaps <= 145");
+    }
+    if (resolved == NSH_FIR_MFMA_F32) {
+        const int rc = nsh_fir_f32_supported(p) ? nsh_fir_f32_prepare(p)
+                                                : nsh::fail_msg("nsh_fir_plan_create: MFMA_F32 form needs decim 1, finite taps and ntaps <= 257");
+        if (rc) {
+            if (p->tf32_dev) (void)hipFree(p->tf32_dev);
+            (void)hipFree(p->taps_dev);
+            delete p;
+            return rc;
+        }
     }
     if (resolved == NSH_FIR_MFMA || resolved == NSH_FIR_MFMA16) {
         if (resolved == NSH_FIR_MFMA && !nsh_fir_mfma_supported(p)) {
@@ -198,6 +208,8 @@ int nsh_fir_plan_create(int dev, const float* taps_host, int ntaps, int decim, i
     if (resolved == NSH_FIR_DIRECT) {
         static const int R[9] = { 0, 8, 8, 0, 4, 0, 0, 0, 2 };
         p->kernel = "k_fir_direct<" + std::to_string(p->D) + "," + std::to_string(R[p->D]) + ">";
+    } else if (resolved == NSH_FIR_MFMA_F32) {
+        // named by nsh_fir_f32_prepare
     } else {
         p->kernel = nsh_fir_mfma_kernel_name(p);
     }
@@ -214,6 +226,7 @@ int nsh_fir_plan_destroy(void* plan)
     if (p->frag16_dev) (void)hipFree(p->frag16_dev);
     if (p->frag8_dev) (void)hipFree(p->frag8_dev);
     if (p->frag12_dev) (void)hipFree(p->frag12_dev);
+    if (p->tf32_dev) (void)hipFree(p->tf32_dev);
     if (p->fragd_dev) (void)hipFree(p->fragd_dev);
     if (p->fragd8_dev) (void)hipFree(p->fragd8_dev);
     delete p;
@@ -232,6 +245,8 @@ int nsh_fir_ccf(void* plan, const float* in, const float* hist_in, float* hist_o
     hipStream_t s = nsh::S(stream);
     if (p->algo == NSH_FIR_MFMA || p->algo == NSH_FIR_MFMA_BF16X3)
         return nsh_fir_mfma_run(p, (const float2*)in, (const float2*)hist_in, (float2*)hist_out, (float2*)out, n_out, s);
+    if (p->algo == NSH_FIR_MFMA_F32)
+        return nsh_fir_f32_run(p, (const float2*)in, (const float2*)hist_in, (float2*)hist_out, (float2*)out, n_out, s);
     if (p->algo == NSH_FIR_MFMA16)
         return nsh_fir_mfma16_run(p, (const float2*)in, (const float2*)hist_in, (float2*)hist_out, (float2*)out, n_out, s);
     return run_direct(p, (const float2*)in, (const float2*)hist_in, (float2*)hist_out, (float2*)out, n_out, s);

@@ -33,6 +33,10 @@ struct nsh_fir_plan {
     // [part(2)][shift(8)][32Q + 24] fp16 (a lane's 8 taps of a k-step = one aligned 16-B read)
     void* frag12_dev = nullptr;
     int sh8 = 0;
+    // exact fp32 form (k_fir_f32mfma, NSH_FIR_MFMA_F32): QF tap blocks of 16, the reversed taps
+    // as 4 shifted copies [4][16 QF + 16] fp32
+    int QF = 0;
+    void* tf32_dev = nullptr;
     bool force_x3 = false; // NSH_FIR_MFMA_BF16X3: always the bf16x3 six-product kernel
     int variant = 0;      // MFMA kernel tuning variant (0 = default)
     int wg_per_cu = 0;    // decim-1 fp16x2 kernel: workgroups per CU over the launch (0 = auto)
@@ -49,6 +53,10 @@ int nsh_fir_mfma_run(const nsh_fir_plan* p, const float2* in, const float2* hist
                      float2* out, int64_t n_out, hipStream_t s);
 int nsh_fir_mfma16_run(const nsh_fir_plan* p, const float2* in, const float2* hist_in, float2* hist_out,
                        float2* out, int64_t n_out, hipStream_t s);
+bool nsh_fir_f32_supported(const nsh_fir_plan* p);
+int nsh_fir_f32_prepare(nsh_fir_plan* p);
+int nsh_fir_f32_run(const nsh_fir_plan* p, const float2* in, const float2* hist_in, float2* hist_out, float2* out,
+                    int64_t n_out, hipStream_t s);
 bool nsh_fir_cascade2_ok(const nsh_fir_plan* p1, const nsh_fir_plan* p2);
 int nsh_fir_cascade2_run(const nsh_fir_plan* p1, const nsh_fir_plan* p2, const float2* in, const float2* h1i, float2* h1o,
                          const float2* h2i, float2* h2o, float2* out, int64_t n_out, hipStream_t s);

@@ -132,8 +132,8 @@ def test_mul_const_vcc_bitexact(torch_cuda, vlen, nitems):
 # "mfma" is the default matrix-core kernel (decim 1: per-chunk scaled fp16x2, k_fir_mfma12),
 # "mfma_x3" forces the bf16x3 six-product kernel (k_fir_mfma2), "mfma16" the 16-sample form.
 ALGOS = [("direct", nsh.FIR_DIRECT), ("mfma", nsh.FIR_MFMA), ("mfma_v9", nsh.FIR_MFMA),
-         ("mfma_x3", nsh.FIR_MFMA_BF16X3), ("mfma16", nsh.FIR_MFMA16)]
-MAX_TAPS = {"direct": 4096, "mfma": 161, "mfma_v9": 161, "mfma_x3": 161, "mfma16": 145}
+         ("mfma_x3", nsh.FIR_MFMA_BF16X3), ("mfma16", nsh.FIR_MFMA16), ("mfma_f32", nsh.FIR_MFMA_F32)]
+MAX_TAPS = {"direct": 4096, "mfma": 161, "mfma_v9": 161, "mfma_x3": 161, "mfma16": 145, "mfma_f32": 257}
 VARIANT = {"mfma_v9": "9"}  # name -> NSH_FIR_MFMA_VARIANT for tuning variants under test
 
 
@@ -545,3 +545,49 @@ def test_fft_roundtrip_large(torch_cuda):
     sub = x[: 64 * 1024].cpu().numpy()
     ok, e, s = orc.tol_ok(X[: 64 * 1024].cpu().numpy(), orc.fft1024(sub))
     assert ok, (e, s)
+
+
+@pytest.mark.parametrize("ntaps", [1, 15, 16, 17, 127, 200, 257])
+def test_fir_mfma_f32_exact_class(torch_cuda, ntaps):
+    """The exact-fp32 matrix form (k_fir_f32mfma): fp32 products and sums, no split -- its
+    error is the fp32 direct form's order-of-summation difference, far inside 1e-5, including
+    at tap counts past the split forms' limit and across calls with history."""
+    torch = torch_cuda
+    rng = np.random.default_rng(ntaps)
+    h = (rng.standard_normal(ntaps) * 0.1).astype(np.float32)
+    plan = nsh.FirPlan(h, 1, nsh.FIR_MFMA_F32)
+    assert plan.kernel == "k_fir_f32mfma<%d>" % ((ntaps + 30) // 16), plan.kernel
+    x = orc.synth(70_001, 31)
+    hist = orc.synth(max(ntaps - 1, 1), 77)[: ntaps - 1]
+    y, hout = run_fir(torch, plan, x, x.size, hist=hist if ntaps > 1 else None)
+    y_ref, h_ref = orc.fir_ccf(x, h, hist=hist if ntaps > 1 else None, return_hist=True)
+    ok, err, scale = orc.tol_ok(y, y_ref)
+    assert ok, (ntaps, err, scale)
+    np.testing.assert_array_equal(hout, h_ref)
+    # the error class of exact fp32: no worse than twice the fp32 direct form's
+    yd, _ = run_fir(torch, nsh.FirPlan(h, 1, nsh.FIR_DIRECT), x, x.size, hist=hist if ntaps > 1 else None)
+    _, err_d, _ = orc.tol_ok(yd, y_ref)
+    assert err <= max(2 * err_d, 1e-7 * scale), (err, err_d, scale)
+
+
+def test_fir_mfma_f32_nonfinite_and_range(torch_cuda):
+    """inf/NaN chunks take the fp32 direct form inside the launch (the zero-padded K would
+    make inf*0 = NaN): the non-finite pattern equals the oracle's; 1e+-30 and subnormal
+    samples need no scaling in fp32 and meet the tolerance."""
+    torch = torch_cuda
+    h = _firwin127()
+    x = orc.synth(60_000, 13)
+    x[1000] = np.complex64(complex(np.inf, 0.5))
+    x[30_000] = np.complex64(complex(0.25, np.nan))
+    x[40_000:41_000] *= np.float32(1e30)
+    x[50_000:51_000] *= np.float32(1e-40)
+    plan = nsh.FirPlan(h, 1, nsh.FIR_MFMA_F32)
+    y, _ = run_fir(torch, plan, x, x.size)
+    ref = orc.fir_ccf(x, h)
+    for part in ("real", "imag"):
+        a, b = getattr(y, part), getattr(ref, part)
+        np.testing.assert_array_equal(np.isnan(a), np.isnan(b))
+        np.testing.assert_array_equal(np.isinf(a), np.isinf(b))
+    fin = np.isfinite(ref)
+    big = np.abs(ref[fin]).max()
+    assert np.all(np.abs(y[fin] - ref[fin]) <= 1e-5 * np.abs(ref[fin]) + 1e-6 * big)
