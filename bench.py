@@ -138,34 +138,50 @@ def run_c5(a, dist, backend, rank, world, device, torch, orc, nsr):
     transport = a.c5_transport if a.c5_transport != "default" else ("rccl" if own_gpus and world > 1 else "auto")
     res = {"layout": "G=%d stage groups x %d time shards" % (G, shards), "stages": "4 x fir_filter_ccf(firwin(127,0.45), D=2)",
            "samples_per_shard": n, "transport_requested": transport}
-    pipe = None
-    try:
-        pipe = nsr.C5Pipeline(taps, n_in, group=group, n_groups=G, device=device, first_index=first,
-                              base_port=base_port, transport=transport, buf_bytes=a.c5_buf_mib << 20)
-        for _ in range(a.c5_warmup):
-            pipe.run()
-        if dist is not None:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(a.c5_steps):
-            pipe.run()
-        torch.cuda.synchronize()
-        el = time.perf_counter() - t0
-        ok, err = True, 0.0
-        if pipe.last:
-            m = 4096
-            J = (first + n_in) // 16  # one past the last output (global output index)
-            lo = 16 * (J - m) - C5_HALO
-            y_ref = orc.synth(16 * m + C5_HALO, lo)
-            for _ in range(4):
-                y_ref = orc.fir_ccf(y_ref, taps, decim=2)
-            ok, err, _ = orc.tol_ok(pipe.tail(m), y_ref[-m:])
-        tr = pipe.transport()
-        status = 0.0
-    except Exception as e:  # reported, not fatal: the headline is already measured
-        el, ok, err, tr, status = 0.0, False, 0.0, "", 1.0
-        res["error_rank%d" % rank] = str(e)[:300]
+    # The leg runs in a daemon thread under a deadline (--c5-timeout): on the driver's first
+    # multi-GPU run it is the first execution of the RCCL edge transport, and a hang there must
+    # not cost the headline line. No collective is issued inside the thread (a rank stuck in it
+    # would pair its peers' collectives wrongly); each rank times its own runs, max over ranks.
+    box = {"pipe": None, "el": 0.0, "ok": False, "err": 0.0, "tr": "", "status": 2.0}
+
+    def leg():
+        try:
+            pipe = box["pipe"] = nsr.C5Pipeline(taps, n_in, group=group, n_groups=G, device=device, first_index=first,
+                                                base_port=base_port, transport=transport,
+                                                buf_bytes=a.c5_buf_mib << 20)
+            for _ in range(a.c5_warmup):
+                pipe.run()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(a.c5_steps):
+                pipe.run()
+            torch.cuda.synchronize()
+            box["el"] = time.perf_counter() - t0
+            ok, err = True, 0.0
+            if pipe.last:
+                m = 4096
+                J = (first + n_in) // 16  # one past the last output (global output index)
+                lo = 16 * (J - m) - C5_HALO
+                y_ref = orc.synth(16 * m + C5_HALO, lo)
+                for _ in range(4):
+                    y_ref = orc.fir_ccf(y_ref, taps, decim=2)
+                ok, err, _ = orc.tol_ok(pipe.tail(m), y_ref[-m:])
+            box.update(ok=ok, err=err, tr=pipe.transport(), status=0.0)
+        except Exception as e:  # reported, not fatal: the headline is already measured
+            box.update(status=1.0, error=str(e)[:300])
+
+    import threading
+
+    th = threading.Thread(target=leg, daemon=True)
+    th.start()
+    th.join(a.c5_timeout)
+    if th.is_alive():
+        box["error"] = "timed out after %.0f s" % a.c5_timeout
+        res["timed_out"] = True
+    el, ok, err, tr, status = box["el"], box["ok"], box["err"], box["tr"], box["status"]
+    if "error" in box:
+        res["error_rank%d" % rank] = box["error"]
+    pipe = None if th.is_alive() else box["pipe"]
     if dist is not None:
         dev_kind = "cuda" if backend == "nccl" else "cpu"
         v = torch.tensor([el, 0.0 if ok else 1.0, err, status], dtype=torch.float64, device=dev_kind)
@@ -184,6 +200,7 @@ def run_c5(a, dist, backend, rank, world, device, torch, orc, nsr):
     if pipe is not None:
         pipe.close()
     res["ok"] = status == 0.0
+    res["_abandoned_any"] = status == 2.0  # some rank's leg is still running: exit hard after the line
     if status == 0.0:
         res.update({"steps": a.c5_steps, "warmup": a.c5_warmup, "ms_per_step": round(el / a.c5_steps * 1e3, 3),
                     "value": round(shards * n * a.c5_steps / el / 1e6, 1), "unit": "MSamples/s (input, whole job)",
@@ -252,6 +269,7 @@ def main():
     ap.add_argument("--c5-warmup", type=int, default=2)
     ap.add_argument("--c5-buf-mib", type=int, default=64)
     ap.add_argument("--c5-transport", default="default", choices=["default", "auto", "rccl", "socket"])
+    ap.add_argument("--c5-timeout", type=float, default=120.0, help="deadline for the C5 leg (s)")
     ap.add_argument("--rank-check", action="store_true", help=argparse.SUPPRESS)  # launcher test (CPU, gloo)
     a = ap.parse_args()
 
@@ -403,11 +421,13 @@ def main():
                                              "launch size; not measured in this run" % src)
     fb.close()
 
+    abandoned = False
     if a.fp32_leg == "on" and a.algo == "auto":
         out["fp32_exact"] = run_fp32_leg(a, n, taps, first, device, barrier, dist, tdev, torch, orc, nsr, nsh)
 
     if a.c5 == "on" or (a.c5 == "auto" and world > 1):
         out["c5_pipeline"] = run_c5(a, dist, backend, rank, world, device, torch, orc, nsr)
+        abandoned = out["c5_pipeline"].pop("_abandoned_any")
 
     if rank == 0 and world == 1 and not a.no_cpu:
         ncpu = 1 << a.cpu_log2n
@@ -422,10 +442,13 @@ def main():
                       "scheduler_mt thread-per-block (4 threads; the FIR on one core), vmcircbuf 32768 B default buffers; "
                       "%.2f s on %s" % (a.cpu_log2n, secs, cpu_model()),
         }
-    if dist is not None:
+    if dist is not None and not abandoned:
         dist.barrier()
     if rank == 0:
         print(json.dumps(out), flush=True)
+    if abandoned:  # a hung pipeline leg: leave without joining it (the headline is printed)
+        sys.stderr.flush()
+        os._exit(0)
     if dist is not None:
         dist.destroy_process_group()
 
