@@ -95,7 +95,9 @@ public:
     bool writer_done() const override;
     bool reader_done() const override;
     void reset_flags() override;
-    // Tags live on the LOCAL ring; they are not carried over the process boundary.
+    // Tags live on the LOCAL ring; the tags of each DATA message's items travel with it (their
+    // offsets relative to the message's first item) and land on the receiving ring at the
+    // same items, so absolute offsets survive the process boundary.
     gr::buffer* tag_target() override { return _buffer ? _buffer.get() : this; }
 
     void buffer_ready() override; // connect, handshake, start the receive thread

@@ -44,6 +44,83 @@ struct hello {
 };
 using clk = std::chrono::steady_clock;
 double since(clk::time_point t0) { return std::chrono::duration<double>(clk::now() - t0).count(); }
+
+// ---- tags on the wire: the tags of a DATA message's items travel with it ----------------
+// record = u64 offset relative to the message's first item, then key, value, srcid as
+// [u8 variant index | 255 = null][payload]; payloads: bool u8, int64 / double 8 B, string
+// and float vector u32 count + bytes (the PMT stand-in's value types, pmtf.hpp).
+template <class T>
+void put_raw(std::string& b, const T& v)
+{
+    b.append(reinterpret_cast<const char*>(&v), sizeof(T));
+}
+void put_pmt(std::string& b, const pmtf::pmt_sptr& p)
+{
+    if (!p) {
+        b.push_back((char)255);
+        return;
+    }
+    const auto& v = p->value();
+    b.push_back((char)v.index());
+    switch (v.index()) {
+    case 0: break;
+    case 1: b.push_back(std::get<bool>(v) ? 1 : 0); break;
+    case 2: put_raw(b, std::get<int64_t>(v)); break;
+    case 3: put_raw(b, std::get<double>(v)); break;
+    case 4: {
+        const auto& str = std::get<std::string>(v);
+        put_raw(b, (uint32_t)str.size());
+        b.append(str);
+        break;
+    }
+    case 5: {
+        const auto& f = std::get<std::vector<float>>(v);
+        put_raw(b, (uint32_t)f.size());
+        b.append(reinterpret_cast<const char*>(f.data()), f.size() * sizeof(float));
+        break;
+    }
+    }
+}
+struct reader {
+    const std::string& b;
+    size_t i = 0;
+    template <class T>
+    T raw()
+    {
+        if (i + sizeof(T) > b.size()) throw std::runtime_error("remote edge: truncated tag record");
+        T v;
+        std::memcpy(&v, b.data() + i, sizeof(T));
+        i += sizeof(T);
+        return v;
+    }
+    pmtf::pmt_sptr pmt()
+    {
+        const uint8_t k = raw<uint8_t>();
+        switch (k) {
+        case 255: return nullptr;
+        case 0: return std::make_shared<pmtf::pmt_base>();
+        case 1: return pmtf::make(raw<uint8_t>() != 0);
+        case 2: return pmtf::make(raw<int64_t>());
+        case 3: return pmtf::make(raw<double>());
+        case 4: {
+            const uint32_t n = raw<uint32_t>();
+            if (i + n > b.size()) throw std::runtime_error("remote edge: truncated tag record");
+            std::string str(b.data() + i, n);
+            i += n;
+            return pmtf::make(std::move(str));
+        }
+        case 5: {
+            const uint32_t n = raw<uint32_t>();
+            if (i + (size_t)n * sizeof(float) > b.size()) throw std::runtime_error("remote edge: truncated tag record");
+            std::vector<float> f(n);
+            std::memcpy(f.data(), b.data() + i, (size_t)n * sizeof(float));
+            i += (size_t)n * sizeof(float);
+            return pmtf::make(std::move(f));
+        }
+        default: throw std::runtime_error("remote edge: bad tag value type");
+        }
+    }
+};
 } // namespace
 
 // ---- control / data socket ------------------------------------------------------------
@@ -100,9 +177,9 @@ public:
     }
     // message + payload as one unit with respect to other senders on this socket
     template <typename F>
-    void send_msg_with(uint32_t type, uint64_t n, F&& payload)
+    void send_msg_with(uint32_t type, uint64_t n, F&& payload, uint32_t aux = 0)
     {
-        msg m{ type, 0, n };
+        msg m{ type, aux, n };
         std::lock_guard<std::mutex> g(_send_m);
         send_bytes(&m, sizeof(m));
         payload();
@@ -579,6 +656,24 @@ void domain_adapter_remote::recv_loop()
         if (m.type != M_DATA) throw std::runtime_error("remote edge: unexpected message");
         const int n = (int)m.n;
         const size_t bytes = (size_t)n * _isz;
+        std::vector<tag_t> tags; // m.aux tags, offsets relative to this message's first item
+        if (m.aux) {
+            const uint32_t len = [&] {
+                uint32_t l = 0;
+                if (!_ch->recv_bytes(&l, sizeof(l))) throw std::runtime_error("remote edge: peer closed in tags");
+                return l;
+            }();
+            std::string blob(len, '\0');
+            if (len && !_ch->recv_bytes(&blob[0], len)) throw std::runtime_error("remote edge: peer closed in tags");
+            reader rd{ blob };
+            for (uint32_t k = 0; k < m.aux; ++k) {
+                const uint64_t rel = rd.raw<uint64_t>();
+                auto key = rd.pmt();
+                auto value = rd.pmt();
+                auto srcid = rd.pmt();
+                tags.emplace_back(rel, std::move(key), std::move(value), std::move(srcid));
+            }
+        }
         // Data after the k-th DONE belongs to run k+1: it waits until this process has
         // started that run (so runs do not mix), then for n contiguous writable items, or
         // is discarded if this run's reader has already finished.
@@ -620,6 +715,11 @@ void domain_adapter_remote::recv_loop()
             continue;
         }
         _tr->recv(*_ch, dst, bytes);
+        const uint64_t w0 = _buffer->total_written(); // the items' absolute offsets start here
+        for (auto& t : tags) {
+            t.offset += w0;
+            _buffer->add_tag(std::move(t));
+        }
         _buffer->post_write(n);
         _moved.fetch_add((uint64_t)n);
         notify_downstream();
@@ -634,8 +734,28 @@ void domain_adapter_remote::pump()
         buffer_info_t ri{};
         if (!_buffer->read_info(ri) || ri.n_items <= 0) break;
         const int m = std::min(ri.n_items, _max_chunk);
-        _ch->send_msg_with(remote::M_DATA, (uint64_t)m, [&] { _tr->send(*_ch, ri.ptr, (size_t)m * _isz); });
-        _buffer->prune_tags(m); // tags do not cross processes; drop them with their items
+        // the tags of these m items travel in the same message (offsets relative to its first item)
+        const uint64_t r0 = _buffer->total_read();
+        const auto tags = _buffer->tags_in_window(0, (uint64_t)m);
+        std::string blob;
+        for (auto& t : tags) {
+            remote::put_raw(blob, (uint64_t)(t.offset - r0));
+            remote::put_pmt(blob, t.key);
+            remote::put_pmt(blob, t.value);
+            remote::put_pmt(blob, t.srcid);
+        }
+        _ch->send_msg_with(
+            remote::M_DATA, (uint64_t)m,
+            [&] {
+                if (!tags.empty()) {
+                    const uint32_t len = (uint32_t)blob.size();
+                    _ch->send_bytes(&len, sizeof(len));
+                    _ch->send_bytes(blob.data(), blob.size());
+                }
+                _tr->send(*_ch, ri.ptr, (size_t)m * _isz);
+            },
+            (uint32_t)tags.size());
+        _buffer->prune_tags(m); // sent with their items
         _buffer->post_read(m);
         _moved.fetch_add((uint64_t)m);
     }

@@ -10,8 +10,11 @@
 #include "qa_ref.hpp"
 
 #include <cstdlib>
+#include <gnuradio/blocklib/blocks/annotator.hpp>
 #include <gnuradio/blocklib/blocks/copy.hpp>
 #include <gnuradio/blocklib/blocks/head.hpp>
+#include <gnuradio/blocklib/blocks/null_sink.hpp>
+#include <gnuradio/blocklib/blocks/null_source.hpp>
 #include <gnuradio/blocklib/blocks/multiply_const.hpp>
 #include <gnuradio/blocklib/blocks/vector_sink.hpp>
 #include <gnuradio/blocklib/blocks/vector_source.hpp>
@@ -19,6 +22,7 @@
 #include <gnuradio/blocklib/hip/fir_filter_ccf.hpp>
 #include <gnuradio/blocklib/hip/multiply_const.hpp>
 #include <gnuradio/blocklib/hip/synth_source.hpp>
+#include <gnuradio/domain_adapter_direct.hpp>
 #include <gnuradio/domain_adapter_remote.hpp>
 #include <gnuradio/flowgraph.hpp>
 #include <gnuradio/hip_buffer.hpp>
@@ -73,6 +77,50 @@ TEST(RemoteCpu, ChainRestart)
         if (rank() == 1) {
             if (snk->data().size() != n) std::fprintf(stderr, "  run %d: %zu items\n", run, snk->data().size());
             EXPECT_TRUE(snk->data() == ref);
+        }
+    }
+}
+
+// Tags across processes (reference qa_tags.cpp AcrossDomains shape, here over a process
+// boundary): src -> head -> ann0 [0] ~~> copy -> ann1 -> sink [1]. ann1 must see ann0's 4 tags
+// at their absolute offsets with their values and srcid, in each of two runs (the edge
+// counters keep counting across runs, on both sides alike).
+TEST(RemoteCpu, TagsCrossProcesses)
+{
+    const int N = 40000;
+    auto src = blocks::null_source::make(sizeof(gr_complex));
+    auto head = blocks::head::make(sizeof(gr_complex), N);
+    auto ann0 = blocks::annotator::make(10000, sizeof(gr_complex), 1, 1, tag_propagation_policy_t::TPP_ALL_TO_ALL);
+    auto cp = blocks::copy::make(sizeof(gr_complex));
+    auto ann1 = blocks::annotator::make(1u << 30, sizeof(gr_complex), 1, 1, tag_propagation_policy_t::TPP_ALL_TO_ALL);
+    auto snk = blocks::null_sink::make(sizeof(gr_complex));
+    ann0->set_alias("ann0");
+    auto fg = flowgraph::make();
+    fg->connect(src, 0, head, 0);
+    fg->connect(head, 0, ann0, 0);
+    fg->connect(ann0, 0, cp, 0);
+    fg->connect(cp, 0, ann1, 0);
+    fg->connect(ann1, 0, snk, 0);
+    auto s0 = sched_for(0, schedulers::scheduler_mt::make("r0", 8192));
+    auto s1 = sched_for(1, schedulers::scheduler_mt::make("r1", 8192));
+    fg->set_schedulers({ s0, s1 });
+    auto o = opts();
+    o.base_port += 60;
+    auto da = domain_adapter_remote_conf::make(o);
+    domain_conf_vec dc{ domain_conf(s0, { src, head, ann0 }, da), domain_conf(s1, { cp, ann1, snk }, da) };
+    fg->partition(dc);
+    for (int run = 0; run < 2; ++run) {
+        fg->run();
+        if (rank() == 1) {
+            auto seen = ann1->data();
+            ASSERT_TRUE(seen.size() == 4u * (run + 1));
+            for (size_t i = 0; i < 4; ++i) {
+                const auto& t = seen[4 * run + i];
+                EXPECT_EQ(t.offset, (uint64_t)(N * run + 10000 * i));
+                EXPECT_TRUE(std::get<int64_t>(t.value->value()) == (int64_t)(4 * run + i));
+                EXPECT_TRUE(std::get<std::string>(t.key->value()) == "seq");
+                EXPECT_TRUE(t.srcid && std::get<std::string>(t.srcid->value()) == "ann0");
+            }
         }
     }
 }
@@ -171,6 +219,50 @@ TEST(RemoteGpu, DeviceChainRestart)
             if (snk->data().size() != n) std::fprintf(stderr, "  run %d: %zu items\n", run, snk->data().size());
             EXPECT_TRUE(snk->data() == ref);
         }
+    }
+}
+
+// Tags through device rings and a process crossing: host annotator -[H2D]-> hip::copy [0]
+// ~~(device rings; staged or RCCL)~~> hip::copy -[D2H]-> host annotator [1].
+TEST(RemoteGpu, DeviceTags)
+{
+    const int N = 1 << 20;
+    auto src = blocks::null_source::make(sizeof(gr_complex));
+    auto head = blocks::head::make(sizeof(gr_complex), N);
+    auto ann0 = blocks::annotator::make(1u << 18, sizeof(gr_complex), 1, 1, tag_propagation_policy_t::TPP_ALL_TO_ALL);
+    auto c0 = hip::copy::make(1);
+    auto c1 = hip::copy::make(1);
+    auto ann1 = blocks::annotator::make(1u << 30, sizeof(gr_complex), 1, 1, tag_propagation_policy_t::TPP_ALL_TO_ALL);
+    auto snk = blocks::null_sink::make(sizeof(gr_complex));
+    auto fg = flowgraph::make();
+    fg->connect(src, 0, head, 0);
+    fg->connect(head, 0, ann0, 0);
+    fg->connect(ann0, 0, c0, 0)->set_custom_buffer(HIP_BUFFER_ARGS_H2D);
+    fg->connect(c0, 0, c1, 0);
+    fg->connect(c1, 0, ann1, 0)->set_custom_buffer(HIP_BUFFER_ARGS_D2H);
+    fg->connect(ann1, 0, snk, 0);
+    auto s0 = sched_for(0, schedulers::scheduler_mt::make("h0", 1u << 20));
+    auto g0 = sched_for(0, schedulers::scheduler_hip::make("g0", 0, 1u << 20));
+    auto g1 = sched_for(1, schedulers::scheduler_hip::make("g1", 0, 1u << 20));
+    auto s1 = sched_for(1, schedulers::scheduler_mt::make("h1", 1u << 20));
+    fg->set_schedulers({ s0, g0, g1, s1 });
+    auto o = opts();
+    o.base_port += 70;
+    auto da = domain_adapter_remote_conf::make(o);
+    auto dd = domain_adapter_direct_conf::make(buffer_preference_t::DOWNSTREAM);
+    // a crossing takes its downstream domain's conf: only g1's is the remote one
+    domain_conf_vec dc{ domain_conf(s0, { src, head, ann0 }, dd), domain_conf(g0, { c0 }, dd),
+                        domain_conf(g1, { c1 }, da), domain_conf(s1, { ann1, snk }, dd) };
+    fg->partition(dc);
+    fg->run();
+    if (rank() == 1) {
+        auto seen = ann1->data();
+        ASSERT_TRUE(seen.size() == 4u);
+        for (size_t i = 0; i < 4; ++i) {
+            EXPECT_EQ(seen[i].offset, (uint64_t)((1u << 18) * i));
+            EXPECT_TRUE(std::get<int64_t>(seen[i].value->value()) == (int64_t)i);
+        }
+        EXPECT_EQ(snk->consumed(), (uint64_t)N);
     }
 }
 

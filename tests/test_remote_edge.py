@@ -60,12 +60,13 @@ def run_pair(case, timeout=120):
 
 
 @pytest.mark.parametrize("case", ["RemoteCpu.ChainRestart", "RemoteCpu.TwoCrossingsBothWays",
-                                  "RemoteCpu.ReaderFinishesFirst"])
+                                  "RemoteCpu.ReaderFinishesFirst", "RemoteCpu.TagsCrossProcesses"])
 def test_remote_edges_cpu(case):
     run_pair(case)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", ["RemoteGpu.DeviceChainRestart", "RemoteGpu.DecimatingPipelineC5"])
+@pytest.mark.parametrize("case", ["RemoteGpu.DeviceChainRestart", "RemoteGpu.DecimatingPipelineC5",
+                                  "RemoteGpu.DeviceTags"])
 def test_remote_edges_gpu(case):
     run_pair(case, timeout=300)
