@@ -148,6 +148,27 @@ int nsh_fir_cascade2_supported(void* plan1, void* plan2);
 int nsh_fir_cascade2_ccf(void* plan1, void* plan2, const float* in, const float* hist1_in, float* hist1_out,
                          const float* hist2_in, float* hist2_out, float* out, int64_t n_out, void* stream);
 
+/* Decimating FIR chain in one pass (the fused form of nstages fir_filter_ccf(h_s, D_s) blocks in
+ * a chain; BASELINE config C5 = 4 x fir_filter_ccf(firwin(127, 0.45), 2); replaces nstages
+ * nsh_fir_ccf calls and the intermediate streams). The chain composes into one decimating filter
+ *   y[m] = sum_n heq[n] x[m D - n],   D = prod D_s,   heq = h_1 * (h_2 up D_1) * (h_3 up D_1 D_2) ...
+ * (composed in double at plan creation), computed by polyphase-FFT overlap-save
+ * (k_fir_pfft<D>, D = 8 or 16; ceil((len(heq) - 1) / D) <= 256). Per call: in = n_out * D
+ * samples; hist_in / hist_out = nsh_fir_cascade_hist_len(plan) = len(heq) - 1 input samples, as
+ * for nsh_fir_ccf (NULL hist_in reads as zeros; hist_out may be NULL; no aliasing). A chain whose
+ * stages all start from zero history is equivalent to this plan from a zero history. Outputs are
+ * within fp32 transform rounding of the chain (C5: 2.2e-7 of max|y| against the oracle's
+ * double-accumulated chain; tolerance 1e-5); frames holding inf/NaN are computed by the fp32
+ * direct form on heq (non-finite outputs exactly where the chain's are). */
+int nsh_fir_cascade_plan_create(int dev, const float* const* taps_host, const int* ntaps, const int* decims,
+                                int nstages, void** plan);
+int nsh_fir_cascade_plan_destroy(void* plan);
+int nsh_fir_cascade_decim(void* plan);         /* D = prod D_s */
+int nsh_fir_cascade_hist_len(void* plan);      /* len(heq) - 1 */
+const char* nsh_fir_cascade_kernel(void* plan); /* "k_fir_pfft<16>" */
+int nsh_fir_cascade_ccf(void* plan, const float* in, const float* hist_in, float* hist_out, float* out,
+                        int64_t n_out, void* stream);
+
 /* ---- FFT (fft_vcc, 1024-point, unnormalised both ways) ------------------------------
  * frames of 1024 complex samples; inverse=1 computes sum_k X[k] e^{+2 pi i kn/1024}
  * (= 1024 * numpy.fft.ifft). nsh_channelizer1024 fuses fft -> multiply by w[1024]

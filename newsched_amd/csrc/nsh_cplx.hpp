@@ -1,0 +1,60 @@
+// Complex arithmetic on packed (re, im) pairs and wave reductions shared by the FFT-based
+// kernels (nsh_fft.hip, nsh_fir_pfft.hip). gfx950 only.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace nsh {
+
+// A complex value is a packed pair (re, im): adds are one v_pk_add_f32, a twiddle multiply is
+// one v_pk_mul_f32 + one v_pk_fma_f32 with the swizzles/negations as operand modifiers. (Written
+// on HIP's float2 struct, the compiler packed the same arithmetic itself but built the operand
+// pairs with ~380 v_mov per channelizer frame, a third of its VALU issue.)
+typedef float cf __attribute__((ext_vector_type(2)));
+
+// a * w with a fused second product: re = fma(-a.y, w.y, a.x w.x), im = fma(a.y, w.x, a.x w.y)
+__device__ __forceinline__ cf cmulw(cf a, cf w)
+{
+    return __builtin_elementwise_fma(a.yy, cf{ -w.y, w.x }, a.xx * w);
+}
+// a * conj(w): re = fma(a.y, w.y, a.x w.x), im = fma(a.y, w.x, -a.x w.y)
+__device__ __forceinline__ cf cmulc(cf a, cf w)
+{
+    return __builtin_elementwise_fma(a.yy, w.yx, a.xx * cf{ w.x, -w.y });
+}
+// multiply by -i (forward) or +i (inverse)
+template <bool INV>
+__device__ __forceinline__ cf rot(cf a)
+{
+    return INV ? cf{ -a.y, a.x } : cf{ a.y, -a.x };
+}
+
+// In-place DFT4 of (a, b, c, d): X_k = sum_n x_n W_4^{nk}, W_4 = e^{-+i pi/2}.
+template <bool INV>
+__device__ __forceinline__ void dft4(cf& a, cf& b, cf& c, cf& d)
+{
+    const cf s0 = a + c, d0 = a - c;
+    const cf s1 = b + d, t = b - d;
+    a = s0 + s1;
+    c = s0 - s1;
+    // d0 -+ i t as one packed fma each: t swapped by op_sel, (1, -1) = 1.0 with neg_hi; a
+    // multiply by 1 is exact, so this rounds exactly as d0 + rot(t) (the compiler emitted rot()
+    // as a v_xor + v_mov pair before each add)
+    const cf pm = INV ? cf{ -1.f, 1.f } : cf{ 1.f, -1.f };
+    b = __builtin_elementwise_fma(t.yx, pm, d0);
+    d = __builtin_elementwise_fma(t.yx, -pm, d0);
+}
+
+// Wave-wide unsigned max, uniform result: DPP within each 16-lane row (quad_perm xor 1, xor 2,
+// row_ror 4, 8: VALU, no LDS) then the four row results by v_readlane.
+__device__ __forceinline__ unsigned wave_umax(unsigned v)
+{
+    v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xf, 0xf, false));  // quad_perm [1,0,3,2]
+    v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xf, 0xf, false));  // quad_perm [2,3,0,1]
+    v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xf, 0xf, false)); // row_ror:4
+    v = max(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xf, 0xf, false)); // row_ror:8
+    const unsigned a = (unsigned)__builtin_amdgcn_readlane((int)v, 0), b = (unsigned)__builtin_amdgcn_readlane((int)v, 16);
+    const unsigned c = (unsigned)__builtin_amdgcn_readlane((int)v, 32), d = (unsigned)__builtin_amdgcn_readlane((int)v, 48);
+    return max(max(a, b), max(c, d));
+}
+
+} // namespace nsh

@@ -21,6 +21,7 @@
 // indices j + 64 m (m < 16), exactly pass 1's input layout, so a frame crosses HBM once
 // each way (16 B/sample instead of 48 B unfused) and LDS twice per transform.
 #include "nsh_common.hpp"
+#include "nsh_cplx.hpp"
 
 #include <cmath>
 #include <mutex>
@@ -31,17 +32,11 @@ namespace {
 constexpr int N = 1024;
 constexpr int NT = 256;
 
-// A complex value is a packed pair (re, im): adds are one v_pk_add_f32, a twiddle multiply is
-// one v_pk_mul_f32 + one v_pk_fma_f32 with the swizzles/negations as operand modifiers. (Written
-// on HIP's float2 struct, the compiler packed the same arithmetic itself but built the operand
-// pairs with ~380 v_mov per channelizer frame, a third of its VALU issue.)
-typedef float cf __attribute__((ext_vector_type(2)));
+using nsh::cf;
+using nsh::cmulw;
+using nsh::dft4;
+using nsh::rot;
 
-// a * w with a fused second product: re = fma(-a.y, w.y, a.x w.x), im = fma(a.y, w.x, a.x w.y)
-__device__ __forceinline__ cf cmulw(cf a, cf w)
-{
-    return __builtin_elementwise_fma(a.yy, cf{ -w.y, w.x }, a.xx * w);
-}
 // the channelizer's spectrum multiply: nsh_mul_const_vcc's two-product rounding exactly, so
 // the fused channelizer stays bit-identical to fft -> multiply_const_vcc -> ifft
 __device__ __forceinline__ cf cmul_rn(cf a, cf b)
@@ -50,25 +45,6 @@ __device__ __forceinline__ cf cmul_rn(cf a, cf b)
     const cf u = a.yy * b.yx; // (ay by, ay bx)
     return t + u * cf{ -1.f, 1.f }; // (ax bx - ay by, ax by + ay bx): exact sign flip, one rounding
 }
-// multiply by -i (forward) or +i (inverse)
-template <bool INV>
-__device__ __forceinline__ cf rot(cf a)
-{
-    return INV ? cf{ -a.y, a.x } : cf{ a.y, -a.x };
-}
-
-// In-place DFT4 of (a, b, c, d): X_k = sum_n x_n W_4^{nk}, W_4 = e^{-+i pi/2}.
-template <bool INV>
-__device__ __forceinline__ void dft4(cf& a, cf& b, cf& c, cf& d)
-{
-    const cf s0 = a + c, d0 = a - c;
-    const cf s1 = b + d, d1 = rot<INV>(b - d);
-    a = s0 + s1;
-    c = s0 - s1;
-    b = d0 + d1;
-    d = d0 - d1;
-}
-
 // W_16^m, m = 0..9 (forward; conjugated for the inverse)
 template <bool INV>
 __device__ __forceinline__ cf w16(int m)

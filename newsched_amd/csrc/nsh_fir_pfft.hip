@@ -1,0 +1,497 @@
+// libnsh_hip.so: a chain of decimating FIRs in one pass over HBM -- the fused form of
+// fir_filter_ccf(h_1, D_1) -> ... -> fir_filter_ccf(h_S, D_S) (BASELINE config C5:
+// 4 x fir_filter_ccf(firwin(127, 0.45), 2)), by polyphase-FFT overlap-save on the composite
+// filter. No reference counterpart (the reference has no FIR block); the block
+// convention is the one nsh_fir_ccf and the oracle follow (oracle/nsh_oracle.c orc_fir_ccf):
+//   y_s[m] = sum_k h_s[k] y_{s-1}[m D_s - k]
+// which composes exactly (in real arithmetic) into one decimating filter
+//   y[m] = sum_n heq[n] x[m D - n],  D = prod D_s,  heq = h_1 * (h_2 up D_1) * (h_3 up D_1 D_2) * ...
+// (4 x (127, 2): D = 16, 1891 composite taps). heq is composed in double on the host.
+//
+// Algorithm (P = D phases, M = 512): a frame is P*M consecutive input samples
+// u[t] = x[P (j0 - Q) + t], Q = ceil((Leq - 1) / P); its decimated circular convolution
+//   c[q] = sum_p (u_p (*) g_p)[q],  u_p[n] = u[P n + p],  g_p[q'] = heq[P q' - p]   (512-periodic)
+// equals the linear output y[j0 + q - Q] for q >= Q, i.e. V = M - Q outputs per frame
+// (C5: Q = 119, V = 393), frames hopping by V rows of P samples. In frequency:
+//   c = IFFT_512( sum_p FFT_512(u_p) . F_p ),   F_p = FFT_512(g_p) / 512   (host, double -> fp32)
+// so a frame costs P forward 512-point FFTs, a P-term complex MAC per bin and one inverse
+// FFT -- about 60 FLOP per input sample instead of the cascade's ~480 (direct or Toeplitz).
+//
+// Kernel k_fir_pfft<P>: one workgroup of P waves per CU, walking a contiguous range of frames.
+//   * LDS ring of M rows x P samples (row = one P-sample input row, XOR-swizzled so that wave p
+//     reading phase p of 64 consecutive rows is bank-conflict-free); a frame shares Q rows with
+//     the previous one, so each input sample is read from HBM once (plus Q rows at the start of
+//     the workgroup's range). The next frame's V new rows are prefetched into registers (16-B
+//     nontemporal buffer loads) one frame ahead and written into the rows the current frame
+//     has finished with.
+//   * wave p: its 512 phase samples -> registers (scaled by 2^k, below) -> radix-8 Stockham FFT
+//     (3 passes, two exchanges through a wave-private padded LDS image, no barrier) -> times
+//     F_p (held in registers for the whole launch) -> its image.
+//   * barrier; waves 0..7 sum the P images per bin in a fixed order (deterministic) into Z;
+//     every wave writes its share of the next frame's rows; barrier.
+//   * wave (frame mod P) runs the inverse FFT of Z from LDS and stores the V valid outputs
+//     (nontemporal 8-B stores); the other waves go on with the next frame meanwhile.
+// Scale: the frame's input is multiplied by 2^k (k from the frame's largest magnitude, reduced
+// per wave over the rows as they arrive) so that it lies in [1, 2) before the transforms, and
+// the outputs by 2^-k: exact power-of-two scaling, so no finite input overflows or loses
+// precision to fp32's range. A frame holding inf or NaN is computed by the fp32 direct form on
+// the composite taps in the same launch (its non-finite outputs sit exactly where the
+// cascade's do: the composite support is the cascade's).
+// Accuracy: fp32 transforms, error ~1e-7 of the frame's RMS (C5: 2.2e-7 of max|y| vs the
+// oracle's double-accumulated cascade; north-star tolerance 1e-5).
+#include "nsh_common.hpp"
+#include "nsh_cplx.hpp"
+
+#include <cmath>
+#include <mutex>
+#include <set>
+#include <string>
+#include <utility>
+#include <vector>
+
+namespace {
+
+using nsh::cf;
+using nsh::cmulw;
+using nsh::dft4;
+using nsh::rot;
+
+constexpr int M = 512;          // FFT length per phase
+constexpr int IMG = M + M / 8;  // a wave's padded LDS image (one pad entry per 8)
+
+__device__ __forceinline__ int ipad(int i) { return i + (i >> 3); }
+
+// ring entry of (slot s, phase p): rows of P samples, phase XOR-swizzled by (s / (32 / P)) so
+// that 32 consecutive slots read at one phase hit 32 distinct bank pairs
+template <int P>
+__device__ __forceinline__ int ring_at(int s, int p)
+{
+    return s * P + (p ^ ((s / (32 / P)) & (P - 1)));
+}
+
+// In-place DFT8, natural order in and out: X[k] = E[k] + W_8^k O[k], X[k + 4] = E[k] - W_8^k O[k]
+template <bool INV>
+__device__ __forceinline__ void dft8(cf (&v)[8])
+{
+    constexpr float R2 = 0.70710678118654757f;
+    dft4<INV>(v[0], v[2], v[4], v[6]); // E[0..3] in v[0], v[2], v[4], v[6]
+    dft4<INV>(v[1], v[3], v[5], v[7]); // O[0..3] in v[1], v[3], v[5], v[7]
+    const cf w1 = cf{ R2, INV ? R2 : -R2 }, w3 = cf{ -R2, INV ? R2 : -R2 };
+    const cf o1 = cmulw(v[3], w1), o2 = rot<INV>(v[5]), o3 = cmulw(v[7], w3);
+    const cf e0 = v[0], e1 = v[2], e2 = v[4], e3 = v[6], o0 = v[1];
+    v[0] = e0 + o0;
+    v[4] = e0 - o0;
+    v[1] = e1 + o1;
+    v[5] = e1 - o1;
+    v[2] = e2 + o2;
+    v[6] = e2 - o2;
+    v[3] = e3 + o3;
+    v[7] = e3 - o3;
+}
+
+// A wave's image addresses: pass-1 stores at b1 + r (= ipad(8 j + r)), pass-2 stores at b3 + 9 r
+// (= ipad((j >> 3) 64 + (j & 7) + 8 r)), natural-order loads/stores at b2 + 72 r (= ipad(j + 64 r)):
+// one base register each, the rest immediate offsets.
+struct img_bases {
+    cf* b1;
+    cf* b2;
+    cf* b3;
+};
+__device__ __forceinline__ img_bases bases_of(cf* img)
+{
+    const int j = threadIdx.x & 63;
+    return img_bases{ img + 9 * j, img + j + (j >> 3), img + (j >> 3) * 72 + (j & 7) };
+}
+
+// Forward 512-point transform of the values v[r] = x[lane + 64 r] of one wave (Stockham, radix
+// 8, three passes); on return v[r] = X[lane + 64 r]. t2[r] = W_64^{(lane & 7) r},
+// t3[r] = W_512^{lane r}. The image is this wave's own: no workgroup barrier. (The inverse
+// transform is conj(FFT(conj(.))), the conjugations folded into the neighbouring operations.)
+__device__ __forceinline__ void fft512_wave(cf (&v)[8], const img_bases& ib, const cf (&t2)[8], const cf (&t3)[8])
+{
+    dft8<false>(v); // pass 1 (Ns = 1) -> dst[8 j + r]
+#pragma unroll
+    for (int r = 0; r < 8; ++r) ib.b1[r] = v[r];
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int r = 0; r < 8; ++r) v[r] = ib.b2[72 * r];
+#pragma unroll
+    for (int r = 1; r < 8; ++r) v[r] = cmulw(v[r], t2[r]);
+    dft8<false>(v); // pass 2 (Ns = 8) -> dst[(j >> 3) 64 + (j & 7) + 8 r]
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int r = 0; r < 8; ++r) ib.b3[9 * r] = v[r];
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int r = 0; r < 8; ++r) v[r] = ib.b2[72 * r];
+#pragma unroll
+    for (int r = 1; r < 8; ++r) v[r] = cmulw(v[r], t3[r]);
+    dft8<false>(v); // pass 3 (Ns = 64) -> X[j + 64 r], kept in registers
+    __builtin_amdgcn_wave_barrier(); // the image is rewritten next
+}
+
+__device__ __forceinline__ float2 virt(const float2* __restrict__ in, const float2* __restrict__ hist, int64_t g,
+                                       int64_t n_in, int L)
+{
+    if (g >= 0) return g < n_in ? in[g] : make_float2(0.f, 0.f);
+    if (g >= -(int64_t)(L - 1)) return hist ? hist[g + (L - 1)] : make_float2(0.f, 0.f); // null: zeros
+    return make_float2(0.f, 0.f);
+}
+
+__device__ __forceinline__ unsigned absbits(float v) { return __float_as_uint(v) & 0x7fffffffu; }
+__device__ __forceinline__ unsigned maxbits4(const float4& v)
+{
+    return max(max(absbits(v.x), absbits(v.y)), max(absbits(v.z), absbits(v.w)));
+}
+
+// raw buffer resource over [base, base + items) (items clamped to [0, cap]): loads past the end
+// return 0, stores past it are dropped
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t span_rsrc(const float2* base, int64_t items, int64_t cap)
+{
+    items = items < 0 ? 0 : (items > cap ? cap : items);
+    const uint64_t a = (uint64_t)base;
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+    const int bytes = __builtin_amdgcn_readfirstlane((int)(items * 8));
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0, bytes, 0x00020000);
+}
+
+struct pfft_args {
+    const float2* x;
+    const float2* hist_in;
+    float2* hist_out;
+    float2* out;
+    int64_t n_out;
+    const float2* F;   // [P][M]: FFT_512(g_p) / 512
+    const float2* tw;  // [M]: e^{-2 pi i t / 512}
+    const float* heq;  // [L] composite taps (fp32), for frames with inf/NaN
+    int L;
+    int Q;
+    int V;
+    int64_t nf;        // frames in the launch
+    int64_t fpw;       // frames per workgroup
+};
+
+constexpr int PRE = 4; // 16-B prefetch slots per thread: V rows x P samples / 2 / (64 P) <= 4
+
+template <int P>
+__device__ __forceinline__ void load_rows(float4 (&pre)[PRE], const pfft_args& a, int64_t n_in, int64_t fn)
+{
+    // window fn's new rows = x[P fn V, P (fn + 1) V)
+    const int64_t b = (int64_t)P * fn * a.V;
+    const __amdgpu_buffer_rsrc_t r = span_rsrc(a.x + b, n_in - b, (int64_t)P * a.V);
+#pragma unroll
+    for (int k = 0; k < PRE; ++k) pre[k] = nsh::buf_load_f4(r, (int)(threadIdx.x + 64 * P * k) * 16);
+}
+
+// write the prefetched rows of window fn into the ring; returns this thread's max magnitude bits.
+// Slot k of thread t holds samples 2 i, 2 i + 1, i = t + 64 P k: rows (2 t) / P + 128 k, phases
+// (2 t) % P and + 1 -- one swizzle for every k (128 k / (32 / P) is a multiple of P), so each
+// ring entry is one of two bases plus 128 P k, modulo the ring.
+template <int P>
+__device__ __forceinline__ unsigned store_rows(const float4 (&pre)[PRE], cf* __restrict__ ring, const pfft_args& a, int64_t fn)
+{
+    const int items = P * a.V / 2;
+    const int t = threadIdx.x;
+    const int s0 = (int)((fn * a.V + a.Q + (2 * t) / P) & (M - 1)), ph = (2 * t) % P;
+    const int ea = ring_at<P>(s0, ph), eb = ring_at<P>(s0, ph + 1);
+    unsigned m = 0;
+#pragma unroll
+    for (int k = 0; k < PRE; ++k) {
+        if (t + 64 * P * k < items) {
+            ring[(ea + 128 * P * k) & (M * P - 1)] = cf{ pre[k].x, pre[k].y };
+            ring[(eb + 128 * P * k) & (M * P - 1)] = cf{ pre[k].z, pre[k].w };
+            m = max(m, maxbits4(pre[k]));
+        }
+    }
+    return m;
+}
+
+template <int P>
+__global__ __launch_bounds__(64 * P, 1) void k_fir_pfft(pfft_args a)
+{
+    constexpr int NT = 64 * P;
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    cf* ring = reinterpret_cast<cf*>(lds);   // M * P
+    cf* imgs = ring + M * P;                  // P * IMG
+    cf* zb = imgs + P * IMG;                  // IMG
+    unsigned* mx = reinterpret_cast<unsigned*>(zb + IMG); // [2][P] per-wave max bits of new rows
+
+    const int tid = threadIdx.x, j = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6); // wave-uniform: SGPR arithmetic
+    const int64_t f0 = (int64_t)blockIdx.x * a.fpw;
+    const int64_t f1 = min(a.nf, f0 + a.fpw);
+    if (f0 >= f1) return; // whole workgroup
+    const int64_t n_in = a.n_out * P;
+    const int L = a.L, Q = a.Q, V = a.V;
+    const img_bases ib = bases_of(imgs + w * IMG);
+
+    if (a.hist_out && blockIdx.x == gridDim.x - 1) // the next call's history: the L-1 samples before x[n_in]
+        for (int k = tid; k < L - 1; k += NT) a.hist_out[k] = virt(a.x, a.hist_in, n_in - (L - 1) + k, n_in, L);
+
+    cf t2[8], t3[8], fw[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        const float2 u = a.tw[8 * (((j & 7) * r) & 63)], v = a.tw[(j * r) & (M - 1)];
+        t2[r] = cf{ u.x, u.y };
+        t3[r] = cf{ v.x, v.y };
+        const float2 f = a.F[w * M + j + 64 * r];
+        fw[r] = cf{ f.x, f.y };
+    }
+
+    // first window: rows [f0 V, f0 V + M), history-aware
+    unsigned m = 0;
+    for (int i = tid; i < M * P; i += NT) {
+        const float2 xv = virt(a.x, a.hist_in, (int64_t)P * (f0 * V - Q) + i, n_in, L);
+        const int s = (int)((f0 * V + i / P) & (M - 1));
+        ring[ring_at<P>(s, i % P)] = cf{ xv.x, xv.y };
+        m = max(m, max(absbits(xv.x), absbits(xv.y)));
+    }
+    m = nsh::wave_umax(m);
+    if (j == 0) {
+        mx[(f0 & 1) * P + w] = m;
+        mx[((f0 + 1) & 1) * P + w] = 0u;
+    }
+    float4 pre[PRE];
+    load_rows<P>(pre, a, n_in, f0 + 1);
+    nsh::lds_barrier();
+
+    for (int64_t f = f0; f < f1; ++f) {
+        // Re-define the per-lane constants each frame (empty asm): otherwise the compiler hoists
+        // the swizzled/negated copies that cmulw's operand modifiers give for free, i.e. holds
+        // every twiddle twice (the kernel has 128 VGPRs at 16 waves per CU).
+#pragma unroll
+        for (int r = 0; r < 8; ++r) asm volatile("" : "+v"(fw[r]));
+#pragma unroll
+        for (int r = 1; r < 8; ++r) asm volatile("" : "+v"(t2[r]), "+v"(t3[r]));
+        // the window's largest magnitude: this frame's new rows and the previous frame's (which
+        // hold the overlap; the first window's slot covers all of it)
+        unsigned wm = 0;
+#pragma unroll
+        for (int k = 0; k < 2 * P; k += 4) {
+            const uint4 u = *reinterpret_cast<const uint4*>(mx + k);
+            wm = max(wm, max(max(u.x, u.y), max(u.z, u.w)));
+        }
+        const bool bad = wm >= 0x7f800000u; // inf or NaN in the window
+        int ks = 127 - (int)(wm >> 23);      // max * 2^ks in [1, 2)
+        ks = ks > 126 ? 126 : (ks < -126 ? -126 : ks);
+        const float sc = __uint_as_float((unsigned)(ks + 127) << 23);
+        const float usc = __uint_as_float((unsigned)(127 - ks) << 23);
+        const int64_t rowf = f * V;
+        if (!bad) {
+            // rows rowf + j + 64 r share one swizzle (64 r moves s / (32 / P) by a multiple of P)
+            const int e0 = ring_at<P>((int)((rowf + j) & (M - 1)), w);
+            cf v[8];
+#pragma unroll
+            for (int r = 0; r < 8; ++r) v[r] = ring[(e0 + 64 * P * r) & (M * P - 1)] * sc;
+            fft512_wave(v, ib, t2, t3);
+#pragma unroll
+            for (int r = 0; r < 8; ++r) ib.b2[72 * r] = cmulw(v[r], fw[r]);
+        } else {
+            // fp32 direct form on the composite taps: y[j] = sum_n heq[n] u[P q - n], q = Q + t
+            for (int t = tid; t < V; t += NT) {
+                const int q = Q + t;
+                cf acc = cf{ 0.f, 0.f };
+                for (int n = 0; n < L; ++n) {
+                    const int tau = P * q - n;
+                    const cf u = ring[ring_at<P>((int)((rowf + tau / P) & (M - 1)), tau % P)];
+                    acc = __builtin_elementwise_fma(cf{ a.heq[n], a.heq[n] }, u, acc);
+                }
+                if (rowf + t < a.n_out) a.out[rowf + t] = make_float2(acc.x, acc.y);
+            }
+        }
+        nsh::lds_barrier(); // B1: window f read, images hold the per-phase products
+        if (!bad && tid < M) {
+            const cf* src = imgs + ipad(tid);
+            cf z = src[0];
+#pragma unroll
+            for (int p = 1; p < P; ++p) z += src[p * IMG];
+            zb[ipad(tid)] = cf{ z.x, -z.y }; // conj: the inverse runs as a forward transform
+        }
+        if (f + 1 < f1) {
+            unsigned mn = nsh::wave_umax(store_rows<P>(pre, ring, a, f + 1));
+            if (j == 0) mx[((f + 1) & 1) * P + w] = mn;
+            load_rows<P>(pre, a, n_in, f + 2 < f1 ? f + 2 : a.nf + 1); // past the stream: empty range
+        }
+        nsh::lds_barrier(); // B2: Z and window f+1 complete
+        if (!bad && w == (int)(f % P)) {
+            const cf* zsrc = zb + j + (j >> 3);
+            cf v[8];
+#pragma unroll
+            for (int r = 0; r < 8; ++r) v[r] = zsrc[72 * r];
+            fft512_wave(v, ib, t2, t3);
+            const __amdgpu_buffer_rsrc_t ro = span_rsrc(a.out + rowf, a.n_out - rowf, V);
+            const cf us = cf{ usc, -usc }; // 2^-k and the output conjugation
+            int ob = (j - Q) * 8;
+            asm volatile("" : "+v"(ob)); // computed here, not hoisted (8 offsets would spill)
+#pragma unroll
+            for (int r = 0; r < 8; ++r)
+                if (j + 64 * r >= Q) nsh::buf_store_f2(ro, ob + 512 * r, v[r] * us);
+        }
+    }
+}
+
+hipError_t set_lds_attr(const void* fn, int bytes, int dev)
+{
+    static std::mutex mtx;
+    static std::set<std::pair<const void*, int>> done;
+    std::lock_guard<std::mutex> g(mtx);
+    if (done.count({ fn, dev })) return hipSuccess;
+    const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (e == hipSuccess) done.insert({ fn, dev });
+    return e;
+}
+
+template <int P>
+constexpr int lds_bytes()
+{
+    return (M * P + P * IMG + IMG) * 8 + 2 * P * 4;
+}
+
+} // namespace
+
+struct nsh_fir_casc_plan {
+    int dev = 0;
+    int D = 1;    // total decimation = phases P
+    int L = 0;    // composite taps
+    int Q = 0;    // overlap rows
+    int V = 0;    // outputs per frame
+    int n_cu = 256;
+    int wg_per_cu = 1;
+    float2* F = nullptr;
+    float2* tw = nullptr;
+    float* heq = nullptr;
+    std::string kernel;
+};
+
+extern "C" {
+
+int nsh_fir_cascade_plan_create(int dev, const float* const* taps_host, const int* ntaps, const int* decims,
+                                int nstages, void** plan)
+{
+    if (!plan) return nsh::fail_msg("nsh_fir_cascade_plan_create: null plan pointer");
+    *plan = nullptr;
+    if (nstages < 1 || !taps_host || !ntaps || !decims) return nsh::fail_msg("nsh_fir_cascade_plan_create: no stages");
+    // composite taps, in double: heq = h_1 * (h_2 up D_1) * ...
+    std::vector<double> heq(1, 1.0);
+    int D = 1;
+    for (int s = 0; s < nstages; ++s) {
+        if (ntaps[s] < 1 || !taps_host[s] || decims[s] < 1)
+            return nsh::fail_msg("nsh_fir_cascade_plan_create: every stage needs >= 1 tap and decim >= 1");
+        if ((int64_t)D * decims[s] > 16) return nsh::fail_msg("nsh_fir_cascade_plan_create: total decimation above 16");
+        for (int k = 0; k < ntaps[s]; ++k)
+            if (!std::isfinite(taps_host[s][k])) return nsh::fail_msg("nsh_fir_cascade_plan_create: taps must be finite");
+        std::vector<double> c(heq.size() + (size_t)(ntaps[s] - 1) * D, 0.0);
+        for (size_t i = 0; i < heq.size(); ++i)
+            for (int k = 0; k < ntaps[s]; ++k) c[i + (size_t)k * D] += heq[i] * (double)taps_host[s][k];
+        heq.swap(c);
+        D *= decims[s];
+    }
+    if (D != 8 && D != 16) return nsh::fail_msg("nsh_fir_cascade_plan_create: total decimation must be 8 or 16");
+    const int L = (int)heq.size();
+    const int Q = (L - 1 + D - 1) / D;
+    if (Q > M / 2) return nsh::fail_msg("nsh_fir_cascade_plan_create: composite filter longer than 256 output rows");
+    auto* p = new nsh_fir_casc_plan();
+    p->D = D;
+    p->L = L;
+    p->Q = Q;
+    p->V = M - Q;
+    p->dev = dev;
+    hipError_t e = hipSetDevice(dev); // as nsh_fir_plan_create: the plan's device becomes current
+    int ncu = 0;
+    if (e == hipSuccess && hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, p->dev) == hipSuccess && ncu > 0)
+        p->n_cu = ncu;
+    p->wg_per_cu = D == 16 ? 1 : 2;
+    // F_p[k] = FFT_512(g_p)[k] / 512, g_p[q'] = heq[D q' - p]
+    std::vector<float2> F((size_t)D * M), tw(M);
+    std::vector<double> cs(M), sn(M);
+    for (int t = 0; t < M; ++t) {
+        const double ang = -2.0 * M_PI * (double)t / (double)M;
+        cs[t] = std::cos(ang);
+        sn[t] = std::sin(ang);
+        tw[t] = make_float2((float)cs[t], (float)sn[t]);
+    }
+    for (int ph = 0; ph < D; ++ph)
+        for (int k = 0; k < M; ++k) {
+            double re = 0.0, im = 0.0;
+            for (int q = 0; q <= Q; ++q) {
+                const int n = D * q - ph;
+                if (n < 0 || n >= L) continue;
+                const int t = (int)(((int64_t)k * q) & (M - 1));
+                re += heq[n] * cs[t];
+                im += heq[n] * sn[t];
+            }
+            F[(size_t)ph * M + k] = make_float2((float)(re / M), (float)(im / M));
+        }
+    std::vector<float> hf(heq.begin(), heq.end());
+    if (e == hipSuccess) e = hipMalloc(&p->F, F.size() * sizeof(float2));
+    if (e == hipSuccess) e = hipMalloc(&p->tw, tw.size() * sizeof(float2));
+    if (e == hipSuccess) e = hipMalloc(&p->heq, hf.size() * sizeof(float));
+    if (e == hipSuccess) e = hipMemcpy(p->F, F.data(), F.size() * sizeof(float2), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(p->tw, tw.data(), tw.size() * sizeof(float2), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(p->heq, hf.data(), hf.size() * sizeof(float), hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        const void* fn = D == 16 ? (const void*)k_fir_pfft<16> : (const void*)k_fir_pfft<8>;
+        e = set_lds_attr(fn, D == 16 ? lds_bytes<16>() : lds_bytes<8>(), p->dev);
+    }
+    if (e != hipSuccess) {
+        if (p->F) (void)hipFree(p->F);
+        if (p->tw) (void)hipFree(p->tw);
+        if (p->heq) (void)hipFree(p->heq);
+        delete p;
+        return nsh::fail(e, "nsh_fir_cascade_plan_create");
+    }
+    p->kernel = "k_fir_pfft<" + std::to_string(D) + ">";
+    *plan = p;
+    return 0;
+}
+
+int nsh_fir_cascade_plan_destroy(void* plan)
+{
+    auto* p = static_cast<nsh_fir_casc_plan*>(plan);
+    if (!p) return 0;
+    if (p->F) (void)hipFree(p->F);
+    if (p->tw) (void)hipFree(p->tw);
+    if (p->heq) (void)hipFree(p->heq);
+    delete p;
+    return 0;
+}
+
+int nsh_fir_cascade_decim(void* plan) { return plan ? static_cast<nsh_fir_casc_plan*>(plan)->D : 0; }
+int nsh_fir_cascade_hist_len(void* plan) { return plan ? static_cast<nsh_fir_casc_plan*>(plan)->L - 1 : 0; }
+const char* nsh_fir_cascade_kernel(void* plan) { return plan ? static_cast<nsh_fir_casc_plan*>(plan)->kernel.c_str() : ""; }
+
+int nsh_fir_cascade_ccf(void* plan, const float* in, const float* hist_in, float* hist_out, float* out, int64_t n_out,
+                        void* stream)
+{
+    auto* p = static_cast<nsh_fir_casc_plan*>(plan);
+    if (!p) return nsh::fail_msg("nsh_fir_cascade_ccf: null plan");
+    if (n_out <= 0) return 0;
+    if (n_out > ((int64_t)1 << 40)) return nsh::fail_msg("nsh_fir_cascade_ccf: n_out too large");
+    if (hist_in == hist_out && p->L > 1) return nsh::fail_msg("nsh_fir_cascade_ccf: hist_out must not alias hist_in");
+    pfft_args a;
+    a.x = (const float2*)in;
+    a.hist_in = (const float2*)hist_in;
+    a.hist_out = (float2*)hist_out;
+    a.out = (float2*)out;
+    a.n_out = n_out;
+    a.F = p->F;
+    a.tw = p->tw;
+    a.heq = p->heq;
+    a.L = p->L;
+    a.Q = p->Q;
+    a.V = p->V;
+    a.nf = (n_out + p->V - 1) / p->V;
+    const int64_t max_wg = (int64_t)p->n_cu * p->wg_per_cu;
+    int64_t wg = a.nf < max_wg ? a.nf : max_wg;
+    a.fpw = (a.nf + wg - 1) / wg;
+    wg = (a.nf + a.fpw - 1) / a.fpw;
+    if (p->D == 16)
+        hipLaunchKernelGGL(k_fir_pfft<16>, dim3((unsigned)wg), dim3(1024), lds_bytes<16>(), nsh::S(stream), a);
+    else
+        hipLaunchKernelGGL(k_fir_pfft<8>, dim3((unsigned)wg), dim3(512), lds_bytes<8>(), nsh::S(stream), a);
+    NSH_CK_LAUNCH("nsh_fir_cascade_ccf");
+    return 0;
+}
+
+} // extern "C"

@@ -63,6 +63,13 @@ SIGNATURES = {
     "nsh_fir_ccf": (_i, [_vp, _vp, _vp, _vp, _vp, _i64, _vp]),
     "nsh_fir_cascade2_supported": (_i, [_vp, _vp]),
     "nsh_fir_cascade2_ccf": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp]),
+    "nsh_fir_cascade_plan_create": (_i, [_i, C.POINTER(C.POINTER(_f)), C.POINTER(_i), C.POINTER(_i), _i,
+                                         C.POINTER(_vp)]),
+    "nsh_fir_cascade_plan_destroy": (_i, [_vp]),
+    "nsh_fir_cascade_decim": (_i, [_vp]),
+    "nsh_fir_cascade_hist_len": (_i, [_vp]),
+    "nsh_fir_cascade_kernel": (C.c_char_p, [_vp]),
+    "nsh_fir_cascade_ccf": (_i, [_vp, _vp, _vp, _vp, _vp, _i64, _vp]),
     "nsh_fft1024_c2c": (_i, [_vp, _vp, _i64, _i, _vp]),
     "nsh_channelizer1024": (_i, [_vp, _vp, _vp, _i64, _vp]),
 }
@@ -190,6 +197,43 @@ class FirPlan:
     def close(self):
         if getattr(self, "_h", None):
             lib().nsh_fir_plan_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class FirCascadePlan:
+    """A chain of fir_filter_ccf(taps_s, decim_s) stages as one pass; see nsh_fir_cascade_ccf."""
+
+    def __init__(self, stages, device: int = 0):
+        import numpy as np
+
+        self._taps = [np.ascontiguousarray(np.asarray(t, dtype=np.float32)) for t, _ in stages]
+        n = len(self._taps)
+        tp = (C.POINTER(C.c_float) * n)(*[t.ctypes.data_as(C.POINTER(C.c_float)) for t in self._taps])
+        nt = (C.c_int * n)(*[int(t.size) for t in self._taps])
+        dc = (C.c_int * n)(*[int(d) for _, d in stages])
+        h = C.c_void_p()
+        check(lib().nsh_fir_cascade_plan_create(device, tp, nt, dc, n, C.byref(h)), "nsh_fir_cascade_plan_create")
+        self._h = h
+        self.decim = lib().nsh_fir_cascade_decim(h)
+        self.hist_len = lib().nsh_fir_cascade_hist_len(h)
+        self.kernel = lib().nsh_fir_cascade_kernel(h).decode()
+
+    def __call__(self, x, hist_in, hist_out, y, n_out: int, stream=None):
+        """n_out outputs from n_out * decim inputs; hist_in/hist_out: hist_len samples (or 0/None)."""
+        check(lib().nsh_fir_cascade_ccf(self._h, ptr(x) if x is not None else None,
+                                        ptr(hist_in) if hist_in is not None else None,
+                                        ptr(hist_out) if hist_out is not None else None, ptr(y), n_out,
+                                        stream_ptr(stream)), "nsh_fir_cascade_ccf")
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().nsh_fir_cascade_plan_destroy(self._h)
             self._h = None
 
     def __del__(self):

@@ -1,0 +1,253 @@
+"""GPU parity for nsh_fir_cascade_ccf (k_fir_pfft: a chain of decimating fir_filter_ccf stages
+computed in one pass as the composite filter by polyphase-FFT overlap-save) against the oracle's
+stage-by-stage chain (oracle.fir_ccf per stage, double accumulation, fp32 between stages):
+
+* BASELINE config C5 (4 x fir(firwin(127, 0.45), 2)) at every frame-boundary shape: one output,
+  partial frames, exactly one frame (V = 393), several workgroups, a ragged last frame;
+* other chains with total decimation 16 and 8 (mixed tap lengths and decimations, single long
+  stages), the reference-convention golden 4-stage chain (tests/golden/fir127_decim2.npz);
+* call splitting through the (len(heq) - 1)-sample history, nonzero starting history;
+* inf/NaN inputs (same non-finite positions as the chain), per-frame power-of-two scaling over
+  1e-30 .. 1e30 regions (checked against a +-512-output local envelope), determinism.
+
+Tolerance: the north-star 1e-5 (oracle.tol_ok) on the final outputs."""
+import numpy as np
+import pytest
+
+from oracle import oracle as orc
+from newsched_amd import nsh
+
+pytestmark = pytest.mark.gpu
+
+
+def _firwin(n, cutoff):
+    return np.asarray(__import__("scipy.signal", fromlist=["firwin"]).firwin(n, cutoff), np.float32)
+
+
+C5 = [(_firwin(127, 0.45), 2)] * 4
+
+
+def heq_l1(stages):
+    """sum |heq| of the composite filter (double)."""
+    h = np.ones(1)
+    dacc = 1
+    for t, d in stages:
+        u = np.zeros((t.size - 1) * dacc + 1)
+        u[::dacc] = t
+        h = np.convolve(h, u)
+        dacc *= d
+    return float(np.abs(h).sum())
+
+
+def tol_pfft(y, r, x, stages, rel=1e-5):
+    """oracle.tol_ok with the scale floored at 1e-2 of the input level max|x| sum|heq|: transform
+    rounding is relative to the frame's input, so outputs far below it (the first outputs of a
+    stream from zero history, where only the filter's tiny edge taps have data) carry an absolute
+    error of ~1e-10 of the input level -- 1e-7 of that floor, against which 1e-5 is checked."""
+    r = np.asarray(r, np.complex128)
+    floor = 1e-2 * (float(np.abs(x).max()) if x.size else 0.0) * heq_l1(stages)
+    scale = max(float(np.abs(r).max()) if r.size else 0.0, floor)
+    err = np.abs(np.asarray(y, np.complex128) - r)
+    maxerr = float(err.max()) if err.size else 0.0
+    ok = maxerr <= rel * scale and bool(np.all(err <= rel * np.abs(r) + 0.1 * rel * scale))
+    return ok, maxerr, scale
+
+
+def ref_chain(x, stages):
+    y = x
+    for h, d in stages:
+        y = orc.fir_ccf(y, h, d)
+    return y
+
+
+def run_pfft(torch, plan, x, n_out, hist=None, want_hist=True):
+    assert x.size == plan.decim * n_out
+    dx = torch.from_numpy(np.ascontiguousarray(x, np.complex64)).cuda() if x.size else \
+        torch.zeros(1, dtype=torch.complex64, device="cuda")
+    dh = torch.from_numpy(np.ascontiguousarray(hist, np.complex64)).cuda() if hist is not None else None
+    dho = torch.full((plan.hist_len,), complex(9.0, 9.0), dtype=torch.complex64, device="cuda") if want_hist else None
+    dy = torch.full((max(n_out, 1),), complex(7.0, 7.0), dtype=torch.complex64, device="cuda")
+    plan(dx, dh, dho, dy, n_out)
+    torch.cuda.synchronize()
+    return dy.cpu().numpy()[:n_out], (dho.cpu().numpy() if want_hist else None)
+
+
+def test_c5_plan_shape(torch_cuda):
+    p = nsh.FirCascadePlan(C5)
+    assert p.decim == 16 and p.hist_len == 1890 and p.kernel == "k_fir_pfft<16>"
+
+
+@pytest.mark.parametrize("n_out", [1, 2, 118, 119, 392, 393, 394, 786, 787, 5000, 393 * 256, 393 * 256 + 1,
+                                   100_003, 1 << 20])
+def test_c5_vs_oracle_chain(torch_cuda, n_out):
+    p = nsh.FirCascadePlan(C5)
+    x = orc.synth(16 * n_out, n_out % 977)
+    y, hout = run_pfft(torch_cuda, p, x, n_out)
+    ry = ref_chain(x, C5)
+    ok, err, scale = orc.tol_ok(y, ry) if n_out >= 256 else tol_pfft(y, ry, x, C5)
+    assert ok, (n_out, err, scale)
+    # the next call's history: the last 1890 inputs (zeros before the stream), bit-exact
+    full = np.concatenate([np.zeros(1890, np.complex64), x])
+    np.testing.assert_array_equal(hout, full[-1890:])
+
+
+def test_c5_golden_chain4(torch_cuda):
+    """tests/golden/fir127_decim2.npz: y_chain4 = 4 x fir(taps, 2) of x (scipy lfilter-pinned)."""
+    g = np.load("tests/golden/fir127_decim2.npz")
+    taps, x, y4 = g["taps"], g["x"], g["y_chain4"]
+    p = nsh.FirCascadePlan([(taps, 2)] * 4)
+    y, _ = run_pfft(torch_cuda, p, x, x.size // 16)
+    ok, err, scale = orc.tol_ok(y, y4)
+    assert ok, (err, scale)
+
+
+CHAINS = {
+    "taps33-160-64-127": [(_firwin(33, 0.4), 2), (_firwin(160, 0.3), 2), (_firwin(64, 0.45), 2),
+                          (_firwin(127, 0.45), 2)],
+    "d4-d4": [(_firwin(255, 0.2), 4), (_firwin(127, 0.2), 4)],
+    "d2-d8": [(_firwin(31, 0.45), 2), (_firwin(200, 0.1), 8)],
+    "single-d16": [(_firwin(1501, 0.05), 16)],
+    "single-d16-short": [(_firwin(7, 0.05), 16)],
+    "d8-3x2": [(_firwin(127, 0.45), 2)] * 3,
+    "single-d8": [(_firwin(900, 0.1), 8)],
+    "d8-4x2": [(_firwin(127, 0.45), 2), (_firwin(61, 0.4), 4)],
+}
+
+
+@pytest.mark.parametrize("name", sorted(CHAINS))
+@pytest.mark.parametrize("n_out", [1, 300, 4099, 200_001])
+def test_chains_vs_oracle(torch_cuda, name, n_out):
+    stages = CHAINS[name]
+    p = nsh.FirCascadePlan(stages)
+    assert p.decim == int(np.prod([d for _, d in stages]))
+    x = orc.synth(p.decim * n_out, 31 + n_out)
+    y, _ = run_pfft(torch_cuda, p, x, n_out)
+    ry = ref_chain(x, stages)
+    ok, err, scale = orc.tol_ok(y, ry) if n_out >= 256 else tol_pfft(y, ry, x, stages)
+    assert ok, (name, n_out, err, scale)
+
+
+def test_unsupported_chains_rejected(torch_cuda):
+    with pytest.raises(nsh.NshError):
+        nsh.FirCascadePlan([(_firwin(127, 0.45), 2)])            # D = 2
+    with pytest.raises(nsh.NshError):
+        nsh.FirCascadePlan([(_firwin(127, 0.45), 2)] * 5)        # D = 32
+    with pytest.raises(nsh.NshError):
+        nsh.FirCascadePlan([(_firwin(4200, 0.05), 16)])          # 263 overlap rows > 256
+    with pytest.raises(nsh.NshError):
+        nsh.FirCascadePlan([(np.array([1.0, np.inf], np.float32), 16)])
+
+
+def test_c5_split_calls_and_history(torch_cuda):
+    """Call-splitting invariance: calls shorter than a frame and than the history, ping-pong
+    histories; equals the oracle chain over the whole stream."""
+    p = nsh.FirCascadePlan(C5)
+    n_total = 70_001
+    x = orc.synth(16 * n_total, 5)
+    ry = ref_chain(x, C5)
+    cuts = [0, 1, 2, 50, 118, 119, 500, 893, 20_000, 20_001, n_total]
+    hist = None
+    parts = []
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        y, hist = run_pfft(torch_cuda, p, x[16 * a:16 * b], b - a, hist)
+        parts.append(y)
+    ok, err, scale = orc.tol_ok(np.concatenate(parts), ry)
+    assert ok, (err, scale)
+
+
+def test_c5_nonzero_start_history(torch_cuda):
+    """A plan started from hist_in = the 1890 samples before x equals the chain over the longer
+    stream (the composite state is the input history)."""
+    p = nsh.FirCascadePlan(C5)
+    pre, n_out = 16 * 200, 3000
+    s = orc.synth(pre + 16 * n_out, 99)
+    ry = ref_chain(s, C5)[pre // 16:]
+    y, _ = run_pfft(torch_cuda, p, s[pre:], n_out, hist=s[pre - 1890:pre])
+    ok, err, scale = orc.tol_ok(y, ry)
+    assert ok, (err, scale)
+
+
+def test_c5_deterministic(torch_cuda):
+    p = nsh.FirCascadePlan(C5)
+    n_out = 300_000
+    x = orc.synth(16 * n_out, 3)
+    y1, _ = run_pfft(torch_cuda, p, x, n_out)
+    y2, _ = run_pfft(torch_cuda, p, x, n_out)
+    np.testing.assert_array_equal(y1, y2)
+
+
+@pytest.mark.parametrize("kind", ["nan", "inf", "neginf", "huge"])
+def test_c5_nonfinite_inputs(torch_cuda, kind):
+    """inf/NaN frames go through the fp32 direct form on the composite taps: the non-finite
+    outputs sit where the chain's do; every finite output is within tolerance. 'huge' (3e38,
+    finite) must stay finite wherever the chain's output is (scaled transforms never overflow)."""
+    p = nsh.FirCascadePlan(C5)
+    n_out = 20_000
+    x = orc.synth(16 * n_out, 7)
+    val = {"nan": np.nan, "inf": np.inf, "neginf": -np.inf, "huge": 3.0e38}[kind]
+    for pos in (0, 5000, 5001, 16 * 393 * 7 + 3, 16 * n_out - 1):
+        x[pos] = complex(val, 0.25) if kind != "huge" else complex(val, -val)
+    y, _ = run_pfft(torch_cuda, p, x, n_out)
+    ry = ref_chain(x, C5)
+    fin = np.isfinite(ry.real) & np.isfinite(ry.imag)
+    np.testing.assert_array_equal(np.isfinite(y.real) & np.isfinite(y.imag), fin)
+    if kind == "nan":
+        np.testing.assert_array_equal(np.isnan(y.real), np.isnan(ry.real))
+    ok, err, scale = orc.tol_ok(y[fin], ry[fin])
+    assert ok, (kind, err, scale)
+
+
+def _local_ok(y, r, half=512, rel=1e-5):
+    """|y - r| <= rel |r| + 0.1 rel max|r| over the +-half outputs around each one."""
+    from numpy.lib.stride_tricks import sliding_window_view as swv
+
+    a = np.abs(np.asarray(r, np.complex128))
+    env = swv(np.pad(a, half), 2 * half + 1).max(axis=1)
+    err = np.abs(np.asarray(y, np.complex128) - r)
+    bad = err > rel * a + 0.1 * rel * env
+    return not bad.any(), int(bad.sum())
+
+
+def test_c5_per_frame_scaling(torch_cuda):
+    """Regions of magnitude 1e-30, 1e-36 (near fp32's normal floor), 1, 1e30: each is filtered to
+    relative accuracy against its own neighbourhood, not the stream maximum."""
+    p = nsh.FirCascadePlan(C5)
+    n_out = 16 * 1024
+    x = orc.synth(16 * n_out, 11)
+    seg = x.size // 8
+    for i, s in enumerate([1e-30, 1.0, 1e30, 1e-36, 1e20, 1e-20, 1.0, 1e-30]):
+        x[i * seg:(i + 1) * seg] *= np.float32(s)
+    y, _ = run_pfft(torch_cuda, p, x, n_out)
+    ry = ref_chain(x, C5)
+    ok, nbad = _local_ok(y, ry)
+    assert ok, nbad
+
+
+def test_c5_zero_and_empty(torch_cuda):
+    p = nsh.FirCascadePlan(C5)
+    y, _ = run_pfft(torch_cuda, p, np.zeros(16 * 5000, np.complex64), 5000)
+    assert not np.any(y)
+    y, _ = run_pfft(torch_cuda, p, np.zeros(0, np.complex64), 0)  # n_out = 0: no launch, no error
+    assert y.size == 0
+
+
+def test_c5_windowed_large(torch_cuda):
+    """2^26 inputs (2^22 outputs, every workgroup busy with ~40 frames): windows at the start,
+    the middle (workgroup boundaries) and the tail against the oracle with their histories."""
+    torch = torch_cuda
+    p = nsh.FirCascadePlan(C5)
+    n_out = 1 << 22
+    dx = torch.empty(16 * n_out, dtype=torch.complex64, device="cuda")
+    nsh.synth(dx, 16 * n_out, 0)
+    dy = torch.empty(n_out, dtype=torch.complex64, device="cuda")
+    dho = torch.empty(1890, dtype=torch.complex64, device="cuda")
+    p(dx, None, dho, dy, n_out)
+    torch.cuda.synchronize()
+    y = dy.cpu().numpy()
+    for start in (0, 393 * 164 - 7, n_out // 2 + 12345, n_out - 3000):
+        m = 3000 if start + 3000 <= n_out else n_out - start
+        lo = max(0, start - 128)  # 128 outputs of lead-in cover the 1890-sample support
+        xs = orc.synth(16 * (start + m - lo), 16 * lo)
+        ry = ref_chain(xs, C5)[start - lo:]
+        ok, err, scale = orc.tol_ok(y[start:start + m], ry)
+        assert ok, (start, err, scale)

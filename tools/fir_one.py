@@ -12,7 +12,7 @@ import torch
 from newsched_amd import nsh
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--algo", default="mfma", choices=["mfma", "mfma_x3", "direct"])
+ap.add_argument("--algo", default="mfma", choices=["mfma", "mfma_x3", "direct", "casc"])
 ap.add_argument("--log2n", type=int, default=25)
 ap.add_argument("--reps", type=int, default=10)
 a = ap.parse_args()
@@ -23,9 +23,15 @@ nsh.synth(x, n, 0)
 y = torch.empty_like(x)
 hin = torch.zeros(126, dtype=torch.complex64, device="cuda")
 hout = torch.zeros_like(hin)
-p = nsh.FirPlan(h, 1, {"mfma": nsh.FIR_MFMA, "mfma_x3": nsh.FIR_MFMA_BF16X3, "direct": nsh.FIR_DIRECT}[a.algo])
-for _ in range(a.reps):
-    p(x, hin, hout, y, n)
+if a.algo == "casc":  # C5's fused chain (nsh_fir_cascade_ccf): 4 x fir(firwin(127, 0.45), 2)
+    p = nsh.FirCascadePlan([(ss.firwin(127, 0.45).astype(np.float32), 2)] * 4)
+    hc = torch.zeros(p.hist_len, dtype=torch.complex64, device="cuda")
+    for _ in range(a.reps):
+        p(x, None, hc, y, n // 16)
+else:
+    p = nsh.FirPlan(h, 1, {"mfma": nsh.FIR_MFMA, "mfma_x3": nsh.FIR_MFMA_BF16X3, "direct": nsh.FIR_DIRECT}[a.algo])
+    for _ in range(a.reps):
+        p(x, hin, hout, y, n)
 for _ in range(a.reps):
     nsh.copy(x, y, 8 * n)  # calibration: exactly 8n B read + 8n B written per launch
 torch.cuda.synchronize()

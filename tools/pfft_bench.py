@@ -1,0 +1,79 @@
+"""C5 kernel timing: the fused chain k_fir_pfft<16> (nsh_fir_cascade_ccf) vs the four staged
+decimate-by-2 launches it replaces, same process, interleaved rounds, HIP events on the launch
+stream, >= 1 s warm-up. Input 2^LOG2 resident samples; bytes per input sample: 8.5 fused (read 8,
+write 0.5), 22.5 staged.
+Usage: python tools/pfft_bench.py [--log2n 28] [--reps 20] [--rounds 3]"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np
+import scipy.signal as ss
+import torch
+
+from newsched_amd import nsh
+
+
+def timed(fn, reps, s):
+    st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    with torch.cuda.stream(s):
+        st.record(s)
+        for _ in range(reps):
+            fn()
+        en.record(s)
+    en.synchronize()
+    return st.elapsed_time(en) / reps * 1e3  # us
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--log2n", type=int, default=28)
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--rounds", type=int, default=3)
+    a = ap.parse_args()
+    n = 1 << a.log2n
+    s = torch.cuda.Stream()
+    h = ss.firwin(127, 0.45).astype(np.float32)
+    x = torch.empty(n, dtype=torch.complex64, device="cuda")
+    nsh.synth(x, n, 0, stream=s)
+    y = torch.empty(n // 16, dtype=torch.complex64, device="cuda")
+    hc = torch.empty(1890, dtype=torch.complex64, device="cuda")
+    pc = nsh.FirCascadePlan([(h, 2)] * 4)
+    st = [nsh.FirPlan(h, 2) for _ in range(4)]
+    mids = [torch.empty(n >> (i + 1), dtype=torch.complex64, device="cuda") for i in range(4)]
+    hs = [torch.empty(126, dtype=torch.complex64, device="cuda") for _ in range(4)]
+
+    def fused():
+        pc(x, None, hc, y, n // 16, stream=s)
+
+    def staged():
+        src = x
+        for i in range(4):
+            st[i](src, 0, hs[i], mids[i], n >> (i + 1), stream=s)
+            src = mids[i]
+
+    t0 = time.time()
+    while time.time() - t0 < 1.0:
+        timed(fused, 5, s)
+        timed(staged, 5, s)
+    res = {"log2n": a.log2n, "fused_kernel": pc.kernel, "staged_kernel": st[0].kernel, "fused_us": [], "staged_us": []}
+    for _ in range(a.rounds):
+        res["fused_us"].append(round(timed(fused, a.reps, s), 1))
+        res["staged_us"].append(round(timed(staged, a.reps, s), 1))
+    f, g = min(res["fused_us"]), min(res["staged_us"])
+    res["fused_GSps_input"] = round(n / f / 1e3, 1)
+    res["fused_hbm_frac_8.5B"] = round(8.5 * n / f / 1e3 / 8000, 4)
+    res["staged_GSps_input"] = round(n / g / 1e3, 1)
+    res["speedup"] = round(g / f, 3)
+    # parity of the fused tail against the staged chain (both device paths; the oracle check is in tests)
+    torch.cuda.synchronize()
+    d = (y[-4096:] - mids[3][-4096:]).abs().max().item() / mids[3][-4096:].abs().max().item()
+    res["fused_vs_staged_tail_rel"] = d
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
