@@ -49,6 +49,13 @@
 #include <utility>
 #include <vector>
 
+// Timing-only ablation hooks for tools/probe/pfft_ab.py (0 in every product build): 1 = no inverse
+// transform, 2 = no forward transform, 4 = no global loads, 8 = no phase reduction, 16 = no
+// window reads from the ring.
+#ifndef NSH_PFFT_ABLATE
+#define NSH_PFFT_ABLATE 0
+#endif
+
 namespace {
 
 using nsh::cf;
@@ -56,10 +63,39 @@ using nsh::cmulw;
 using nsh::dft4;
 using nsh::rot;
 
-constexpr int M = 512;          // FFT length per phase
-constexpr int IMG = M + M / 8;  // a wave's padded LDS image (one pad entry per 8)
+#ifndef NSH_PFFT_ASM_CMUL
+#define NSH_PFFT_ASM_CMUL 1
+#endif
+// a * w for a per-lane constant w (twiddles, filter spectrum): v_pk_mul (w.x broadcast) + v_pk_fma
+// with the swap and the one negation of a as operand modifiers. Written in C (cmulw) the compiler
+// materialises (-w.y, w.x) with a v_xor + v_mov per use; s_nop 0 covers the packed-math
+// read-after-write wait it would insert itself.
+__device__ __forceinline__ cf cmul_tw(cf a, cf w)
+{
+#if NSH_PFFT_ASM_CMUL
+    cf d;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]\n\ts_nop 0\n\t"
+        "v_pk_fma_f32 %0, %2, %1, %0 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_lo:[1,0,0]\n\ts_nop 0"
+        : "=&v"(d)
+        : "v"(w), "v"(a));
+    return d;
+#else
+    return cmulw(a, w);
+#endif
+}
 
-__device__ __forceinline__ int ipad(int i) { return i + (i >> 3); }
+constexpr int M = 512;          // FFT length per phase
+constexpr int IMG = 572;         // a wave's LDS image: the largest padded index below + 1, kept even so
+                                // every carve stays 16-B aligned (an off-alignment b64/b128 access
+                                // replays at 64-128 cycles)
+
+// Three layouts of a wave's 512-entry image, each bank-conflict-free for both of its access
+// patterns over every 32-lane half (a 64-bit access covers banks 2e, 2e+1 of entry e), and each
+// a base register plus immediate offsets (layouts found by exhaustive search over paddings):
+//   exchange 1 (pass-1 stores at 8 j + r, pass-2 loads at j + 64 r):        e = i + (i >> 5)
+//   exchange 2 (pass-2 stores at 64 (j >> 3) + (j & 7) + 8 r, pass-3 loads):  e = i + 3 (i >> 5) + 2 (i >> 6)
+//   products / reduction / Z (stores and loads at j + 64 r, or at tid):       e = i
+// (i + (i >> 3) made 2-way conflicts on every natural-order access: 34 % of LDS cycles.)
 
 // ring entry of (slot s, phase p): rows of P samples, phase XOR-swizzled by (s / (32 / P)) so
 // that 32 consecutive slots read at one phase hit 32 distinct bank pairs
@@ -89,18 +125,24 @@ __device__ __forceinline__ void dft8(cf (&v)[8])
     v[7] = e3 - o3;
 }
 
-// A wave's image addresses: pass-1 stores at b1 + r (= ipad(8 j + r)), pass-2 stores at b3 + 9 r
-// (= ipad((j >> 3) 64 + (j & 7) + 8 r)), natural-order loads/stores at b2 + 72 r (= ipad(j + 64 r)):
-// one base register each, the rest immediate offsets.
+// A wave's image addresses (one base register each, the rest immediate offsets):
+//   x1 + r        = e1(8 j + r)       = 8 j + (j >> 2) + r
+//   b1 + 66 r     = e1(j + 64 r)      = j + (j >> 5) + 66 r
+//   x2 + o2(r)    = e2(64 (j >> 3) + (j & 7) + 8 r) = 72 (j >> 3) + (j & 7) + 8 r + 3 [r >= 4]
+//   b2 + 72 r     = e2(j + 64 r)      = j + 3 (j >> 5) + 72 r
+//   n  + 64 r     = j + 64 r          (products, natural order)
 struct img_bases {
+    cf* x1;
     cf* b1;
+    cf* x2;
     cf* b2;
-    cf* b3;
+    cf* n;
 };
 __device__ __forceinline__ img_bases bases_of(cf* img)
 {
     const int j = threadIdx.x & 63;
-    return img_bases{ img + 9 * j, img + j + (j >> 3), img + (j >> 3) * 72 + (j & 7) };
+    return img_bases{ img + 8 * j + (j >> 2), img + j + (j >> 5), img + 72 * (j >> 3) + (j & 7), img + j + 3 * (j >> 5),
+                      img + j };
 }
 
 // Forward 512-point transform of the values v[r] = x[lane + 64 r] of one wave (Stockham, radix
@@ -111,21 +153,21 @@ __device__ __forceinline__ void fft512_wave(cf (&v)[8], const img_bases& ib, con
 {
     dft8<false>(v); // pass 1 (Ns = 1) -> dst[8 j + r]
 #pragma unroll
-    for (int r = 0; r < 8; ++r) ib.b1[r] = v[r];
+    for (int r = 0; r < 8; ++r) ib.x1[r] = v[r];
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (int r = 0; r < 8; ++r) v[r] = ib.b2[72 * r];
+    for (int r = 0; r < 8; ++r) v[r] = ib.b1[66 * r];
 #pragma unroll
-    for (int r = 1; r < 8; ++r) v[r] = cmulw(v[r], t2[r]);
+    for (int r = 1; r < 8; ++r) v[r] = cmul_tw(v[r], t2[r]);
     dft8<false>(v); // pass 2 (Ns = 8) -> dst[(j >> 3) 64 + (j & 7) + 8 r]
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (int r = 0; r < 8; ++r) ib.b3[9 * r] = v[r];
+    for (int r = 0; r < 8; ++r) ib.x2[8 * r + (r >= 4 ? 3 : 0)] = v[r];
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int r = 0; r < 8; ++r) v[r] = ib.b2[72 * r];
 #pragma unroll
-    for (int r = 1; r < 8; ++r) v[r] = cmulw(v[r], t3[r]);
+    for (int r = 1; r < 8; ++r) v[r] = cmul_tw(v[r], t3[r]);
     dft8<false>(v); // pass 3 (Ns = 64) -> X[j + 64 r], kept in registers
     __builtin_amdgcn_wave_barrier(); // the image is rewritten next
 }
@@ -266,12 +308,7 @@ __global__ __launch_bounds__(64 * P, 1) void k_fir_pfft(pfft_args a)
         for (int r = 1; r < 8; ++r) asm volatile("" : "+v"(t2[r]), "+v"(t3[r]));
         // the window's largest magnitude: this frame's new rows and the previous frame's (which
         // hold the overlap; the first window's slot covers all of it)
-        unsigned wm = 0;
-#pragma unroll
-        for (int k = 0; k < 2 * P; k += 4) {
-            const uint4 u = *reinterpret_cast<const uint4*>(mx + k);
-            wm = max(wm, max(max(u.x, u.y), max(u.z, u.w)));
-        }
+        const unsigned wm = nsh::wave_umax(j < 2 * P ? mx[j] : 0u); // one LDS read, DPP max
         const bool bad = wm >= 0x7f800000u; // inf or NaN in the window
         int ks = 127 - (int)(wm >> 23);      // max * 2^ks in [1, 2)
         ks = ks > 126 ? 126 : (ks < -126 ? -126 : ks);
@@ -283,10 +320,11 @@ __global__ __launch_bounds__(64 * P, 1) void k_fir_pfft(pfft_args a)
             const int e0 = ring_at<P>((int)((rowf + j) & (M - 1)), w);
             cf v[8];
 #pragma unroll
-            for (int r = 0; r < 8; ++r) v[r] = ring[(e0 + 64 * P * r) & (M * P - 1)] * sc;
-            fft512_wave(v, ib, t2, t3);
+            for (int r = 0; r < 8; ++r)
+                v[r] = (NSH_PFFT_ABLATE & 16) ? cf{ sc, (float)r } : ring[(e0 + 64 * P * r) & (M * P - 1)] * sc;
+            if (!(NSH_PFFT_ABLATE & 2)) fft512_wave(v, ib, t2, t3);
 #pragma unroll
-            for (int r = 0; r < 8; ++r) ib.b2[72 * r] = cmulw(v[r], fw[r]);
+            for (int r = 0; r < 8; ++r) ib.n[64 * r] = cmul_tw(v[r], fw[r]);
         } else {
             // fp32 direct form on the composite taps: y[j] = sum_n heq[n] u[P q - n], q = Q + t
             for (int t = tid; t < V; t += NT) {
@@ -302,23 +340,22 @@ __global__ __launch_bounds__(64 * P, 1) void k_fir_pfft(pfft_args a)
         }
         nsh::lds_barrier(); // B1: window f read, images hold the per-phase products
         if (!bad && tid < M) {
-            const cf* src = imgs + ipad(tid);
+            const cf* src = imgs + tid;
             cf z = src[0];
 #pragma unroll
-            for (int p = 1; p < P; ++p) z += src[p * IMG];
-            zb[ipad(tid)] = cf{ z.x, -z.y }; // conj: the inverse runs as a forward transform
+            for (int p = 1; p < ((NSH_PFFT_ABLATE & 8) ? 1 : P); ++p) z += src[p * IMG];
+            zb[tid] = cf{ z.x, -z.y }; // conj: the inverse runs as a forward transform
         }
         if (f + 1 < f1) {
             unsigned mn = nsh::wave_umax(store_rows<P>(pre, ring, a, f + 1));
             if (j == 0) mx[((f + 1) & 1) * P + w] = mn;
-            load_rows<P>(pre, a, n_in, f + 2 < f1 ? f + 2 : a.nf + 1); // past the stream: empty range
+            if (!(NSH_PFFT_ABLATE & 4)) load_rows<P>(pre, a, n_in, f + 2 < f1 ? f + 2 : a.nf + 1); // past the stream: empty range
         }
         nsh::lds_barrier(); // B2: Z and window f+1 complete
-        if (!bad && w == (int)(f % P)) {
-            const cf* zsrc = zb + j + (j >> 3);
+        if (!(NSH_PFFT_ABLATE & 1) && !bad && w == (int)(f % P)) {
             cf v[8];
 #pragma unroll
-            for (int r = 0; r < 8; ++r) v[r] = zsrc[72 * r];
+            for (int r = 0; r < 8; ++r) v[r] = zb[j + 64 * r];
             fft512_wave(v, ib, t2, t3);
             const __amdgpu_buffer_rsrc_t ro = span_rsrc(a.out + rowf, a.n_out - rowf, V);
             const cf us = cf{ usc, -usc }; // 2^-k and the output conjugation
@@ -345,6 +382,7 @@ hipError_t set_lds_attr(const void* fn, int bytes, int dev)
 template <int P>
 constexpr int lds_bytes()
 {
+    static_assert(((M * P + P * IMG + IMG) * 8) % 16 == 0, "LDS carves must stay 16-B aligned");
     return (M * P + P * IMG + IMG) * 8 + 2 * P * 4;
 }
 
