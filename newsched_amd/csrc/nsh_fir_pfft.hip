@@ -212,7 +212,18 @@ struct pfft_args {
     int V;
     int64_t nf;        // frames in the launch
     int64_t fpw;       // frames per workgroup
+    unsigned long long* trace; // NSH_PFFT_TRACE builds only: per-frame phase timestamps of workgroup 0
 };
+
+#ifndef NSH_PFFT_TRACE
+#define NSH_PFFT_TRACE 0
+#endif
+// probe builds: s_memtime at phase k of frame f (< 64) by wave w of workgroup 0
+#define PFFT_T(k)                                                                                      \
+    do {                                                                                               \
+        if (NSH_PFFT_TRACE && blockIdx.x == 0 && f - f0 < 64 && j == 0)                                 \
+            a.trace[((f - f0) * 16 + w) * 8 + (k)] = __builtin_amdgcn_s_memtime();                     \
+    } while (0)
 
 constexpr int PRE = 4; // 16-B prefetch slots per thread: V rows x P samples / 2 / (64 P) <= 4
 
@@ -299,6 +310,12 @@ __global__ __launch_bounds__(64 * P, 1) void k_fir_pfft(pfft_args a)
     nsh::lds_barrier();
 
     for (int64_t f = f0; f < f1; ++f) {
+        PFFT_T(0);
+        // The next window's rows (consumed in this frame's phase B) are requested here, at the top
+        // of the transform phase: the CU's texture path moves 64 B/clk, so the 50 KB of a frame's
+        // new rows take ~800 cycles to issue and ~800 to return -- issued in phase B they held
+        // every wave there; here they overlap the transforms.
+        if (f > f0 && !(NSH_PFFT_ABLATE & 4)) load_rows<P>(pre, a, n_in, f + 1 < f1 ? f + 1 : a.nf + 1);
         // Re-define the per-lane constants each frame (empty asm): otherwise the compiler hoists
         // the swizzled/negated copies that cmulw's operand modifiers give for free, i.e. holds
         // every twiddle twice (the kernel has 128 VGPRs at 16 waves per CU).
@@ -338,7 +355,9 @@ __global__ __launch_bounds__(64 * P, 1) void k_fir_pfft(pfft_args a)
                 if (rowf + t < a.n_out) a.out[rowf + t] = make_float2(acc.x, acc.y);
             }
         }
+        PFFT_T(1);
         nsh::lds_barrier(); // B1: window f read, images hold the per-phase products
+        PFFT_T(2);
         if (!bad && tid < M) {
             const cf* src = imgs + tid;
             cf z = src[0];
@@ -346,13 +365,18 @@ __global__ __launch_bounds__(64 * P, 1) void k_fir_pfft(pfft_args a)
             for (int p = 1; p < ((NSH_PFFT_ABLATE & 8) ? 1 : P); ++p) z += src[p * IMG];
             zb[tid] = cf{ z.x, -z.y }; // conj: the inverse runs as a forward transform
         }
+        PFFT_T(6);
         if (f + 1 < f1) {
             unsigned mn = nsh::wave_umax(store_rows<P>(pre, ring, a, f + 1));
             if (j == 0) mx[((f + 1) & 1) * P + w] = mn;
-            if (!(NSH_PFFT_ABLATE & 4)) load_rows<P>(pre, a, n_in, f + 2 < f1 ? f + 2 : a.nf + 1); // past the stream: empty range
+            PFFT_T(7);
         }
+        PFFT_T(3);
         nsh::lds_barrier(); // B2: Z and window f+1 complete
-        if (!(NSH_PFFT_ABLATE & 1) && !bad && w == (int)(f % P)) {
+        PFFT_T(4);
+        // the inverse transform goes to one of waves 0..3 (one per SIMD, the oldest and so the
+        // first in each SIMD's issue arbitration), rotating over the four SIMDs
+        if (!(NSH_PFFT_ABLATE & 1) && !bad && w == (int)(f & 3)) {
             cf v[8];
 #pragma unroll
             for (int r = 0; r < 8; ++r) v[r] = zb[j + 64 * r];
@@ -364,6 +388,7 @@ __global__ __launch_bounds__(64 * P, 1) void k_fir_pfft(pfft_args a)
 #pragma unroll
             for (int r = 0; r < 8; ++r)
                 if (j + 64 * r >= Q) nsh::buf_store_f2(ro, ob + 512 * r, v[r] * us);
+            PFFT_T(5);
         }
     }
 }
@@ -401,6 +426,16 @@ struct nsh_fir_casc_plan {
     float* heq = nullptr;
     std::string kernel;
 };
+
+#if NSH_PFFT_TRACE
+unsigned long long* g_pfft_trace = nullptr;
+extern "C" int nsh_pfft_trace_copy(unsigned long long* host) // probe builds only
+{
+    NSH_CK(hipDeviceSynchronize());
+    NSH_CK(hipMemcpy(host, g_pfft_trace, 64 * 16 * 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    return 0;
+}
+#endif
 
 extern "C" {
 
@@ -523,6 +558,16 @@ int nsh_fir_cascade_ccf(void* plan, const float* in, const float* hist_in, float
     const int64_t max_wg = (int64_t)p->n_cu * p->wg_per_cu;
     int64_t wg = a.nf < max_wg ? a.nf : max_wg;
     a.fpw = (a.nf + wg - 1) / wg;
+    a.trace = nullptr;
+#if NSH_PFFT_TRACE
+    {
+        static unsigned long long* tr = nullptr;
+        if (!tr) NSH_CK(hipMalloc(&tr, 64 * 16 * 8 * sizeof(unsigned long long)));
+        NSH_CK(hipMemsetAsync(tr, 0, 64 * 16 * 8 * sizeof(unsigned long long), nsh::S(stream)));
+        a.trace = tr;
+        g_pfft_trace = tr;
+    }
+#endif
     wg = (a.nf + a.fpw - 1) / a.fpw;
     if (p->D == 16)
         hipLaunchKernelGGL(k_fir_pfft<16>, dim3((unsigned)wg), dim3(1024), lds_bytes<16>(), nsh::S(stream), a);
