@@ -27,6 +27,9 @@ public:
     bool start() override;
     work_return_code_t work(std::vector<block_work_input>& in, std::vector<block_work_output>& out) override;
     int decimation() const { return _decim; }
+    const std::vector<float>& taps() const { return _taps; }
+    int requested_algo() const { return _algo; } // as given to make() (0 = AUTO)
+    bool has_initial_history() const { return !_init_hist.empty(); }
     int algo() const; // resolved algorithm (after start())
     std::string kernel() const; // the kernel its work() launches (after start())
     uint64_t launches() const { return _launches; }

@@ -3,12 +3,14 @@
 #include <gnuradio/blocklib/hip/arith.hpp>
 #include <gnuradio/blocklib/hip/copy.hpp>
 #include <gnuradio/blocklib/hip/fft.hpp>
+#include <gnuradio/blocklib/hip/fir_filter_cascade_ccf.hpp>
 #include <gnuradio/blocklib/hip/fir_filter_ccf.hpp>
 #include <gnuradio/blocklib/hip/multiply_const.hpp>
 #include <gnuradio/blocklib/hip/synth_source.hpp>
 #include <gnuradio/hip_context.hpp>
 
 #include <algorithm>
+#include <cmath>
 #include <stdexcept>
 
 #include "nsh_hip.h"
@@ -205,6 +207,128 @@ double fir_filter_ccf::kernel_ms()
         float ms = 0;
         check(nsh_event_sync(_ev[i].second), "hip::fir_filter_ccf timing");
         check(nsh_event_elapsed_ms(_ev[i].first, _ev[i].second, &ms), "hip::fir_filter_ccf timing");
+        total += ms;
+    }
+    return total;
+}
+
+// ---- fused decimating FIR chain -----------------------------------------------------
+namespace {
+int total_decim(const std::vector<fir_filter_cascade_ccf::stage>& st)
+{
+    int64_t d = 1;
+    for (auto& s : st) d *= s.second > 0 ? s.second : 0;
+    return d > 64 ? 64 : (int)d;
+}
+} // namespace
+
+bool fir_filter_cascade_ccf::supported(const std::vector<stage>& st)
+{
+    if (st.empty()) return false;
+    const int D = total_decim(st);
+    if (D != 8 && D != 16) return false;
+    int64_t len = 1, dacc = 1; // composite length 1 + sum (L_s - 1) prod_{t<s} D_t
+    for (auto& s : st) {
+        if (s.first.empty()) return false;
+        for (float v : s.first)
+            if (!std::isfinite(v)) return false;
+        len += (int64_t)(s.first.size() - 1) * dacc;
+        dacc *= s.second;
+    }
+    return (len - 1 + D - 1) / D <= 256; // nsh_fir_cascade_plan_create's limit
+}
+
+fir_filter_cascade_ccf::fir_filter_cascade_ccf(const std::vector<stage>& stages)
+    : decim_block("fir_filter_cascade_ccf (hip)", (unsigned)total_decim(stages)), _stages(stages)
+{
+    if (!supported(stages))
+        throw std::invalid_argument("hip::fir_filter_cascade_ccf: needs total decimation 8 or 16, finite taps and "
+                                    "ceil((len(heq)-1)/D) <= 256");
+}
+
+fir_filter_cascade_ccf::~fir_filter_cascade_ccf() { release(); }
+
+void fir_filter_cascade_ccf::release()
+{
+    for (auto& e : _ev) {
+        nsh_event_destroy(e.first);
+        nsh_event_destroy(e.second);
+    }
+    _ev.clear();
+    _ev_used = 0;
+    if (_plan) nsh_fir_cascade_plan_destroy(_plan);
+    for (auto& h : _hist)
+        if (h) nsh_free(h);
+    _plan = nullptr;
+    _hist[0] = _hist[1] = nullptr;
+}
+
+std::string fir_filter_cascade_ccf::kernel() const { return _plan ? nsh_fir_cascade_kernel(_plan) : std::string(); }
+
+bool fir_filter_cascade_ccf::start()
+{
+    const int dev = current_device();
+    if (_plan && dev != _dev) release();
+    if (!_plan) {
+        _dev = dev;
+        std::vector<const float*> tp;
+        std::vector<int> nt, dc;
+        for (auto& s : _stages) {
+            tp.push_back(s.first.data());
+            nt.push_back((int)s.first.size());
+            dc.push_back(s.second);
+        }
+        check(nsh_fir_cascade_plan_create(dev, tp.data(), nt.data(), dc.data(), (int)_stages.size(), &_plan),
+              "hip::fir_filter_cascade_ccf plan");
+        _hist_len = (size_t)nsh_fir_cascade_hist_len(_plan);
+        const size_t hbytes = std::max<size_t>(_hist_len, 1) * sizeof(gr_complex);
+        check(nsh_malloc(dev, hbytes, &_hist[0]), "hip::fir_filter_cascade_ccf history");
+        check(nsh_malloc(dev, hbytes, &_hist[1]), "hip::fir_filter_cascade_ccf history");
+    }
+    _zero_hist = true; // a fresh stream: the first call reads a null (zero) history
+    _cur = 0;
+    _ev_used = 0;
+    _timed_samples = 0;
+    return block::start();
+}
+
+work_return_code_t fir_filter_cascade_ccf::work(std::vector<block_work_input>& in, std::vector<block_work_output>& out)
+{
+    const int n_out = out[0].n_items; // decim_block::do_work: in[0].n_items == D * n_out
+    void* s = current_stream();
+    std::pair<void*, void*>* ev = nullptr;
+    if (_timing) {
+        if (_ev_used == _ev.size()) {
+            std::pair<void*, void*> p{ nullptr, nullptr };
+            check(nsh_event_create(&p.first), "hip::fir_filter_cascade_ccf timing");
+            check(nsh_event_create(&p.second), "hip::fir_filter_cascade_ccf timing");
+            _ev.push_back(p);
+        }
+        ev = &_ev[_ev_used++];
+        check(nsh_event_record(ev->first, s), "hip::fir_filter_cascade_ccf timing");
+    }
+    check(nsh_fir_cascade_ccf(_plan, (const float*)in[0].buffer->read_ptr(),
+                              _zero_hist ? nullptr : (const float*)_hist[_cur], (float*)_hist[_cur ^ 1],
+                              (float*)out[0].buffer->write_ptr(), n_out, s),
+          "hip::fir_filter_cascade_ccf");
+    _zero_hist = false;
+    if (ev) {
+        check(nsh_event_record(ev->second, s), "hip::fir_filter_cascade_ccf timing");
+        _timed_samples += (uint64_t)n_out;
+    }
+    _cur ^= 1;
+    ++_launches;
+    out[0].n_produced = n_out;
+    return work_return_code_t::WORK_OK;
+}
+
+double fir_filter_cascade_ccf::kernel_ms()
+{
+    double total = 0;
+    for (size_t i = 0; i < _ev_used; ++i) {
+        float ms = 0;
+        check(nsh_event_sync(_ev[i].second), "hip::fir_filter_cascade_ccf timing");
+        check(nsh_event_elapsed_ms(_ev[i].first, _ev[i].second, &ms), "hip::fir_filter_cascade_ccf timing");
         total += ms;
     }
     return total;

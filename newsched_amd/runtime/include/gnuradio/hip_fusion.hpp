@@ -59,5 +59,13 @@ fusion_result fuse_elementwise_cc(flat_graph_sptr fg);
 // and product rounding in k_chan1024 as in the three kernels, the output is bit-identical.
 fusion_result fuse_channelizer(flat_graph_sptr fg);
 
+// FIR-chain pass: fir_filter_ccf blocks linked as above (single D2D edges, one input edge each,
+// same tag policy; AUTO algorithm, no preloaded history) are cut into runs of >= 2 stages whose
+// total decimation is 8 or 16 (the longest such run from each position) and each run becomes
+// ONE fir_filter_cascade_ccf: one HBM pass over the input instead of one per stage, results
+// within fp32 transform rounding of the staged chain (not bit-identical: the composite filter is
+// applied by polyphase FFT). scheduler_hip::set_fir_fusion(false) turns it off.
+fusion_result fuse_fir_cascade(flat_graph_sptr fg);
+
 } // namespace hip
 } // namespace gr

@@ -11,8 +11,11 @@
 //
 // Before buffers are allocated, initialize() fuses every maximal chain of elementwise
 // device blocks (multiply_const_cc, copy, multiply_const_chain_cc joined by D2D edges)
-// into one block with one launch per work() call (gnuradio/hip_fusion.hpp). Results are
-// bit-identical; set_fusion(false) keeps every block and edge as connected.
+// into one block with one launch per work() call (gnuradio/hip_fusion.hpp), and
+// fft -> multiply_const_vcc -> ifft into the channelizer; those results are bit-identical.
+// Chains of decimating fir_filter_ccf blocks with total decimation 8 or 16 become one
+// fir_filter_cascade_ccf (within tolerance, not bit-identical; set_fir_fusion(false) keeps
+// them). set_fusion(false) keeps every block and edge as connected.
 #pragma once
 #include <gnuradio/hip_buffer.hpp>
 #include <gnuradio/hip_fusion.hpp>
@@ -40,6 +43,10 @@ public:
     // Elementwise fusion on (default) or off; takes effect at the next initialize().
     void set_fusion(bool on) { _fusion = on; }
     bool fusion() const { return _fusion; }
+    // The FIR-chain pass (hip::fuse_fir_cascade; within tolerance, not bit-identical) on (default)
+    // or off; applies when fusion() is on.
+    void set_fir_fusion(bool on) { _fir_fusion = on; }
+    bool fir_fusion() const { return _fir_fusion; }
     // What the last initialize() fused: blocks that replaced chains, and the chains.
     const hip::fusion_result& fusion_plan() const { return _plan; }
 
@@ -52,6 +59,7 @@ private:
     int _device;
     void* _stream = nullptr;
     bool _fusion = true;
+    bool _fir_fusion = true;
     hip::fusion_result _plan;
 };
 

@@ -1,5 +1,7 @@
 // Elementwise-chain fusion pass for scheduler_hip (see gnuradio/hip_fusion.hpp).
 #include <gnuradio/blocklib/hip/fft.hpp>
+#include <gnuradio/blocklib/hip/fir_filter_cascade_ccf.hpp>
+#include <gnuradio/blocklib/hip/fir_filter_ccf.hpp>
 #include <gnuradio/blocklib/hip/multiply_const.hpp>
 #include <gnuradio/hip_buffer.hpp>
 #include <gnuradio/hip_fusion.hpp>
@@ -217,6 +219,75 @@ fusion_result fuse_channelizer(flat_graph_sptr fg)
         used.insert(b.get());
         used.insert(m.get());
         used.insert(f2.get());
+    }
+    if (r.fused.empty()) return r;
+    r.graph = rewrite_chains(fg, r.chains, r.fused, r);
+    return r;
+}
+
+fusion_result fuse_fir_cascade(flat_graph_sptr fg)
+{
+    fusion_result r;
+    r.graph = fg;
+    auto as_block = [](const node_sptr& n) { return std::dynamic_pointer_cast<block>(n); };
+    auto as_fir = [](const block_sptr& b) -> std::shared_ptr<fir_filter_ccf> {
+        auto f = std::dynamic_pointer_cast<fir_filter_ccf>(b);
+        // a forced algorithm or a preloaded history keeps the block as placed
+        if (!f || f->requested_algo() != 0 || f->has_initial_history()) return nullptr;
+        return f;
+    };
+    std::map<block*, std::vector<edge_sptr>> outs;
+    std::map<block*, int> ins;
+    for (auto& e : fg->edges()) {
+        if (auto s = as_block(e->src().node())) outs[s.get()].push_back(e);
+        if (auto d = as_block(e->dst().node())) ins[d.get()]++;
+    }
+    // the FIR that b's single output edge feeds, if that edge may be fused
+    auto next = [&](const block_sptr& b) -> std::shared_ptr<fir_filter_ccf> {
+        auto it = outs.find(b.get());
+        if (it == outs.end() || it->second.size() != 1) return nullptr;
+        auto e = it->second[0];
+        auto d = as_fir(as_block(e->dst().node()));
+        if (!d || d == b || !device_to_device(e) || ins[d.get()] != 1) return nullptr;
+        if (d->tag_propagation_policy() != b->tag_propagation_policy()) return nullptr;
+        return d;
+    };
+    std::set<block*> interior;
+    for (auto& b : fg->calc_used_blocks())
+        if (as_fir(b))
+            if (auto d = next(b)) interior.insert(d.get());
+    for (auto& b : fg->calc_used_blocks()) {
+        auto head = as_fir(b);
+        if (!head || interior.count(b.get())) continue;
+        std::vector<std::shared_ptr<fir_filter_ccf>> chain{ head };
+        std::set<block*> seen{ b.get() };
+        for (auto d = next(head); d && seen.insert(d.get()).second; d = next(chain.back())) chain.push_back(d);
+        // segments: from each position the longest run of >= 2 stages with total decimation 8 or
+        // 16 that the cascade kernel supports
+        for (size_t i = 0; i < chain.size();) {
+            size_t best = 0;
+            std::vector<fir_filter_cascade_ccf::stage> st, best_st;
+            int64_t dec = 1;
+            for (size_t k = i; k < chain.size(); ++k) {
+                dec *= chain[k]->decimation();
+                if (dec > 16) break;
+                st.emplace_back(chain[k]->taps(), chain[k]->decimation());
+                if (k > i && (dec == 8 || dec == 16) && fir_filter_cascade_ccf::supported(st)) {
+                    best = k - i + 1;
+                    best_st = st;
+                }
+            }
+            if (!best) {
+                ++i;
+                continue;
+            }
+            auto f = fir_filter_cascade_ccf::make(best_st);
+            f->set_tag_propagation_policy(chain[i]->tag_propagation_policy());
+            f->set_alias("fused(" + chain[i]->alias() + ".." + chain[i + best - 1]->alias() + ")");
+            r.chains.emplace_back(chain.begin() + i, chain.begin() + i + best);
+            r.fused.push_back(f);
+            i += best;
+        }
     }
     if (r.fused.empty()) return r;
     r.graph = rewrite_chains(fg, r.chains, r.fused, r);

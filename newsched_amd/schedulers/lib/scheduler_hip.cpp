@@ -48,6 +48,14 @@ void scheduler_hip::initialize(flat_graph_sptr fg, flowgraph_monitor_sptr fgmon,
         _plan.chains.insert(_plan.chains.end(), ch.chains.begin(), ch.chains.end());
         _plan.cut.insert(_plan.cut.end(), ch.cut.begin(), ch.cut.end());
         _plan.added.insert(_plan.added.end(), ch.added.begin(), ch.added.end());
+        if (_fir_fusion) {
+            auto fc = hip::fuse_fir_cascade(_plan.graph);
+            _plan.graph = fc.graph;
+            _plan.fused.insert(_plan.fused.end(), fc.fused.begin(), fc.fused.end());
+            _plan.chains.insert(_plan.chains.end(), fc.chains.begin(), fc.chains.end());
+            _plan.cut.insert(_plan.cut.end(), fc.cut.begin(), fc.cut.end());
+            _plan.added.insert(_plan.added.end(), fc.added.begin(), fc.added.end());
+        }
         fg = _plan.graph;
     }
     scheduler_mt::initialize(fg, fgmon, nbr);

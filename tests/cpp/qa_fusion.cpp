@@ -10,6 +10,8 @@
 #include <gnuradio/blocklib/hip/arith.hpp>
 #include <gnuradio/blocklib/hip/copy.hpp>
 #include <gnuradio/blocklib/hip/fft.hpp>
+#include <gnuradio/blocklib/hip/fir_filter_cascade_ccf.hpp>
+#include <gnuradio/blocklib/hip/fir_filter_ccf.hpp>
 #include <gnuradio/blocklib/hip/multiply_const.hpp>
 #include <gnuradio/flowgraph.hpp>
 #include <gnuradio/hip_buffer.hpp>
@@ -282,4 +284,94 @@ TEST(Fusion, UndoRestoresPortLinks)
         EXPECT_TRUE(snapshot() == before);
         EXPECT_FALSE(connected(xin, r.fused[0]->output_stream_ports()[0]));
     }
+}
+
+// ---- FIR-chain pass (hip::fuse_fir_cascade) ------------------------------------------------
+static std::vector<float> lp(int n)
+{
+    std::vector<float> h((size_t)n);
+    for (int i = 0; i < n; ++i) h[(size_t)i] = 1.0f / (float)(n + i); // any finite taps
+    return h;
+}
+static std::shared_ptr<hip::fir_filter_cascade_ccf> as_casc(const block_sptr& b)
+{
+    return std::dynamic_pointer_cast<hip::fir_filter_cascade_ccf>(b);
+}
+
+// BASELINE C5: src -> 4 x fir(127, 2) -> sink becomes one cascade (D = 16); a fifth stage is left
+TEST(Fusion, FirChainC5)
+{
+    for (int nst : { 4, 5 }) {
+        auto src = blocks::vector_source_c::make(std::vector<gr_complex>(64));
+        auto snk = blocks::null_sink::make(sizeof(gr_complex));
+        auto fg = flowgraph::make();
+        std::vector<block_sptr> firs;
+        for (int i = 0; i < nst; ++i) firs.push_back(hip::fir_filter_ccf::make(lp(127), 2));
+        fg->connect(src, 0, firs[0], 0)->set_custom_buffer(HIP_BUFFER_ARGS_H2D);
+        for (int i = 0; i + 1 < nst; ++i) fg->connect(firs[(size_t)i], 0, firs[(size_t)i + 1], 0);
+        fg->connect(firs.back(), 0, snk, 0)->set_custom_buffer(HIP_BUFFER_ARGS_D2H);
+        auto r = hip::fuse_fir_cascade(flat(fg));
+        ASSERT_TRUE(r.fused.size() == 1u);
+        ASSERT_TRUE(r.chains[0].size() == 4u);
+        auto c = as_casc(r.fused[0]);
+        ASSERT_TRUE(c != nullptr);
+        EXPECT_TRUE(c->decimation() == 16u);
+        EXPECT_TRUE(c->stages().size() == 4u);
+        EXPECT_TRUE(connected(src->output_stream_ports()[0], c->input_stream_ports()[0]));
+        if (nst == 4)
+            EXPECT_TRUE(connected(c->output_stream_ports()[0], snk->input_stream_ports()[0]));
+        else // the fifth stage stays, fed by the cascade
+            EXPECT_TRUE(connected(c->output_stream_ports()[0], firs[4]->input_stream_ports()[0]));
+        EXPECT_TRUE(r.graph->calc_used_blocks().size() == (nst == 4 ? 3u : 4u));
+        r.undo();
+        EXPECT_TRUE(connected(firs[0]->output_stream_ports()[0], firs[1]->input_stream_ports()[0]));
+    }
+}
+
+// runs with total decimation 8 or 16 only; a run that would exceed 16 ends where it still fits
+TEST(Fusion, FirChainSegments)
+{
+    auto count = [](std::vector<int> decims, std::vector<int> ntaps) {
+        auto src = blocks::vector_source_c::make(std::vector<gr_complex>(64));
+        auto snk = blocks::null_sink::make(sizeof(gr_complex));
+        auto fg = flowgraph::make();
+        std::vector<block_sptr> firs;
+        for (size_t i = 0; i < decims.size(); ++i) firs.push_back(hip::fir_filter_ccf::make(lp(ntaps[i]), decims[i]));
+        fg->connect(src, 0, firs[0], 0)->set_custom_buffer(HIP_BUFFER_ARGS_H2D);
+        for (size_t i = 0; i + 1 < firs.size(); ++i) fg->connect(firs[i], 0, firs[i + 1], 0);
+        fg->connect(firs.back(), 0, snk, 0)->set_custom_buffer(HIP_BUFFER_ARGS_D2H);
+        auto r = hip::fuse_fir_cascade(flat(fg));
+        std::vector<size_t> lens;
+        for (auto& c : r.chains) lens.push_back(c.size());
+        return lens;
+    };
+    EXPECT_TRUE(count({ 2, 2 }, { 31, 31 }) == std::vector<size_t>{});              // D = 4: no gain kept
+    EXPECT_TRUE(count({ 2, 2, 2 }, { 31, 31, 31 }) == std::vector<size_t>{ 3 });    // D = 8
+    EXPECT_TRUE(count({ 4, 4 }, { 63, 63 }) == std::vector<size_t>{ 2 });           // D = 16
+    EXPECT_TRUE(count({ 2, 8, 2, 2, 2 }, { 31, 31, 31, 31, 31 }) == (std::vector<size_t>{ 2, 3 }));
+    EXPECT_TRUE(count({ 1, 2, 2, 2 }, { 15, 31, 31, 31 }) == std::vector<size_t>{ 4 }); // decim-1 stage joins
+    EXPECT_TRUE(count({ 2, 2, 2, 2 }, { 1200, 127, 127, 127 }).empty() == false);  // D = 8 prefix fits
+    EXPECT_TRUE(count({ 8, 2 }, { 4200, 3 }).empty());                             // too long for 256 rows
+}
+
+TEST(Fusion, FirChainBoundaries)
+{
+    // 0: forced algorithm, 1: preloaded history, 2: fan-out after stage 2, 3: host edge in the middle
+    auto run = [](int variant) {
+        auto src = blocks::vector_source_c::make(std::vector<gr_complex>(64));
+        auto snk = blocks::null_sink::make(sizeof(gr_complex));
+        auto fg = flowgraph::make();
+        std::vector<std::shared_ptr<hip::fir_filter_ccf>> firs;
+        for (int i = 0; i < 4; ++i) firs.push_back(hip::fir_filter_ccf::make(lp(127), 2, variant == 0 && i == 2 ? 1 : 0));
+        if (variant == 1) firs[1]->set_initial_history(std::vector<gr_complex>(126));
+        fg->connect(src, 0, firs[0], 0)->set_custom_buffer(HIP_BUFFER_ARGS_H2D);
+        for (int i = 0; i < 3; ++i) {
+            auto e = fg->connect(firs[(size_t)i], 0, firs[(size_t)i + 1], 0);
+            if (variant == 3 && i == 1) e->set_custom_buffer(HIP_BUFFER_ARGS_D2H);
+        }
+        if (variant == 2) fg->connect(firs[1], 0, blocks::null_sink::make(sizeof(gr_complex)), 0);
+        fg->connect(firs.back(), 0, snk, 0)->set_custom_buffer(HIP_BUFFER_ARGS_D2H);
+        return hip::fuse_fir_cascade(flat(fg)).fused.size();
+    };
+    for (int v = 0; v < 4; ++v) EXPECT_TRUE(run(v) == 0u);
 }

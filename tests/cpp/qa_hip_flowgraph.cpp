@@ -22,6 +22,7 @@
 #include <gnuradio/blocklib/hip/arith.hpp>
 #include <gnuradio/blocklib/hip/copy.hpp>
 #include <gnuradio/blocklib/hip/fft.hpp>
+#include <gnuradio/blocklib/hip/fir_filter_cascade_ccf.hpp>
 #include <gnuradio/blocklib/hip/fir_filter_ccf.hpp>
 #include <gnuradio/blocklib/hip/multiply_const.hpp>
 #include <gnuradio/blocklib/hip/synth_source.hpp>
@@ -355,22 +356,42 @@ TEST(HipDomain, ChannelizerFromBlocksFused)
 
 TEST(HipDomain, DecimatingChainC5)
 {
-    const size_t n = 1u << 20;
+    // 4 x fir(127, 2): staged (FIR fusion off) and fused by scheduler_hip into one
+    // fir_filter_cascade_ccf (default), both against the in-test chain; 512 KiB buffers make
+    // many work() calls (history hand-off), the fused graph runs twice (restart), and a ragged
+    // length leaves a partial last output group unconsumed in both forms.
     const auto h = lowpass(127, 0.225);
-    auto src = hip::synth_source::make(0, n);
-    std::vector<hip::fir_filter_ccf::sptr> st;
-    for (int i = 0; i < 4; ++i) st.push_back(hip::fir_filter_ccf::make(h, 2));
-    auto snk = blocks::vector_sink_c::make(1, n / 16);
-    auto fg = flowgraph::make();
-    fg->connect(src, 0, st[0], 0);
-    for (int i = 1; i < 4; ++i) fg->connect(st[i - 1], 0, st[i], 0);
-    fg->connect(st[3], 0, snk, 0)->set_custom_buffer(HIP_BUFFER_ARGS_D2H);
-    fg->set_scheduler(schedulers::scheduler_hip::make("hip", 0, 1u << 19));
-    fg->validate();
-    fg->run();
-    auto ref = synth(n);
-    for (int i = 0; i < 4; ++i) ref = fir_ref(ref, h, 2);
-    EXPECT_TRUE(close_normwise(snk->data(), ref));
+    for (size_t n : { size_t(1) << 20, (size_t(1) << 20) + 37 }) {
+        auto ref = synth(n - n % 16);
+        for (int i = 0; i < 4; ++i) ref = fir_ref(ref, h, 2);
+        for (int fused = 0; fused < 2; ++fused) {
+            auto src = hip::synth_source::make(0, n);
+            std::vector<hip::fir_filter_ccf::sptr> st;
+            for (int i = 0; i < 4; ++i) st.push_back(hip::fir_filter_ccf::make(h, 2));
+            auto snk = blocks::vector_sink_c::make(1, n / 16);
+            auto fg = flowgraph::make();
+            fg->connect(src, 0, st[0], 0);
+            for (int i = 1; i < 4; ++i) fg->connect(st[i - 1], 0, st[i], 0);
+            fg->connect(st[3], 0, snk, 0)->set_custom_buffer(HIP_BUFFER_ARGS_D2H);
+            auto sched = schedulers::scheduler_hip::make("hip", 0, 1u << 19);
+            sched->set_fir_fusion(fused == 1);
+            fg->set_scheduler(sched);
+            fg->validate();
+            EXPECT_TRUE(sched->fusion_plan().fused.size() == (fused ? 1u : 0u));
+            for (int run = 0; run < 1 + fused; ++run) {
+                fg->run();
+                ASSERT_TRUE(snk->data().size() == ref.size());
+                EXPECT_TRUE(close_normwise(snk->data(), ref));
+            }
+            if (fused) {
+                auto c = std::dynamic_pointer_cast<hip::fir_filter_cascade_ccf>(sched->fusion_plan().fused[0]);
+                ASSERT_TRUE(c != nullptr);
+                EXPECT_TRUE(c->kernel() == "k_fir_pfft<16>");
+                EXPECT_TRUE(c->launches() > 4u);
+                EXPECT_TRUE(st[0]->launches() == 0u); // the staged blocks were replaced
+            }
+        }
+    }
 }
 
 TEST(HipDomain, CrossThreadDeviceEdges)

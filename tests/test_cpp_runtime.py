@@ -50,4 +50,4 @@ def test_fusion_pass_graph_rewrite():
     """scheduler_hip's fusion passes (elementwise chains, fft -> w -> ifft channelizer) as host
     logic (no device touched)."""
     out = run("qa_fusion", 120)
-    assert "7 test(s), 0 failure(s)" in out
+    assert "10 test(s), 0 failure(s)" in out
