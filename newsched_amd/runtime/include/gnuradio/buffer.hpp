@@ -140,6 +140,12 @@ public:
         _writer_done.store(false);
         _reader_done.store(false);
     }
+    // A restarted flowgraph is a new run: items the previous run wrote but nobody read (a
+    // decimator's input remainder below one output, a source that ran ahead of a head) are
+    // dropped with their tags, so the next run's stream starts at its first item. Called from
+    // prepare_run() with every thread of the previous run finished and every stream drained.
+    // Default: nothing kept (buffers that hold no items of their own, e.g. remote adapters).
+    virtual void discard_unread() {}
 
 protected:
     void set_type(const std::string& t) { _type = t; }
@@ -147,6 +153,13 @@ protected:
     std::string _type;
     uint64_t _total_read = 0;
     uint64_t _total_written = 0;
+    // the discard_unread() bookkeeping shared by the ring buffers (caller holds _buf_mutex)
+    void drop_unread_locked()
+    {
+        _total_read = _total_written;
+        _tags.erase(std::remove_if(_tags.begin(), _tags.end(), [this](const tag_t& t) { return t.offset < _total_read; }),
+                    _tags.end());
+    }
     std::mutex _buf_mutex;
     std::vector<tag_t> _tags;
 

@@ -75,6 +75,10 @@ public:
     {
         if (_buffer_loc == buffer_location_t::LOCAL && _buffer) _buffer->reset_flags();
     }
+    void discard_unread() override
+    {
+        if (_buffer_loc == buffer_location_t::LOCAL && _buffer) _buffer->discard_unread();
+    }
 
     // Forward a notification that arrived at this adapter's port to the far side.
     struct forwarder : neighbor_interface {

@@ -64,6 +64,7 @@ public:
     int device() const { return _dev; }
     void* device_base() const { return _dbase; } // ring start (mapped twice)
     void reset_flags() override;
+    void discard_unread() override;
 
 private:
     size_t readable_locked();

@@ -42,6 +42,7 @@ public:
     void post_read(int num_items) override;
     void post_write(int num_items) override;
     void copy_items(std::shared_ptr<buffer> from, int nitems) override;
+    void discard_unread() override;
 
 protected:
     uint8_t* _buffer = nullptr; // 2 * _buf_size bytes of address space

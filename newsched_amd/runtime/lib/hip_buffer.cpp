@@ -240,4 +240,11 @@ void hip_buffer::copy_items(std::shared_ptr<buffer> from, int nitems)
 
 void hip_buffer::reset_flags() { buffer::reset_flags(); }
 
+void hip_buffer::discard_unread()
+{
+    std::lock_guard<std::mutex> g(_buf_mutex);
+    while (!_pending.empty()) poll_pending_locked(true); // host<->device copies of the last run
+    drop_unread_locked();
+}
+
 } // namespace gr

@@ -89,6 +89,12 @@ bool vmcirc_buffer::write_info(buffer_info_t& info)
     return true;
 }
 
+void vmcirc_buffer::discard_unread()
+{
+    std::lock_guard<std::mutex> g(_buf_mutex);
+    drop_unread_locked();
+}
+
 void vmcirc_buffer::post_read(int n)
 {
     std::lock_guard<std::mutex> g(_buf_mutex);

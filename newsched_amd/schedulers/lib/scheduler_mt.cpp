@@ -97,7 +97,10 @@ void scheduler_mt::prepare_run()
         _n_finished = 0;
     }
     if (_bufman)
-        for (auto& b : _bufman->all_buffers()) b->reset_flags();
+        for (auto& b : _bufman->all_buffers()) {
+            b->reset_flags();
+            b->discard_unread();
+        }
 }
 
 void scheduler_mt::start()

@@ -251,3 +251,31 @@ def test_c5_windowed_large(torch_cuda):
         ry = ref_chain(xs, C5)[start - lo:]
         ok, err, scale = orc.tol_ok(y[start:start + m], ry)
         assert ok, (start, err, scale)
+
+
+def test_c5_many_calls_ring_offsets(torch_cuda):
+    """The flowgraph pattern: one device input buffer read at advancing offsets (multiples of 16
+    samples), outputs written at arbitrary 8-B-aligned offsets of one buffer, ping-pong
+    histories, a side stream; 300 calls of random sizes (1 .. 3000 outputs)."""
+    torch = torch_cuda
+    p = nsh.FirCascadePlan(C5)
+    rng = np.random.default_rng(5)
+    sizes = rng.integers(1, 3000, 300)
+    n_total = int(sizes.sum())
+    x = orc.synth(16 * n_total, 77)
+    ry = ref_chain(x, C5)
+    dx = torch.from_numpy(x).cuda()
+    dy = torch.full((n_total + 1,), complex(5.0, 5.0), dtype=torch.complex64, device="cuda")
+    hs = [torch.empty(1890, dtype=torch.complex64, device="cuda") for _ in range(2)]
+    s = torch.cuda.Stream()
+    pos, cur = 0, 0
+    with torch.cuda.stream(s):
+        for i, m in enumerate(sizes):
+            m = int(m)
+            p(dx[16 * pos:], None if i == 0 else hs[cur], hs[cur ^ 1], dy[1 + pos:], m, stream=s)
+            cur ^= 1
+            pos += m
+    s.synchronize()
+    y = dy.cpu().numpy()[1:]
+    ok, err, scale = orc.tol_ok(y, ry)
+    assert ok, (err, scale, int(np.argmax(np.abs(y - ry))))

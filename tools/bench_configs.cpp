@@ -111,7 +111,8 @@ struct gpu_fg {
     size_t isz;
     int dev = 0;
 
-    gpu_fg(std::vector<block_sptr> chain, int64_t n_items_, size_t isz_, size_t out_buf_bytes, bool fusion = true)
+    gpu_fg(std::vector<block_sptr> chain, int64_t n_items_, size_t isz_, size_t out_buf_bytes, bool fusion = true,
+           bool fir_fusion = true)
         : n_items(n_items_), isz(isz_)
     {
         auto src = blocks::nop_source::make(isz);
@@ -131,6 +132,7 @@ struct gpu_fg {
         fg->connect(chain.back(), 0, snk, 0);
         sched = schedulers::scheduler_hip::make("hip", dev, out_buf_bytes);
         sched->set_fusion(fusion);
+        sched->set_fir_fusion(fir_fusion);
         fg->set_scheduler(sched);
         fg->validate();
         // the head's output edge (its consumer may be a fused block replacing chain[0])
@@ -314,26 +316,35 @@ int main(int argc, char** argv)
     // ---- C5 at G = 1: 4 x (127-tap, D = 2) ----------------------------------------------------
     {
         const auto h = lowpass(127, 0.225); // firwin(127, 0.45)
-        std::vector<block_sptr> chain;
-        for (int i = 0; i < 4; ++i) chain.push_back(hip::fir_filter_ccf::make(h, 2));
-        gpu_fg g(chain, n, sizeof(gr_complex), (size_t)n * sizeof(gr_complex) / 2);
-        const double s = g.run(steps);
         // parity: last 4096 outputs from the last 4096*16 + 4 stage halos of input
         const int64_t m = 4096, win = m * 16 + 2048;
-        auto x = synth(win, n - win);
-        for (int i = 0; i < 4; ++i) x = fir_ref(x, h, 2);
-        std::vector<gr_complex> r(x.end() - m, x.end());
-        auto y = g.tail(m);
-        const double gbs = 8.5 * n / s / 1e9;
+        auto xr = synth(win, n - win);
+        for (int i = 0; i < 4; ++i) xr = fir_ref(xr, h, 2);
+        std::vector<gr_complex> r(xr.end() - m, xr.end());
         const int64_t nc = 1 << 24;
         std::vector<block_sptr> cc;
         for (int i = 0; i < 4; ++i) cc.push_back(blocks::fir_filter_ccf::make(h, 2));
         const double cs = cpu_run(cc, nc);
-        emit("{\"config\": \"C5\", \"variant\": \"G=1: 4 x fir_filter_ccf(127 taps, decim 2) in one scheduler_hip domain\", \"value\": " +
-             num(n / s / 1e6) + ", \"unit\": \"MSamples/s (input)\", \"ms_per_run\": " + num(s * 1e3, 3) +
-             ", \"hbm_bytes_per_input_sample\": 8.5, \"achieved_GBs\": " + num(gbs) + ", \"hbm_frac\": " + num(gbs / hbm, 4) +
-             ", \"parity_tail_rel_err\": " + num(rel_err(y, r), 9) + ", \"cpu_baseline\": {\"value\": " + num(nc / cs / 1e6, 2) +
-             ", \"unit\": \"MSamples/s (input)\", \"sample\": \"2^24 samples, vector_source->head->4x blocks::fir_filter_ccf(decim 2)->null_sink, scheduler_mt thread per block\"}}");
+        for (int fused = 1; fused >= 0; --fused) {
+            std::vector<block_sptr> chain;
+            for (int i = 0; i < 4; ++i) chain.push_back(hip::fir_filter_ccf::make(h, 2));
+            gpu_fg g(chain, n, sizeof(gr_complex), (size_t)n * sizeof(gr_complex) / 2, true, fused == 1);
+            const double s = g.run(steps);
+            auto y = g.tail(m);
+            const double gbs = 8.5 * n / s / 1e9;
+            const char* var = fused ? "G=1: 4 x fir_filter_ccf(127 taps, decim 2), fused by scheduler_hip into one "
+                                      "fir_filter_cascade_ccf (k_fir_pfft<16>, default)"
+                                    : "G=1: 4 x fir_filter_ccf(127 taps, decim 2), FIR fusion off (4 launches, every "
+                                      "stage streams its own input)";
+            emit(std::string("{\"config\": \"C5\", \"variant\": \"") + var + "\", \"value\": " + num(n / s / 1e6) +
+                 ", \"unit\": \"MSamples/s (input)\", \"ms_per_run\": " + num(s * 1e3, 3) +
+                 ", \"hbm_bytes_per_input_sample\": 8.5, \"achieved_GBs\": " + num(gbs) + ", \"hbm_frac\": " +
+                 num(gbs / hbm, 4) + ", \"parity_tail_rel_err\": " + num(rel_err(y, r), 9) +
+                 (fused ? ", \"cpu_baseline\": {\"value\": " + num(nc / cs / 1e6, 2) +
+                              ", \"unit\": \"MSamples/s (input)\", \"sample\": \"2^24 samples, vector_source->head->4x "
+                              "blocks::fir_filter_ccf(decim 2)->null_sink, scheduler_mt thread per block\"}}"
+                        : std::string("}")));
+        }
     }
     // ---- C3 with host endpoints: the PCIe-inclusive rate (not the metric: bench.py's input is
     // resident). vector_source(repeat) -> head -[H2D]-> hip::fir_filter_ccf -[D2H]-> null_sink,
