@@ -249,6 +249,62 @@ def run_fp32_leg(a, n, taps, first, device, barrier, dist, tdev, torch, orc, nsr
             "parity": {"max_abs_err": err, "ok": bool(ok)}}
 
 
+def run_c5_fused_leg(a, first, device, barrier, dist, tdev, torch, orc, nsh):
+    """BASELINE config C5's chain 4 x fir_filter_ccf(firwin(127, 0.45), 2) as the fused kernel
+    scheduler_hip puts in its place (hip::fir_filter_cascade_ccf -> nsh_fir_cascade_ccf,
+    k_fir_pfft<16>): 2^log2n resident input samples per GPU, one launch per step, HIP events on
+    the launch stream; roofline against the chain's 8.5 B per input sample (read 8, write 0.5)."""
+    n = 1 << a.c5_fused_log2n
+    taps = firwin(127, 0.45)
+    plan = nsh.FirCascadePlan([(taps, 2)] * 4, device=device)
+    n_out = n // 16
+    x = torch.empty(n, dtype=torch.complex64, device="cuda")
+    nsh.synth(x, n, first)
+    hist = None
+    if first > 0:  # the shard's halo, regenerated
+        hist = torch.from_numpy(orc.synth(plan.hist_len, first - plan.hist_len)).cuda()
+    y = torch.empty(n_out, dtype=torch.complex64, device="cuda")
+    hout = torch.empty(plan.hist_len, dtype=torch.complex64, device="cuda")
+    s = torch.cuda.Stream()
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < 0.5:
+        plan(x, hist, hout, y, n_out, stream=s)
+        s.synchronize()
+    steps = max(5, a.steps // 4)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    barrier()
+    t0 = time.perf_counter()
+    with torch.cuda.stream(s):
+        for e0, e1 in ev:
+            e0.record(s)
+            plan(x, hist, hout, y, n_out, stream=s)
+            e1.record(s)
+    s.synchronize()
+    barrier()
+    el = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([el], dtype=torch.float64, device=tdev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    avg_ms = sum(e0.elapsed_time(e1) for e0, e1 in ev) / steps
+    m = 4096
+    lo = first + n - 16 * m - C5_HALO
+    xr = orc.synth(16 * m + C5_HALO, lo)
+    for _ in range(4):
+        xr = orc.fir_ccf(xr, taps, 2)
+    ok, err, _ = orc.tol_ok(y[-m:].cpu().numpy(), xr[-m:])
+    plan.close()
+    achieved = 8.5 * n / (avg_ms * 1e-3) / 1e9
+    world = dist.get_world_size() if dist is not None else 1
+    return {"kernel": plan.kernel, "workload": "C5: 4 x fir_filter_ccf(firwin(127,0.45), 2) fused into one "
+            "fir_filter_cascade_ccf, 2^%d resident input samples per GPU" % a.c5_fused_log2n,
+            "steps": steps, "value": round(world * n * steps / el / 1e6, 1), "unit": "MSamples/s (input)",
+            "avg_launch_us": round(avg_ms * 1e3, 2), "achieved_GBs": round(achieved, 1),
+            "bytes_per_input_sample": 8.5, "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "parity": {"check": "last 4096 outputs vs the oracle's 4-stage chain (double accumulation)",
+                       "max_abs_err": err, "ok": bool(ok)}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -264,6 +320,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-log2n", type=int, default=28, help="CPU baseline sample (default: the full stream)")
     ap.add_argument("--c5", choices=["auto", "on", "off"], default="auto", help="C5 pipeline leg (auto: at world > 1)")
+    ap.add_argument("--c5-fused", choices=["on", "off"], default="on",
+                    help="C5's chain as the fused kernel (k_fir_pfft<16>) on resident input, every rank")
+    ap.add_argument("--c5-fused-log2n", type=int, default=28)
     ap.add_argument("--c5-log2n", type=int, default=26)
     ap.add_argument("--c5-steps", type=int, default=5)
     ap.add_argument("--c5-warmup", type=int, default=2)
@@ -424,6 +483,9 @@ def main():
     abandoned = False
     if a.fp32_leg == "on" and a.algo == "auto":
         out["fp32_exact"] = run_fp32_leg(a, n, taps, first, device, barrier, dist, tdev, torch, orc, nsr, nsh)
+
+    if a.c5_fused == "on":
+        out["c5_fused"] = run_c5_fused_leg(a, rank * (1 << a.c5_fused_log2n), device, barrier, dist, tdev, torch, orc, nsh)
 
     if a.c5 == "on" or (a.c5 == "auto" and world > 1):
         out["c5_pipeline"] = run_c5(a, dist, backend, rank, world, device, torch, orc, nsr)

@@ -12,4 +12,6 @@ timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smo
 timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err && echo "bench ok" &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o bench --output-format csv -- python3 bench.py > $O/bench_under_rocprof.json 2> $O/rocprof.err && echo "rocprof ok" &&
 tools/pmc_fir.sh $O/pmc && python3 tools/pmc_summary.py $O/pmc $((1<<25)) $O/pmc_fir.json > /dev/null && echo "pmc ok" &&
+tools/pmc_fir.sh $O/pmc_casc --algo casc && python3 tools/pmc_summary.py $O/pmc_casc $((1<<25)) $O/pmc_casc.json > /dev/null && echo "pmc casc ok" &&
+timeout -k 10 120 python tools/pfft_bench.py > $O/pfft_bench.json 2> $O/pfft_bench.err && echo "pfft bench ok" &&
 timeout -k 10 400 build/tools/bench_configs 28 30 > $O/configs.jsonl 2> $O/configs.err && echo "configs ok"
