@@ -165,7 +165,7 @@ int nsh_fir_cascade_plan_create(int dev, const float* const* taps_host, const in
 int nsh_fir_cascade_plan_destroy(void* plan);
 int nsh_fir_cascade_decim(void* plan);         /* D = prod D_s */
 int nsh_fir_cascade_hist_len(void* plan);      /* len(heq) - 1 */
-const char* nsh_fir_cascade_kernel(void* plan); /* "k_fir_pfft<16>" */
+const char* nsh_fir_cascade_kernel(void* plan); /* "k_fir_pfft<16,1>" */
 int nsh_fir_cascade_ccf(void* plan, const float* in, const float* hist_in, float* hist_out, float* out,
                         int64_t n_out, void* stream);
 

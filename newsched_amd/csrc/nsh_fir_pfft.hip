@@ -145,31 +145,49 @@ __device__ __forceinline__ img_bases bases_of(cf* img)
                       img + j };
 }
 
-// Forward 512-point transform of the values v[r] = x[lane + 64 r] of one wave (Stockham, radix
-// 8, three passes); on return v[r] = X[lane + 64 r]. t2[r] = W_64^{(lane & 7) r},
-// t3[r] = W_512^{lane r}. The image is this wave's own: no workgroup barrier. (The inverse
-// transform is conj(FFT(conj(.))), the conjugations folded into the neighbouring operations.)
-__device__ __forceinline__ void fft512_wave(cf (&v)[8], const img_bases& ib, const cf (&t2)[8], const cf (&t3)[8])
+// Forward 512-point transforms of PW phase sequences per wave, v[i][r] = x_i[lane + 64 r]
+// (Stockham, radix 8, three passes, the PW transforms interleaved pass by pass for ILP); on
+// return v[i][r] = X_i[lane + 64 r]. Transform i exchanges through image i of the wave (ib + i IMG).
+// t2[r] = W_64^{(lane & 7) r}, t3[r] = W_512^{lane r}. The images are this wave's own: no
+// workgroup barrier. (The inverse transform is conj(FFT(conj(.))), the conjugations folded into
+// the neighbouring operations.)
+template <int PW>
+__device__ __forceinline__ void fft512_multi(cf (&v)[PW][8], const img_bases& ib, const cf (&t2)[8], const cf (&t3)[8])
 {
-    dft8<false>(v); // pass 1 (Ns = 1) -> dst[8 j + r]
 #pragma unroll
-    for (int r = 0; r < 8; ++r) ib.x1[r] = v[r];
+    for (int i = 0; i < PW; ++i) dft8<false>(v[i]); // pass 1 (Ns = 1) -> dst[8 j + r]
+#pragma unroll
+    for (int i = 0; i < PW; ++i)
+#pragma unroll
+        for (int r = 0; r < 8; ++r) ib.x1[i * IMG + r] = v[i][r];
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (int r = 0; r < 8; ++r) v[r] = ib.b1[66 * r];
+    for (int i = 0; i < PW; ++i)
 #pragma unroll
-    for (int r = 1; r < 8; ++r) v[r] = cmul_tw(v[r], t2[r]);
-    dft8<false>(v); // pass 2 (Ns = 8) -> dst[(j >> 3) 64 + (j & 7) + 8 r]
+        for (int r = 0; r < 8; ++r) v[i][r] = ib.b1[i * IMG + 66 * r];
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+#pragma unroll
+        for (int r = 1; r < 8; ++r) v[i][r] = cmul_tw(v[i][r], t2[r]);
+        dft8<false>(v[i]); // pass 2 (Ns = 8) -> dst[(j >> 3) 64 + (j & 7) + 8 r]
+    }
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (int r = 0; r < 8; ++r) ib.x2[8 * r + (r >= 4 ? 3 : 0)] = v[r];
+    for (int i = 0; i < PW; ++i)
+#pragma unroll
+        for (int r = 0; r < 8; ++r) ib.x2[i * IMG + 8 * r + (r >= 4 ? 3 : 0)] = v[i][r];
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (int r = 0; r < 8; ++r) v[r] = ib.b2[72 * r];
+    for (int i = 0; i < PW; ++i)
 #pragma unroll
-    for (int r = 1; r < 8; ++r) v[r] = cmul_tw(v[r], t3[r]);
-    dft8<false>(v); // pass 3 (Ns = 64) -> X[j + 64 r], kept in registers
-    __builtin_amdgcn_wave_barrier(); // the image is rewritten next
+        for (int r = 0; r < 8; ++r) v[i][r] = ib.b2[i * IMG + 72 * r];
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+#pragma unroll
+        for (int r = 1; r < 8; ++r) v[i][r] = cmul_tw(v[i][r], t3[r]);
+        dft8<false>(v[i]); // pass 3 (Ns = 64) -> X[j + 64 r], kept in registers
+    }
+    __builtin_amdgcn_wave_barrier(); // the images are rewritten next
 }
 
 __device__ __forceinline__ float2 virt(const float2* __restrict__ in, const float2* __restrict__ hist, int64_t g,
@@ -225,50 +243,62 @@ struct pfft_args {
             a.trace[((f - f0) * 16 + w) * 8 + (k)] = __builtin_amdgcn_s_memtime();                     \
     } while (0)
 
-constexpr int PRE = 4; // 16-B prefetch slots per thread: V rows x P samples / 2 / (64 P) <= 4
+// Workgroup shape: P phases, PW per wave, NT = 64 P / PW threads. A frame's V new rows are P V / 2
+// 16-B loads, i.e. ceil(V PW / 128) <= 4 PW per thread (V <= 512).
+template <int P, int PW>
+struct pshape {
+    static constexpr int NT = 64 * P / PW;
+    static constexpr int WAVES = P / PW;
+    static constexpr int PRE = 4 * PW;
+    static constexpr int RSTEP = 128 / PW; // ring rows between a thread's consecutive slots
+};
 
-template <int P>
-__device__ __forceinline__ void load_rows(float4 (&pre)[PRE], const pfft_args& a, int64_t n_in, int64_t fn)
+template <int P, int PW>
+__device__ __forceinline__ void load_rows(float4 (&pre)[4 * PW], const pfft_args& a, int64_t n_in, int64_t fn)
 {
-    // window fn's new rows = x[P fn V, P (fn + 1) V)
+    using S = pshape<P, PW>;
+    // window fn's new rows = x[P fn V, P (fn + 1) V); slots past them read 0
     const int64_t b = (int64_t)P * fn * a.V;
     const __amdgpu_buffer_rsrc_t r = span_rsrc(a.x + b, n_in - b, (int64_t)P * a.V);
 #pragma unroll
-    for (int k = 0; k < PRE; ++k) pre[k] = nsh::buf_load_f4(r, (int)(threadIdx.x + 64 * P * k) * 16);
+    for (int k = 0; k < S::PRE; ++k) pre[k] = nsh::buf_load_f4(r, (int)(threadIdx.x + S::NT * k) * 16);
 }
 
 // write the prefetched rows of window fn into the ring; returns this thread's max magnitude bits.
-// Slot k of thread t holds samples 2 i, 2 i + 1, i = t + 64 P k: rows (2 t) / P + 128 k, phases
-// (2 t) % P and + 1 -- one swizzle for every k (128 k / (32 / P) is a multiple of P), so each
-// ring entry is one of two bases plus 128 P k, modulo the ring.
-template <int P>
-__device__ __forceinline__ unsigned store_rows(const float4 (&pre)[PRE], cf* __restrict__ ring, const pfft_args& a, int64_t fn)
+// Slot k of thread t holds samples 2 i, 2 i + 1, i = t + NT k: rows (2 t) / P + RSTEP k, phases
+// (2 t) % P and + 1 -- one swizzle for every k (RSTEP k / (32 / P) is a multiple of P), so each
+// ring entry is one of two bases plus RSTEP P k, modulo the ring.
+template <int P, int PW>
+__device__ __forceinline__ unsigned store_rows(const float4 (&pre)[4 * PW], cf* __restrict__ ring,
+                                               const pfft_args& a, int64_t fn)
 {
+    using S = pshape<P, PW>;
     const int items = P * a.V / 2;
     const int t = threadIdx.x;
     const int s0 = (int)((fn * a.V + a.Q + (2 * t) / P) & (M - 1)), ph = (2 * t) % P;
     const int ea = ring_at<P>(s0, ph), eb = ring_at<P>(s0, ph + 1);
     unsigned m = 0;
 #pragma unroll
-    for (int k = 0; k < PRE; ++k) {
-        if (t + 64 * P * k < items) {
-            ring[(ea + 128 * P * k) & (M * P - 1)] = cf{ pre[k].x, pre[k].y };
-            ring[(eb + 128 * P * k) & (M * P - 1)] = cf{ pre[k].z, pre[k].w };
+    for (int k = 0; k < S::PRE; ++k) {
+        if (t + S::NT * k < items) {
+            ring[(ea + S::RSTEP * P * k) & (M * P - 1)] = cf{ pre[k].x, pre[k].y };
+            ring[(eb + S::RSTEP * P * k) & (M * P - 1)] = cf{ pre[k].z, pre[k].w };
             m = max(m, maxbits4(pre[k]));
         }
     }
     return m;
 }
 
-template <int P>
-__global__ __launch_bounds__(64 * P, 1) void k_fir_pfft(pfft_args a)
+template <int P, int PW>
+__global__ __launch_bounds__(64 * P / PW, 1) void k_fir_pfft(pfft_args a)
 {
-    constexpr int NT = 64 * P;
+    using S = pshape<P, PW>;
+    constexpr int NT = S::NT, WAVES = S::WAVES;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     cf* ring = reinterpret_cast<cf*>(lds);   // M * P
     cf* imgs = ring + M * P;                  // P * IMG
     cf* zb = imgs + P * IMG;                  // IMG
-    unsigned* mx = reinterpret_cast<unsigned*>(zb + IMG); // [2][P] per-wave max bits of new rows
+    unsigned* mx = reinterpret_cast<unsigned*>(zb + IMG); // [2][WAVES] per-wave max bits of new rows
 
     const int tid = threadIdx.x, j = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6); // wave-uniform: SGPR arithmetic
@@ -277,19 +307,22 @@ __global__ __launch_bounds__(64 * P, 1) void k_fir_pfft(pfft_args a)
     if (f0 >= f1) return; // whole workgroup
     const int64_t n_in = a.n_out * P;
     const int L = a.L, Q = a.Q, V = a.V;
-    const img_bases ib = bases_of(imgs + w * IMG);
+    const img_bases ib = bases_of(imgs + w * PW * IMG); // the wave's PW images; products in the first
 
     if (a.hist_out && blockIdx.x == gridDim.x - 1) // the next call's history: the L-1 samples before x[n_in]
         for (int k = tid; k < L - 1; k += NT) a.hist_out[k] = virt(a.x, a.hist_in, n_in - (L - 1) + k, n_in, L);
 
-    cf t2[8], t3[8], fw[8];
+    cf t2[8], t3[8], fw[PW][8];
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
         const float2 u = a.tw[8 * (((j & 7) * r) & 63)], v = a.tw[(j * r) & (M - 1)];
         t2[r] = cf{ u.x, u.y };
         t3[r] = cf{ v.x, v.y };
-        const float2 f = a.F[w * M + j + 64 * r];
-        fw[r] = cf{ f.x, f.y };
+#pragma unroll
+        for (int i = 0; i < PW; ++i) {
+            const float2 f = a.F[(w * PW + i) * M + j + 64 * r];
+            fw[i][r] = cf{ f.x, f.y };
+        }
     }
 
     // first window: rows [f0 V, f0 V + M), history-aware
@@ -302,11 +335,11 @@ __global__ __launch_bounds__(64 * P, 1) void k_fir_pfft(pfft_args a)
     }
     m = nsh::wave_umax(m);
     if (j == 0) {
-        mx[(f0 & 1) * P + w] = m;
-        mx[((f0 + 1) & 1) * P + w] = 0u;
+        mx[(f0 & 1) * WAVES + w] = m;
+        mx[((f0 + 1) & 1) * WAVES + w] = 0u;
     }
-    float4 pre[PRE];
-    load_rows<P>(pre, a, n_in, f0 + 1);
+    float4 pre[S::PRE];
+    load_rows<P, PW>(pre, a, n_in, f0 + 1);
     nsh::lds_barrier();
 
     for (int64_t f = f0; f < f1; ++f) {
@@ -315,17 +348,19 @@ __global__ __launch_bounds__(64 * P, 1) void k_fir_pfft(pfft_args a)
         // of the transform phase: the CU's texture path moves 64 B/clk, so the 50 KB of a frame's
         // new rows take ~800 cycles to issue and ~800 to return -- issued in phase B they held
         // every wave there; here they overlap the transforms.
-        if (f > f0 && !(NSH_PFFT_ABLATE & 4)) load_rows<P>(pre, a, n_in, f + 1 < f1 ? f + 1 : a.nf + 1);
+        if (f > f0 && !(NSH_PFFT_ABLATE & 4)) load_rows<P, PW>(pre, a, n_in, f + 1 < f1 ? f + 1 : a.nf + 1);
         // Re-define the per-lane constants each frame (empty asm): otherwise the compiler hoists
         // the swizzled/negated copies that cmulw's operand modifiers give for free, i.e. holds
         // every twiddle twice (the kernel has 128 VGPRs at 16 waves per CU).
 #pragma unroll
-        for (int r = 0; r < 8; ++r) asm volatile("" : "+v"(fw[r]));
+        for (int i = 0; i < PW; ++i)
+#pragma unroll
+            for (int r = 0; r < 8; ++r) asm volatile("" : "+v"(fw[i][r]));
 #pragma unroll
         for (int r = 1; r < 8; ++r) asm volatile("" : "+v"(t2[r]), "+v"(t3[r]));
         // the window's largest magnitude: this frame's new rows and the previous frame's (which
         // hold the overlap; the first window's slot covers all of it)
-        const unsigned wm = nsh::wave_umax(j < 2 * P ? mx[j] : 0u); // one LDS read, DPP max
+        const unsigned wm = nsh::wave_umax(j < 2 * WAVES ? mx[j] : 0u); // one LDS read, DPP max
         const bool bad = wm >= 0x7f800000u; // inf or NaN in the window
         int ks = 127 - (int)(wm >> 23);      // max * 2^ks in [1, 2)
         ks = ks > 126 ? 126 : (ks < -126 ? -126 : ks);
@@ -334,14 +369,24 @@ __global__ __launch_bounds__(64 * P, 1) void k_fir_pfft(pfft_args a)
         const int64_t rowf = f * V;
         if (!bad) {
             // rows rowf + j + 64 r share one swizzle (64 r moves s / (32 / P) by a multiple of P)
-            const int e0 = ring_at<P>((int)((rowf + j) & (M - 1)), w);
-            cf v[8];
+            const int sr = (int)((rowf + j) & (M - 1));
+            cf v[PW][8];
 #pragma unroll
-            for (int r = 0; r < 8; ++r)
-                v[r] = (NSH_PFFT_ABLATE & 16) ? cf{ sc, (float)r } : ring[(e0 + 64 * P * r) & (M * P - 1)] * sc;
-            if (!(NSH_PFFT_ABLATE & 2)) fft512_wave(v, ib, t2, t3);
+            for (int i = 0; i < PW; ++i) {
+                const int e0 = ring_at<P>(sr, w * PW + i);
 #pragma unroll
-            for (int r = 0; r < 8; ++r) ib.n[64 * r] = cmul_tw(v[r], fw[r]);
+                for (int r = 0; r < 8; ++r)
+                    v[i][r] = (NSH_PFFT_ABLATE & 16) ? cf{ sc, (float)r } : ring[(e0 + 64 * P * r) & (M * P - 1)] * sc;
+            }
+            if (!(NSH_PFFT_ABLATE & 2)) fft512_multi<PW>(v, ib, t2, t3);
+            // this wave's share of the phase sum, in a fixed order (deterministic)
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                cf pr = cmul_tw(v[0][r], fw[0][r]);
+#pragma unroll
+                for (int i = 1; i < PW; ++i) pr += cmul_tw(v[i][r], fw[i][r]);
+                ib.n[64 * r] = pr;
+            }
         } else {
             // fp32 direct form on the composite taps: y[j] = sum_n heq[n] u[P q - n], q = Q + t
             for (int t = tid; t < V; t += NT) {
@@ -358,17 +403,20 @@ __global__ __launch_bounds__(64 * P, 1) void k_fir_pfft(pfft_args a)
         PFFT_T(1);
         nsh::lds_barrier(); // B1: window f read, images hold the per-phase products
         PFFT_T(2);
-        if (!bad && tid < M) {
-            const cf* src = imgs + tid;
-            cf z = src[0];
+        if (!bad) {
 #pragma unroll
-            for (int p = 1; p < ((NSH_PFFT_ABLATE & 8) ? 1 : P); ++p) z += src[p * IMG];
-            zb[tid] = cf{ z.x, -z.y }; // conj: the inverse runs as a forward transform
+            for (int k = tid; k < M; k += NT) {
+                const cf* src = imgs + k;
+                cf z = src[0];
+#pragma unroll
+                for (int u = 1; u < ((NSH_PFFT_ABLATE & 8) ? 1 : WAVES); ++u) z += src[u * PW * IMG];
+                zb[k] = cf{ z.x, -z.y }; // conj: the inverse runs as a forward transform
+            }
         }
         PFFT_T(6);
         if (f + 1 < f1) {
-            unsigned mn = nsh::wave_umax(store_rows<P>(pre, ring, a, f + 1));
-            if (j == 0) mx[((f + 1) & 1) * P + w] = mn;
+            unsigned mn = nsh::wave_umax(store_rows<P, PW>(pre, ring, a, f + 1));
+            if (j == 0) mx[((f + 1) & 1) * WAVES + w] = mn;
             PFFT_T(7);
         }
         PFFT_T(3);
@@ -377,17 +425,17 @@ __global__ __launch_bounds__(64 * P, 1) void k_fir_pfft(pfft_args a)
         // the inverse transform goes to one of waves 0..3 (one per SIMD, the oldest and so the
         // first in each SIMD's issue arbitration), rotating over the four SIMDs
         if (!(NSH_PFFT_ABLATE & 1) && !bad && w == (int)(f & 3)) {
-            cf v[8];
+            cf v[1][8];
 #pragma unroll
-            for (int r = 0; r < 8; ++r) v[r] = zb[j + 64 * r];
-            fft512_wave(v, ib, t2, t3);
+            for (int r = 0; r < 8; ++r) v[0][r] = zb[j + 64 * r];
+            fft512_multi<1>(v, ib, t2, t3);
             const __amdgpu_buffer_rsrc_t ro = span_rsrc(a.out + rowf, a.n_out - rowf, V);
             const cf us = cf{ usc, -usc }; // 2^-k and the output conjugation
             int ob = (j - Q) * 8;
             asm volatile("" : "+v"(ob)); // computed here, not hoisted (8 offsets would spill)
 #pragma unroll
             for (int r = 0; r < 8; ++r)
-                if (j + 64 * r >= Q) nsh::buf_store_f2(ro, ob + 512 * r, v[r] * us);
+                if (j + 64 * r >= Q) nsh::buf_store_f2(ro, ob + 512 * r, v[0][r] * us);
             PFFT_T(5);
         }
     }
@@ -403,6 +451,15 @@ hipError_t set_lds_attr(const void* fn, int bytes, int dev)
     if (e == hipSuccess) done.insert({ fn, dev });
     return e;
 }
+
+// Phases per wave. Two per wave (8 waves at P = 16, half the product and reduction LDS traffic,
+// two independent transforms per wave) measured 650 vs 600 us per 2^28 inputs against one per
+// wave (16 waves: more waves per SIMD to cover LDS latency; profiles/r02i_ab_pfft_pw.log).
+#ifndef NSH_PFFT_PW16
+#define NSH_PFFT_PW16 1
+#endif
+constexpr int PW16 = NSH_PFFT_PW16;
+constexpr int PW8 = 1;
 
 template <int P>
 constexpr int lds_bytes()
@@ -504,7 +561,7 @@ int nsh_fir_cascade_plan_create(int dev, const float* const* taps_host, const in
     if (e == hipSuccess) e = hipMemcpy(p->tw, tw.data(), tw.size() * sizeof(float2), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(p->heq, hf.data(), hf.size() * sizeof(float), hipMemcpyHostToDevice);
     if (e == hipSuccess) {
-        const void* fn = D == 16 ? (const void*)k_fir_pfft<16> : (const void*)k_fir_pfft<8>;
+        const void* fn = D == 16 ? (const void*)k_fir_pfft<16, PW16> : (const void*)k_fir_pfft<8, PW8>;
         e = set_lds_attr(fn, D == 16 ? lds_bytes<16>() : lds_bytes<8>(), p->dev);
     }
     if (e != hipSuccess) {
@@ -514,7 +571,7 @@ int nsh_fir_cascade_plan_create(int dev, const float* const* taps_host, const in
         delete p;
         return nsh::fail(e, "nsh_fir_cascade_plan_create");
     }
-    p->kernel = "k_fir_pfft<" + std::to_string(D) + ">";
+    p->kernel = "k_fir_pfft<" + std::to_string(D) + "," + std::to_string(D == 16 ? PW16 : PW8) + ">";
     *plan = p;
     return 0;
 }
@@ -570,9 +627,11 @@ int nsh_fir_cascade_ccf(void* plan, const float* in, const float* hist_in, float
 #endif
     wg = (a.nf + a.fpw - 1) / a.fpw;
     if (p->D == 16)
-        hipLaunchKernelGGL(k_fir_pfft<16>, dim3((unsigned)wg), dim3(1024), lds_bytes<16>(), nsh::S(stream), a);
+        hipLaunchKernelGGL((k_fir_pfft<16, PW16>), dim3((unsigned)wg), dim3(pshape<16, PW16>::NT), lds_bytes<16>(),
+                           nsh::S(stream), a);
     else
-        hipLaunchKernelGGL(k_fir_pfft<8>, dim3((unsigned)wg), dim3(512), lds_bytes<8>(), nsh::S(stream), a);
+        hipLaunchKernelGGL((k_fir_pfft<8, PW8>), dim3((unsigned)wg), dim3(pshape<8, PW8>::NT), lds_bytes<8>(),
+                           nsh::S(stream), a);
     NSH_CK_LAUNCH("nsh_fir_cascade_ccf");
     return 0;
 }

@@ -393,7 +393,7 @@ TEST(HipDomain, DecimatingChainC5)
             if (fused) {
                 auto c = std::dynamic_pointer_cast<hip::fir_filter_cascade_ccf>(sched->fusion_plan().fused[0]);
                 ASSERT_TRUE(c != nullptr);
-                EXPECT_TRUE(c->kernel() == "k_fir_pfft<16>");
+                EXPECT_TRUE(c->kernel() == "k_fir_pfft<16,1>");
                 EXPECT_TRUE(c->launches() > 4u);
                 EXPECT_TRUE(st[0]->launches() == 0u); // the staged blocks were replaced
             }

@@ -74,7 +74,7 @@ def run_pfft(torch, plan, x, n_out, hist=None, want_hist=True):
 
 def test_c5_plan_shape(torch_cuda):
     p = nsh.FirCascadePlan(C5)
-    assert p.decim == 16 and p.hist_len == 1890 and p.kernel == "k_fir_pfft<16>"
+    assert p.decim == 16 and p.hist_len == 1890 and p.kernel == "k_fir_pfft<16,1>"
 
 
 @pytest.mark.parametrize("n_out", [1, 2, 118, 119, 392, 393, 394, 786, 787, 5000, 393 * 256, 393 * 256 + 1,
