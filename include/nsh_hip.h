@@ -110,8 +110,8 @@ int nsh_synth_cf32(float* out, int64_t n, uint64_t first_index, uint64_t seed, v
  *   hist_out : receives the ntaps-1 samples that precede the NEXT call's in[0]
  *              (must not alias hist_in -- ping-pong two buffers)
  * algo: NSH_FIR_AUTO picks by measurement (MFMA for decim 1, 2, 4 with finite
- * taps, else DIRECT); NSH_FIR_DIRECT is the fp32 VALU direct form (any decim; the only form
- * for decim 8 and above); NSH_FIR_MFMA is the split-precision Toeplitz form on the matrix
+ * taps, PFFT for decim 8 and 16, else DIRECT); NSH_FIR_DIRECT is the fp32 VALU direct form
+ * (decim 1, 2, 4, 8); NSH_FIR_MFMA is the split-precision Toeplitz form on the matrix
  * cores: decim 1 on 32-sample blocks, ntaps <= 161, fp16x2 at a per-chunk power-of-two scale
  * with three products (k_fir_mfma12; chunks holding non-finite or fp16-subnormal-range
  * samples take the fp32 direct form inside the same launch); decim 2 and 4 as the polyphase
@@ -119,14 +119,18 @@ int nsh_synth_cf32(float* out, int64_t n, uint64_t first_index, uint64_t seed, v
  * ntaps <= 145); NSH_FIR_MFMA_BF16X3 forces the bf16x3 six-product kernel for decim 1;
  * NSH_FIR_MFMA_F32 is the exact-fp32 Toeplitz form on the fp32-input matrix instructions
  * (decim 1, ntaps <= 257, finite taps; no operand split: fp32 products and sums, chunks with
- * inf/NaN through the fp32 direct form in the same launch). */
+ * inf/NaN through the fp32 direct form in the same launch). NSH_FIR_PFFT (decim 8 and 16; AUTO
+ * picks it there when ceil((ntaps-1)/decim) <= 256 and the taps are finite): the polyphase-FFT
+ * overlap-save kernel of nsh_fir_cascade_ccf with one stage (k_fir_pfft<decim,1>; within fp32
+ * transform rounding of the direct form, see below); decim 16 is only available as PFFT. */
 enum nsh_fir_algo {
     NSH_FIR_AUTO = 0,
     NSH_FIR_DIRECT = 1,
     NSH_FIR_MFMA = 2,
     NSH_FIR_MFMA16 = 3,
     NSH_FIR_MFMA_BF16X3 = 4,
-    NSH_FIR_MFMA_F32 = 5
+    NSH_FIR_MFMA_F32 = 5,
+    NSH_FIR_PFFT = 6
 };
 int nsh_fir_plan_create(int dev, const float* taps_host, int ntaps, int decim, int algo, void** plan);
 int nsh_fir_plan_destroy(void* plan);

@@ -119,8 +119,8 @@ fir_filter_ccf::fir_filter_ccf(const std::vector<float>& taps, int decim, int al
     : decim_block("fir_filter_ccf (hip)", (unsigned)decim), _taps(taps), _decim(decim), _algo(algo)
 {
     if (taps.empty()) throw std::invalid_argument("hip::fir_filter_ccf: no taps");
-    if (decim != 1 && decim != 2 && decim != 4 && decim != 8)
-        throw std::invalid_argument("hip::fir_filter_ccf: decimation must be 1, 2, 4 or 8");
+    if (decim != 1 && decim != 2 && decim != 4 && decim != 8 && decim != 16)
+        throw std::invalid_argument("hip::fir_filter_ccf: decimation must be 1, 2, 4, 8 or 16");
 }
 
 fir_filter_ccf::~fir_filter_ccf() { release(); }

@@ -146,8 +146,8 @@ extern "C" {
 int nsh_fir_plan_create(int dev, const float* taps_host, int ntaps, int decim, int algo, void** plan)
 {
     if (ntaps < 1 || ntaps > 4096) return nsh::fail_msg("nsh_fir_plan_create: ntaps must be in [1, 4096]");
-    if (decim != 1 && decim != 2 && decim != 4 && decim != 8)
-        return nsh::fail_msg("nsh_fir_plan_create: decimation must be 1, 2, 4 or 8");
+    if (decim != 1 && decim != 2 && decim != 4 && decim != 8 && decim != 16)
+        return nsh::fail_msg("nsh_fir_plan_create: decimation must be 1, 2, 4, 8 or 16");
     NSH_CK(hipSetDevice(dev));
     auto* p = new nsh_fir_plan();
     p->dev = dev;
@@ -164,7 +164,7 @@ int nsh_fir_plan_create(int dev, const float* taps_host, int ntaps, int decim, i
         delete p;
         return nsh::fail(e, "nsh_fir_plan_create: taps upload");
     }
-    if (algo < NSH_FIR_AUTO || algo > NSH_FIR_MFMA_F32) {
+    if (algo < NSH_FIR_AUTO || algo > NSH_FIR_PFFT) {
         (void)hipFree(p->taps_dev);
         delete p;
         return nsh::fail_msg("nsh_fir_plan_create: unknown algorithm");
@@ -174,7 +174,32 @@ int nsh_fir_plan_create(int dev, const float* taps_host, int ntaps, int decim, i
         resolved = NSH_FIR_MFMA;
         p->force_x3 = true;
     }
-    if (algo == NSH_FIR_AUTO) resolved = nsh_fir_mfma_supported(p) ? NSH_FIR_MFMA : NSH_FIR_DIRECT;
+    // decim 8 and 16: the polyphase-FFT kernel (k_fir_pfft; 2x the direct form at 127 taps, 5x at
+    // 511) when the filter fits its 256 overlap rows, else the direct form (decim 8 only)
+    const bool pfft_ok = (decim == 8 || decim == 16) && (ntaps - 1 + decim - 1) / decim <= 256 &&
+                         std::all_of(taps_host, taps_host + ntaps, [](float v) { return std::isfinite(v); });
+    if (algo == NSH_FIR_AUTO)
+        resolved = pfft_ok ? NSH_FIR_PFFT : (nsh_fir_mfma_supported(p) ? NSH_FIR_MFMA : NSH_FIR_DIRECT);
+    if ((resolved == NSH_FIR_PFFT && !pfft_ok) || (decim == 16 && resolved != NSH_FIR_PFFT)) {
+        (void)hipFree(p->taps_dev);
+        delete p;
+        return nsh::fail_msg("nsh_fir_plan_create: PFFT needs decim 8 or 16, finite taps and ntaps <= 256 decim + 1; "
+                             "decim 16 needs PFFT");
+    }
+    if (resolved == NSH_FIR_PFFT) {
+        const float* tp[1] = { taps_host };
+        const int nt[1] = { ntaps }, dc[1] = { decim };
+        const int rc = nsh_fir_cascade_plan_create(dev, tp, nt, dc, 1, &p->casc);
+        if (rc) {
+            (void)hipFree(p->taps_dev);
+            delete p;
+            return rc;
+        }
+        p->algo = NSH_FIR_PFFT;
+        p->kernel = nsh_fir_cascade_kernel(p->casc);
+        *plan = p;
+        return 0;
+    }
     if (resolved == NSH_FIR_MFMA16 && !nsh_fir_mfma16_supported(p)) {
         (void)hipFree(p->taps_dev);
         delete p;
@@ -229,6 +254,7 @@ int nsh_fir_plan_destroy(void* plan)
     if (p->tf32_dev) (void)hipFree(p->tf32_dev);
     if (p->fragd_dev) (void)hipFree(p->fragd_dev);
     if (p->fragd8_dev) (void)hipFree(p->fragd8_dev);
+    if (p->casc) nsh_fir_cascade_plan_destroy(p->casc);
     delete p;
     return 0;
 }
@@ -243,6 +269,7 @@ int nsh_fir_ccf(void* plan, const float* in, const float* hist_in, float* hist_o
     if (n_out <= 0) return 0;
     if (hist_in == hist_out && p->L > 1) return nsh::fail_msg("nsh_fir_ccf: hist_out must not alias hist_in");
     hipStream_t s = nsh::S(stream);
+    if (p->algo == NSH_FIR_PFFT) return nsh_fir_cascade_ccf(p->casc, in, hist_in, hist_out, out, n_out, stream);
     if (p->algo == NSH_FIR_MFMA || p->algo == NSH_FIR_MFMA_BF16X3)
         return nsh_fir_mfma_run(p, (const float2*)in, (const float2*)hist_in, (float2*)hist_out, (float2*)out, n_out, s);
     if (p->algo == NSH_FIR_MFMA_F32)

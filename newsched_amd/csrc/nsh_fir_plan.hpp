@@ -37,6 +37,7 @@ struct nsh_fir_plan {
     // as 4 shifted copies [4][16 QF + 16] fp32
     int QF = 0;
     void* tf32_dev = nullptr;
+    void* casc = nullptr; // NSH_FIR_PFFT: a one-stage nsh_fir_cascade plan (k_fir_pfft)
     bool force_x3 = false; // NSH_FIR_MFMA_BF16X3: always the bf16x3 six-product kernel
     int variant = 0;      // MFMA kernel tuning variant (0 = default)
     int wg_per_cu = 0;    // decim-1 fp16x2 kernel: workgroups per CU over the launch (0 = auto)

@@ -18,7 +18,7 @@ LIB_DIR = os.path.join(_HERE, "lib")
 HIP_LIB = os.path.join(LIB_DIR, "libnsh_hip.so")
 
 NSH_H2D, NSH_D2H, NSH_D2D, NSH_DEFAULT = 0, 1, 2, 3
-FIR_AUTO, FIR_DIRECT, FIR_MFMA, FIR_MFMA16, FIR_MFMA_BF16X3, FIR_MFMA_F32 = 0, 1, 2, 3, 4, 5
+FIR_AUTO, FIR_DIRECT, FIR_MFMA, FIR_MFMA16, FIR_MFMA_BF16X3, FIR_MFMA_F32, FIR_PFFT = 0, 1, 2, 3, 4, 5, 6
 
 # name -> (restype, argtypes); mirrors include/nsh_hip.h exactly (tests check the header).
 _vp, _i, _i64, _u64, _sz, _f = C.c_void_p, C.c_int, C.c_int64, C.c_uint64, C.c_size_t, C.c_float

@@ -277,7 +277,8 @@ def test_fir_decim_auto_picks_mfma(torch_cuda):
     h = np.hanning(127).astype(np.float32)
     assert nsh.FirPlan(h, 2).algo == nsh.FIR_MFMA
     assert nsh.FirPlan(h, 4).algo == nsh.FIR_MFMA
-    assert nsh.FirPlan(h, 8).algo == nsh.FIR_DIRECT
+    assert nsh.FirPlan(h, 8).algo == nsh.FIR_PFFT
+    assert nsh.FirPlan(np.ones(2100, np.float32) / 2100, 8).algo == nsh.FIR_DIRECT  # 263 overlap rows > 256
 
 
 @pytest.mark.parametrize("decim", [2, 4])

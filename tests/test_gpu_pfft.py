@@ -279,3 +279,38 @@ def test_c5_many_calls_ring_offsets(torch_cuda):
     y = dy.cpu().numpy()[1:]
     ok, err, scale = orc.tol_ok(y, ry)
     assert ok, (err, scale, int(np.argmax(np.abs(y - ry))))
+
+
+@pytest.mark.parametrize("decim", [8, 16])
+@pytest.mark.parametrize("ntaps", [1, 31, 127, 511, 2049])
+def test_firplan_auto_pfft(torch_cuda, decim, ntaps):
+    """nsh_fir_plan_create(AUTO) routes decim 8 and 16 to the polyphase-FFT kernel (one-stage
+    cascade): same nsh_fir_ccf contract (ntaps-1 history, ping-pong), against the oracle over
+    calls of several sizes."""
+    torch = torch_cuda
+    if (ntaps - 1 + decim - 1) // decim > 256:
+        with pytest.raises(nsh.NshError):
+            nsh.FirPlan(np.ones(ntaps, np.float32), decim)  # decim 16 has no other form
+        return
+    h = np.asarray(__import__("scipy.signal", fromlist=["firwin"]).firwin(ntaps, 0.8 / decim), np.float32) \
+        if ntaps > 1 else np.array([0.75], np.float32)
+    plan = nsh.FirPlan(h, decim)
+    assert plan.algo == nsh.FIR_PFFT and plan.kernel == "k_fir_pfft<%d,1>" % decim
+    cuts = [0, 3, 500, 501, 9000, 40000]
+    x = orc.synth(decim * cuts[-1], ntaps)
+    ref = orc.fir_ccf(x, h, decim)
+    hist = torch.zeros(max(ntaps - 1, 1), dtype=torch.complex64, device="cuda")
+    hout = torch.zeros_like(hist)
+    parts = []
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        dx = torch.from_numpy(x[decim * a:decim * b]).cuda()
+        dy = torch.empty(b - a, dtype=torch.complex64, device="cuda")
+        plan(dx, hist if a else 0, hout, dy, b - a)
+        torch.cuda.synchronize()
+        hist, hout = hout, hist
+        parts.append(dy.cpu().numpy())
+    y = np.concatenate(parts)
+    ok, err, scale = tol_pfft(y, ref, x, [(h, decim)])
+    assert ok, (decim, ntaps, err, scale)
+    ok, err, scale = orc.tol_ok(y[500:], ref[500:])  # past the zero-history transient: the plain rule
+    assert ok, (decim, ntaps, err, scale)
