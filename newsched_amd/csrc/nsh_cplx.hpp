@@ -16,6 +16,20 @@ __device__ __forceinline__ cf cmulw(cf a, cf w)
 {
     return __builtin_elementwise_fma(a.yy, cf{ -w.y, w.x }, a.xx * w);
 }
+// a * w as two packed instructions with the operand swap and the one negation as VOP3P
+// modifiers: v_pk_mul (w.x broadcast) + v_pk_fma (a swapped, its low half negated, w.y broadcast).
+// Written in C (cmulw) the compiler materialises (-w.y, w.x) with a v_xor + v_mov per use when w
+// is loaded or loop-carried; s_nop 0 covers the packed-math read-after-write wait it would insert.
+// re = fma(-a.y, w.y, w.x a.x), im = fma(a.x, w.y, w.x a.y)
+__device__ __forceinline__ cf cmul_asm(cf a, cf w)
+{
+    cf d;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]\n\ts_nop 0\n\t"
+        "v_pk_fma_f32 %0, %2, %1, %0 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_lo:[1,0,0]\n\ts_nop 0"
+        : "=&v"(d)
+        : "v"(w), "v"(a));
+    return d;
+}
 // a * conj(w): re = fma(a.y, w.y, a.x w.x), im = fma(a.y, w.x, -a.x w.y)
 __device__ __forceinline__ cf cmulc(cf a, cf w)
 {

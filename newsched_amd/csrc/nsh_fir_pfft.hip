@@ -66,19 +66,12 @@ using nsh::rot;
 #ifndef NSH_PFFT_ASM_CMUL
 #define NSH_PFFT_ASM_CMUL 1
 #endif
-// a * w for a per-lane constant w (twiddles, filter spectrum): v_pk_mul (w.x broadcast) + v_pk_fma
-// with the swap and the one negation of a as operand modifiers. Written in C (cmulw) the compiler
-// materialises (-w.y, w.x) with a v_xor + v_mov per use; s_nop 0 covers the packed-math
-// read-after-write wait it would insert itself.
+// a * w for the per-lane twiddles and the filter spectrum: nsh::cmul_asm (the C form cost a
+// v_xor + v_mov per product, ~4 % of the kernel)
 __device__ __forceinline__ cf cmul_tw(cf a, cf w)
 {
 #if NSH_PFFT_ASM_CMUL
-    cf d;
-    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]\n\ts_nop 0\n\t"
-        "v_pk_fma_f32 %0, %2, %1, %0 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_lo:[1,0,0]\n\ts_nop 0"
-        : "=&v"(d)
-        : "v"(w), "v"(a));
-    return d;
+    return nsh::cmul_asm(a, w);
 #else
     return cmulw(a, w);
 #endif
