@@ -51,7 +51,8 @@
 
 // Timing-only ablation hooks for tools/probe/pfft_ab.py (0 in every product build): 1 = no inverse
 // transform, 2 = no forward transform, 4 = no global loads, 8 = no phase reduction, 16 = no
-// window reads from the ring.
+// window reads from the ring, 32 = no ring writes, 64 = no exchange writes, 128 = no product
+// writes.
 #ifndef NSH_PFFT_ABLATE
 #define NSH_PFFT_ABLATE 0
 #endif
@@ -83,12 +84,15 @@ constexpr int IMG = 572;         // a wave's LDS image: the largest padded index
                                 // replays at 64-128 cycles)
 
 // Three layouts of a wave's 512-entry image, each bank-conflict-free for both of its access
-// patterns over every 32-lane half (a 64-bit access covers banks 2e, 2e+1 of entry e), and each
-// a base register plus immediate offsets (layouts found by exhaustive search over paddings):
-//   exchange 1 (pass-1 stores at 8 j + r, pass-2 loads at j + 64 r):        e = i + (i >> 5)
+// patterns as the compiler emits them -- stores (ds_write_b64 / ds_write2_b64) and paired loads
+// (ds_read2_b64) serve 16-lane groups from 32 banks, i.e. 16 distinct entries mod 16 per group
+// (MI355X_MICROARCH.md §LDS) -- and each a base register plus immediate offsets (exhaustive
+// search over paddings, tools/probe/lds_banks.py):
+//   exchange 1 (pass-1 stores at 8 j + r, pass-2 loads at j + 64 r):        e = i + (i >> 4)
 //   exchange 2 (pass-2 stores at 64 (j >> 3) + (j & 7) + 8 r, pass-3 loads):  e = i + 3 (i >> 5) + 2 (i >> 6)
 //   products / reduction / Z (stores and loads at j + 64 r, or at tid):       e = i
-// (i + (i >> 3) made 2-way conflicts on every natural-order access: 34 % of LDS cycles.)
+// (i + (i >> 3) made 2-way conflicts on every natural-order access: 34 % of LDS cycles; i + (i >> 5),
+// conflict-free under the 32-lane model of ds_read_b64, left the exchange-1 stores 2-way.)
 
 // ring entry of (slot s, phase p): rows of P samples, phase XOR-swizzled by (s / (32 / P)) so
 // that 32 consecutive slots read at one phase hit 32 distinct bank pairs
@@ -119,8 +123,8 @@ __device__ __forceinline__ void dft8(cf (&v)[8])
 }
 
 // A wave's image addresses (one base register each, the rest immediate offsets):
-//   x1 + r        = e1(8 j + r)       = 8 j + (j >> 2) + r
-//   b1 + 66 r     = e1(j + 64 r)      = j + (j >> 5) + 66 r
+//   x1 + r        = e1(8 j + r)       = 8 j + (j >> 1) + r
+//   b1 + 68 r     = e1(j + 64 r)      = j + (j >> 4) + 68 r
 //   x2 + o2(r)    = e2(64 (j >> 3) + (j & 7) + 8 r) = 72 (j >> 3) + (j & 7) + 8 r + 3 [r >= 4]
 //   b2 + 72 r     = e2(j + 64 r)      = j + 3 (j >> 5) + 72 r
 //   n  + 64 r     = j + 64 r          (products, natural order)
@@ -134,8 +138,60 @@ struct img_bases {
 __device__ __forceinline__ img_bases bases_of(cf* img)
 {
     const int j = threadIdx.x & 63;
-    return img_bases{ img + 8 * j + (j >> 2), img + j + (j >> 5), img + 72 * (j >> 3) + (j & 7), img + j + 3 * (j >> 5),
+    return img_bases{ img + 8 * j + (j >> 1), img + j + (j >> 4), img + 72 * (j >> 3) + (j & 7), img + j + 3 * (j >> 5),
                       img + j };
+}
+
+#ifndef NSH_PFFT_REGX2
+#define NSH_PFFT_REGX2 0
+#endif
+// Exchange 2 without LDS. Stockham's pass-2 -> pass-3 exchange moves (lane 8 a + b, register r) to
+// (lane 8 r + b, register a): it swaps lane bits 3..5 with register bits 0..2, one bit pair at a
+// time -- lane bit 5 <-> register bit 2 by v_permlane32_swap on (v[r], v[r + 4]), lane bit 4 <->
+// register bit 1 by v_permlane16_swap on (v[r], v[r + 2]), lane bit 3 <-> register bit 0 by DPP
+// row_ror:8 moves on (v[r], v[r + 1]) whose bank_mask writes only the lanes that change (lanes
+// 8..15 of each row take v[r + 1] from 8 lanes down, lanes 0..7 take v[r] from 8 lanes up).
+// 32 VALU instructions (40 as compiled) per transform instead of 8 LDS stores and 8 loads.
+// Bit-identical; measured no faster (572 vs 569 us per 2^28 inputs, profiles/r02j_pfft_lds_ab.log):
+// the VALU it adds costs what the LDS traffic it removes did. Off by default.
+__device__ __forceinline__ void swap32(cf& a, cf& b)
+{
+    const auto x = __builtin_amdgcn_permlane32_swap(__float_as_uint(a.x), __float_as_uint(b.x), false, false);
+    const auto y = __builtin_amdgcn_permlane32_swap(__float_as_uint(a.y), __float_as_uint(b.y), false, false);
+    a = cf{ __uint_as_float(x[0]), __uint_as_float(y[0]) };
+    b = cf{ __uint_as_float(x[1]), __uint_as_float(y[1]) };
+}
+__device__ __forceinline__ void swap16(cf& a, cf& b)
+{
+    const auto x = __builtin_amdgcn_permlane16_swap(__float_as_uint(a.x), __float_as_uint(b.x), false, false);
+    const auto y = __builtin_amdgcn_permlane16_swap(__float_as_uint(a.y), __float_as_uint(b.y), false, false);
+    a = cf{ __uint_as_float(x[0]), __uint_as_float(y[0]) };
+    b = cf{ __uint_as_float(x[1]), __uint_as_float(y[1]) };
+}
+__device__ __forceinline__ float ror8_into(float old, float src, int bank_mask_is_upper)
+{
+    return bank_mask_is_upper
+               ? __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(src), 0x128, 0xf, 0xc, false))
+               : __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(src), 0x128, 0xf, 0x3, false));
+}
+__device__ __forceinline__ void swap8(cf& a, cf& b)
+{
+    const cf na = cf{ ror8_into(a.x, b.x, 1), ror8_into(a.y, b.y, 1) };
+    const cf nb = cf{ ror8_into(b.x, a.x, 0), ror8_into(b.y, a.y, 0) };
+    a = na;
+    b = nb;
+}
+__device__ __forceinline__ void exchange2_regs(cf (&v)[8])
+{
+#pragma unroll
+    for (int r = 0; r < 4; ++r) swap32(v[r], v[r + 4]);
+#pragma unroll
+    for (int r = 0; r < 8; r += 4) {
+        swap16(v[r], v[r + 2]);
+        swap16(v[r + 1], v[r + 3]);
+    }
+#pragma unroll
+    for (int r = 0; r < 8; r += 2) swap8(v[r], v[r + 1]);
 }
 
 // Forward 512-point transforms of PW phase sequences per wave, v[i][r] = x_i[lane + 64 r]
@@ -152,28 +208,35 @@ __device__ __forceinline__ void fft512_multi(cf (&v)[PW][8], const img_bases& ib
 #pragma unroll
     for (int i = 0; i < PW; ++i)
 #pragma unroll
-        for (int r = 0; r < 8; ++r) ib.x1[i * IMG + r] = v[i][r];
+        for (int r = 0; r < 8; ++r)
+            if (!(NSH_PFFT_ABLATE & 64)) ib.x1[i * IMG + r] = v[i][r];
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int i = 0; i < PW; ++i)
 #pragma unroll
-        for (int r = 0; r < 8; ++r) v[i][r] = ib.b1[i * IMG + 66 * r];
+        for (int r = 0; r < 8; ++r) v[i][r] = ib.b1[i * IMG + 68 * r];
 #pragma unroll
     for (int i = 0; i < PW; ++i) {
 #pragma unroll
         for (int r = 1; r < 8; ++r) v[i][r] = cmul_tw(v[i][r], t2[r]);
         dft8<false>(v[i]); // pass 2 (Ns = 8) -> dst[(j >> 3) 64 + (j & 7) + 8 r]
     }
-    __builtin_amdgcn_wave_barrier();
+    if (NSH_PFFT_REGX2) {
 #pragma unroll
-    for (int i = 0; i < PW; ++i)
+        for (int i = 0; i < PW; ++i) exchange2_regs(v[i]);
+    } else {
+        __builtin_amdgcn_wave_barrier();
 #pragma unroll
-        for (int r = 0; r < 8; ++r) ib.x2[i * IMG + 8 * r + (r >= 4 ? 3 : 0)] = v[i][r];
-    __builtin_amdgcn_wave_barrier();
+        for (int i = 0; i < PW; ++i)
 #pragma unroll
-    for (int i = 0; i < PW; ++i)
+            for (int r = 0; r < 8; ++r)
+                if (!(NSH_PFFT_ABLATE & 64)) ib.x2[i * IMG + 8 * r + (r >= 4 ? 3 : 0)] = v[i][r];
+        __builtin_amdgcn_wave_barrier();
 #pragma unroll
-        for (int r = 0; r < 8; ++r) v[i][r] = ib.b2[i * IMG + 72 * r];
+        for (int i = 0; i < PW; ++i)
+#pragma unroll
+            for (int r = 0; r < 8; ++r) v[i][r] = ib.b2[i * IMG + 72 * r];
+    }
 #pragma unroll
     for (int i = 0; i < PW; ++i) {
 #pragma unroll
@@ -246,6 +309,31 @@ struct pshape {
     static constexpr int RSTEP = 128 / PW; // ring rows between a thread's consecutive slots
 };
 
+#ifndef NSH_PFFT_SPLIT_READS
+#define NSH_PFFT_SPLIT_READS 1
+#endif
+#ifndef NSH_PFFT_SCALE_ALWAYS
+#define NSH_PFFT_SCALE_ALWAYS 0
+#endif
+#ifndef NSH_PFFT_ROWPERM
+#define NSH_PFFT_ROWPERM 1
+#endif
+// The 16-B slot (2 samples, phases 2m and 2m + 1 of one row) that thread t moves: a permutation of
+// the slots within each wave's 1 KiB (loads stay one contiguous 1 KiB per wave-instruction) such
+// that each 16-lane store group covers rows whose swizzles differ in parity -- P = 16: rows b and
+// b + 2; P = 8: rows b, b + 1, b + 4, b + 5 -- so its 16 ring entries are distinct mod 16 (a
+// ds_write_b64 group's banks). In wave order the group covered rows b, b + 1, which share their
+// swizzle: every ring store was 2-way conflicted.
+template <int P>
+__device__ __forceinline__ int row_slot(int t)
+{
+    if (!NSH_PFFT_ROWPERM) return t;
+    const int l = t & 63, g = l >> 4;
+    if (P == 16) return (t & ~63) + (4 * (g >> 1) + (g & 1) + 2 * ((l >> 3) & 1)) * 8 + (l & 7);
+    const int h = (l >> 2) & 3;
+    return (t & ~63) + (8 * (g >> 1) + 2 * (g & 1) + (h & 1) + 4 * (h >> 1)) * 4 + (l & 3);
+}
+
 template <int P, int PW>
 __device__ __forceinline__ void load_rows(float4 (&pre)[4 * PW], const pfft_args& a, int64_t n_in, int64_t fn)
 {
@@ -254,20 +342,20 @@ __device__ __forceinline__ void load_rows(float4 (&pre)[4 * PW], const pfft_args
     const int64_t b = (int64_t)P * fn * a.V;
     const __amdgpu_buffer_rsrc_t r = span_rsrc(a.x + b, n_in - b, (int64_t)P * a.V);
 #pragma unroll
-    for (int k = 0; k < S::PRE; ++k) pre[k] = nsh::buf_load_f4(r, (int)(threadIdx.x + S::NT * k) * 16);
+    for (int k = 0; k < S::PRE; ++k) pre[k] = nsh::buf_load_f4(r, (row_slot<P>(threadIdx.x) + S::NT * k) * 16);
 }
 
 // write the prefetched rows of window fn into the ring; returns this thread's max magnitude bits.
-// Slot k of thread t holds samples 2 i, 2 i + 1, i = t + NT k: rows (2 t) / P + RSTEP k, phases
-// (2 t) % P and + 1 -- one swizzle for every k (RSTEP k / (32 / P) is a multiple of P), so each
-// ring entry is one of two bases plus RSTEP P k, modulo the ring.
+// Slot k of thread t holds samples 2 i, 2 i + 1, i = u + NT k, u = row_slot(t): rows (2 u) / P +
+// RSTEP k, phases (2 u) % P and + 1 -- one swizzle for every k (RSTEP k / (32 / P) is a multiple
+// of P), so each ring entry is one of two bases plus RSTEP P k, modulo the ring.
 template <int P, int PW>
 __device__ __forceinline__ unsigned store_rows(const float4 (&pre)[4 * PW], cf* __restrict__ ring,
                                                const pfft_args& a, int64_t fn)
 {
     using S = pshape<P, PW>;
     const int items = P * a.V / 2;
-    const int t = threadIdx.x;
+    const int t = row_slot<P>(threadIdx.x);
     const int s0 = (int)((fn * a.V + a.Q + (2 * t) / P) & (M - 1)), ph = (2 * t) % P;
     const int ea = ring_at<P>(s0, ph), eb = ring_at<P>(s0, ph + 1);
     unsigned m = 0;
@@ -357,6 +445,11 @@ __global__ __launch_bounds__(64 * P / PW, 1) void k_fir_pfft(pfft_args a)
         const bool bad = wm >= 0x7f800000u; // inf or NaN in the window
         int ks = 127 - (int)(wm >> 23);      // max * 2^ks in [1, 2)
         ks = ks > 126 ? 126 : (ks < -126 ? -126 : ks);
+        // A window whose largest magnitude lies in [2^-40, 2^41) -- every stream but extreme ones --
+        // is not scaled: a power-of-two scale is exact, so this changes no output bit, and none of
+        // such a frame's intermediates leaves fp32's normal range (saves 8 packed multiplies).
+        const bool scale = NSH_PFFT_SCALE_ALWAYS || ks < -40 || ks > 40;
+        if (!scale) ks = 0;
         const float sc = __uint_as_float((unsigned)(ks + 127) << 23);
         const float usc = __uint_as_float((unsigned)(127 - ks) << 23);
         const int64_t rowf = f * V;
@@ -369,7 +462,13 @@ __global__ __launch_bounds__(64 * P / PW, 1) void k_fir_pfft(pfft_args a)
                 const int e0 = ring_at<P>(sr, w * PW + i);
 #pragma unroll
                 for (int r = 0; r < 8; ++r)
-                    v[i][r] = (NSH_PFFT_ABLATE & 16) ? cf{ sc, (float)r } : ring[(e0 + 64 * P * r) & (M * P - 1)] * sc;
+                    v[i][r] = (NSH_PFFT_ABLATE & 16) ? cf{ sc, (float)r } : ring[(e0 + 64 * P * r) & (M * P - 1)];
+            }
+            if (scale) { // wave-uniform branch
+#pragma unroll
+                for (int i = 0; i < PW; ++i)
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) v[i][r] *= sc;
             }
             if (!(NSH_PFFT_ABLATE & 2)) fft512_multi<PW>(v, ib, t2, t3);
             // this wave's share of the phase sum, in a fixed order (deterministic)
@@ -378,7 +477,7 @@ __global__ __launch_bounds__(64 * P / PW, 1) void k_fir_pfft(pfft_args a)
                 cf pr = cmul_tw(v[0][r], fw[0][r]);
 #pragma unroll
                 for (int i = 1; i < PW; ++i) pr += cmul_tw(v[i][r], fw[i][r]);
-                ib.n[64 * r] = pr;
+                if (!(NSH_PFFT_ABLATE & 128)) ib.n[64 * r] = pr;
             }
         } else {
             // fp32 direct form on the composite taps: y[j] = sum_n heq[n] u[P q - n], q = Q + t
@@ -400,9 +499,17 @@ __global__ __launch_bounds__(64 * P / PW, 1) void k_fir_pfft(pfft_args a)
 #pragma unroll
             for (int k = tid; k < M; k += NT) {
                 const cf* src = imgs + k;
-                cf z = src[0];
+                // all WAVES loads first, as separate ds_read_b64 (paired ds_read2_b64 run at half
+                // the LDS read rate), then the sum in a fixed order
+                cf pv[WAVES];
 #pragma unroll
-                for (int u = 1; u < ((NSH_PFFT_ABLATE & 8) ? 1 : WAVES); ++u) z += src[u * PW * IMG];
+                for (int u = 0; u < WAVES; ++u) {
+                    pv[u] = src[u * PW * IMG];
+                    if (NSH_PFFT_SPLIT_READS) asm volatile("" ::: "memory");
+                }
+                cf z = pv[0];
+#pragma unroll
+                for (int u = 1; u < ((NSH_PFFT_ABLATE & 8) ? 1 : WAVES); ++u) z += pv[u];
                 zb[k] = cf{ z.x, -z.y }; // conj: the inverse runs as a forward transform
             }
         }
