@@ -1417,6 +1417,19 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma9(const float2* __restrict__
 // (L1/L2 hits: every workgroup reads the same bytes).
 // Scale and exact-path test cover the chunk and its halo. Results match v9 to within the
 // split's rounding (v9's scale also covered the whole previous chunk), not bit for bit.
+#ifndef NSH_V12_LDS_PAD
+#define NSH_V12_LDS_PAD 0 // probe builds: extra LDS per workgroup (fewer resident workgroups per CU)
+#endif
+// Shifted tap copies: 4, read as two ds_read_b64 per B fragment (8-B aligned), or 8, read as one
+// ds_read_b128 (16-B aligned). Four copies take 3.5 KiB instead of 7 at Q = 5, which brings the
+// workgroup to 25.5 KiB of LDS: 6 resident workgroups per CU instead of 5 (LDS-bound; 72 VGPRs
+// would allow 7) -- the kernel's rate follows the chunks in flight per CU (5 -> 4 resident
+// workgroups: 734 -> 802 us per 2^28, profiles/r02j_v12_occupancy_ab.log).
+#ifndef NSH_V12_COPIES
+#define NSH_V12_COPIES 4
+#endif
+constexpr int v12_tw(int Q) { return 32 * Q + (NSH_V12_COPIES == 8 ? 24 : 32); } // fp16 per copy (multiple of 8)
+typedef __attribute__((ext_vector_type(4))) _Float16 f16x4;
 template <int Q>
 struct geom12 {
     static constexpr int NT = 256;
@@ -1426,15 +1439,18 @@ struct geom12 {
     static constexpr int NB = (CHUNK + H) / 32;
     static constexpr int PLANE = (NB * 80 + 255) / 256 * 256;
     static constexpr int BUF = 4 * PLANE;
-    static constexpr int TW = 32 * Q + 24;                           // fp16 per shifted copy
+    static constexpr int NCP = NSH_V12_COPIES;                       // shifted copies per plane
+    static constexpr int TW = v12_tw(Q);                             // fp16 per shifted copy
     static constexpr int COPY = ((2 * TW + 63) / 128) * 128 + 64;    // bytes, = 64 mod 128, >= 2 TW
-    static constexpr int TAPS = 2 * 8 * COPY;                        // [plane][shift] copies
-    static constexpr int IMG_UNITS = 2 * 8 * TW / 8;                 // 16-B units of the global image
+    static constexpr int TAPS = 2 * NCP * COPY;                      // [plane][shift] copies
+    static constexpr int IMG_UNITS = 2 * NCP * TW / 8;               // 16-B units of the global image
     static constexpr int SLOTS = BUF + TAPS;                         // u32 max[4], mnz[4]
-    static constexpr int LDS = SLOTS + 32;
+    static constexpr int LDS = SLOTS + 32 + NSH_V12_LDS_PAD;
     static_assert(COPY >= 2 * TW && COPY % 128 == 64, "copy pitch");
     static_assert((HP + 4 * NT) * 16 <= BUF, "a raw fp32 chunk + halo fits the plane buffer");
     static_assert(HP <= NT, "halo pairs: one per thread");
+    static_assert(NCP == 4 || NCP == 8, "4 or 8 shifted tap copies");
+    static_assert(IMG_UNITS <= 2 * NT, "tap image: two 16-B units per thread at most");
 };
 
 template <int Q>
@@ -1563,9 +1579,24 @@ __global__ __launch_bounds__(256) void k_fir_mfma12(const float2* __restrict__ i
                 const f16x8 A1 = *reinterpret_cast<const f16x8*>(lds + off + G::PLANE);
                 // taps h[t0 - j], t0 = i - 16 (st & 1) - 8 h + 32 (st >> 1): R[m0 + j], m0 = 32Q - 1 - t0
                 const int m0 = 32 * Q - 1 - rho + 16 * (st & 1) + 8 * h - 32 * (st >> 1);
-                const int tb = (m0 & 7) * G::COPY + 2 * (m0 & ~7);
-                const f16x8 B0 = *reinterpret_cast<const f16x8*>(tl + tb);
-                const f16x8 B1 = *reinterpret_cast<const f16x8*>(tl + 8 * G::COPY + tb);
+                const int tb = (m0 & (G::NCP - 1)) * G::COPY + 2 * (m0 & ~(G::NCP - 1));
+                f16x8 B0, B1;
+                if (G::NCP == 8) {
+                    B0 = *reinterpret_cast<const f16x8*>(tl + tb);
+                    B1 = *reinterpret_cast<const f16x8*>(tl + G::NCP * G::COPY + tb);
+                } else {
+                    // four separate ds_read_b64 (the empty asm keeps the compiler from pairing
+                    // them into ds_read2_b64, whose 16-lane groups conflict 2-way on this image)
+                    const f16x4 b0 = *reinterpret_cast<const f16x4*>(tl + tb);
+                    asm volatile("" ::: "memory");
+                    const f16x4 b1 = *reinterpret_cast<const f16x4*>(tl + tb + 8);
+                    asm volatile("" ::: "memory");
+                    const f16x4 b2 = *reinterpret_cast<const f16x4*>(tl + G::NCP * G::COPY + tb);
+                    asm volatile("" ::: "memory");
+                    const f16x4 b3 = *reinterpret_cast<const f16x4*>(tl + G::NCP * G::COPY + tb + 8);
+                    B0 = __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7);
+                    B1 = __builtin_shufflevector(b2, b3, 0, 1, 2, 3, 4, 5, 6, 7);
+                }
 #if NSH_FIR_ABLATE & 256 // timing only: LDS fragment reads kept, no matrix work
                 acc_hi[st & 15] += (float)A0[0] + (float)A1[1] + (float)B0[2] + (float)B1[3];
                 continue;
@@ -1602,8 +1633,6 @@ __global__ __launch_bounds__(256) void k_fir_mfma12(const float2* __restrict__ i
     if (c_first == 0) // the last L-1 inputs for the next call (after this workgroup's stores)
         for (int j = tid; j < L - 1; j += G::NT) hist_out[j] = virt(in, hist_in, n_in - (L - 1) + j, n_in, L);
 }
-
-typedef __attribute__((ext_vector_type(4))) _Float16 f16x4;
 
 // ---- k_fir_mfma11: decimating polyphase FIR (D = 2, 4) on the fp16x2 split -----------------
 // k_fir_mfma7's polyphase Toeplitz form (phase streams z_0[i] = x[D i], z_r[i] = x[D i + D - r],
@@ -2787,15 +2816,15 @@ int nsh_fir_mfma_prepare(nsh_fir_plan* p)
                     }
             p->sh8 = sh;
             // v12 tap image: R[m] = h[32Q - 1 - m] (scaled, hi/lo fp16), copy k holds R[k .. k + TW)
-            const int TW = 32 * Q + 24;
-            std::vector<_Float16> f12((size_t)2 * 8 * TW, (_Float16)0.f);
-            for (int k = 0; k < 8; ++k)
+            const int TW = v12_tw(Q), NCP = NSH_V12_COPIES;
+            std::vector<_Float16> f12((size_t)2 * NCP * TW, (_Float16)0.f);
+            for (int k = 0; k < NCP; ++k)
                 for (int e = 0; e < TW; ++e) {
                     const int t = 32 * Q - 1 - (e + k);
                     const float hs = (t >= 0 && t < p->L) ? std::ldexp(p->taps_host[t], sh) : 0.f;
                     const _Float16 h0 = (_Float16)hs;
-                    f12[(size_t)(0 * 8 + k) * TW + e] = h0;
-                    f12[(size_t)(1 * 8 + k) * TW + e] = (_Float16)(hs - (float)h0);
+                    f12[(size_t)(0 * NCP + k) * TW + e] = h0;
+                    f12[(size_t)(1 * NCP + k) * TW + e] = (_Float16)(hs - (float)h0);
                 }
             NSH_CK(hipMalloc(&p->frag12_dev, f12.size() * sizeof(_Float16)));
             NSH_CK(hipMemcpy(p->frag12_dev, f12.data(), f12.size() * sizeof(_Float16), hipMemcpyHostToDevice));
