@@ -1429,6 +1429,15 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma9(const float2* __restrict__
 #define NSH_V12_COPIES 4
 #endif
 constexpr int v12_tw(int Q) { return 32 * Q + (NSH_V12_COPIES == 8 ? 24 : 32); } // fp16 per copy (multiple of 8)
+// Plane row pitch (32 fp16 samples = 64 B per row): 80 B (v9's padded rows) or 64 B with the
+// row's four 16-B chunks XOR-swizzled by (row >> 2) & 3. Either way each 16-lane group of an
+// A-fragment ds_read_b128 (16 consecutive rows, one chunk) hits 16 distinct 16-B slots; the
+// unpadded form takes 17 KiB instead of 22 for the four planes (20.5 KiB per workgroup with the
+// 4-copy tap image: 7 resident workgroups per CU, the 72-VGPR limit) but measured slower than 6
+// (732 vs 708-719 us, bit-identical; profiles/r02j_v12_occupancy_ab.log): 80 is the default.
+#ifndef NSH_V12_PITCH
+#define NSH_V12_PITCH 80
+#endif
 typedef __attribute__((ext_vector_type(4))) _Float16 f16x4;
 template <int Q>
 struct geom12 {
@@ -1437,7 +1446,8 @@ struct geom12 {
     static constexpr int H = 32 * (Q - 1);
     static constexpr int HP = H / 2;
     static constexpr int NB = (CHUNK + H) / 32;
-    static constexpr int PLANE = (NB * 80 + 255) / 256 * 256;
+    static constexpr int PITCH = NSH_V12_PITCH;
+    static constexpr int PLANE = (NB * PITCH + 255) / 256 * 256;
     static constexpr int BUF = 4 * PLANE;
     static constexpr int NCP = NSH_V12_COPIES;                       // shifted copies per plane
     static constexpr int TW = v12_tw(Q);                             // fp16 per shifted copy
@@ -1450,8 +1460,30 @@ struct geom12 {
     static_assert((HP + 4 * NT) * 16 <= BUF, "a raw fp32 chunk + halo fits the plane buffer");
     static_assert(HP <= NT, "halo pairs: one per thread");
     static_assert(NCP == 4 || NCP == 8, "4 or 8 shifted tap copies");
+    static_assert(PITCH == 64 || PITCH == 80, "plane pitch");
+    // byte offset of sample s (even) in a plane
+    static __device__ __forceinline__ int at(int s)
+    {
+        const int row = s >> 5;
+        if (PITCH == 80) return row * 80 + (s & 31) * 2;
+        return row * 64 + ((((s >> 3) & 3) ^ ((row >> 2) & 3)) << 4) + (s & 7) * 2;
+    }
     static_assert(IMG_UNITS <= 2 * NT, "tap image: two 16-B units per thread at most");
 };
+
+template <int Q>
+__device__ __forceinline__ void store_pair12(const float4& v, unsigned char* buf, int s, int sc)
+{
+    using G = geom12<Q>;
+    const int off = G::at(s);
+    unsigned rh, rl, ih, il;
+    split_pair16(v.x, v.z, sc, rh, rl);
+    split_pair16(v.y, v.w, sc, ih, il);
+    *reinterpret_cast<unsigned*>(buf + 0 * G::PLANE + off) = rh;
+    *reinterpret_cast<unsigned*>(buf + 1 * G::PLANE + off) = rl;
+    *reinterpret_cast<unsigned*>(buf + 2 * G::PLANE + off) = ih;
+    *reinterpret_cast<unsigned*>(buf + 3 * G::PLANE + off) = il;
+}
 
 template <int Q>
 __global__ __launch_bounds__(256) void k_fir_mfma12(const float2* __restrict__ in,
@@ -1559,9 +1591,9 @@ __global__ __launch_bounds__(256) void k_fir_mfma12(const float2* __restrict__ i
 #pragma unroll
             for (int u = 0; u < 4; ++u) r[G::HP + tid + G::NT * u] = v[u];
         } else {
-            if (tid < G::HP) store_pair9<Q>(hv, lds, 2 * tid, s);
+            if (tid < G::HP) store_pair12<Q>(hv, lds, 2 * tid, s);
 #pragma unroll
-            for (int u = 0; u < 4; ++u) store_pair9<Q>(v[u], lds, G::H + 2 * (tid + G::NT * u), s);
+            for (int u = 0; u < 4; ++u) store_pair12<Q>(v[u], lds, G::H + 2 * (tid + G::NT * u), s);
         }
         nsh::lds_barrier();
         nf2 o[8];
@@ -1569,12 +1601,19 @@ __global__ __launch_bounds__(256) void k_fir_mfma12(const float2* __restrict__ i
             direct_tile9<Q>(lds, taps, L, wave, h, phase, o);
         } else {
             const int b = rho & 15, c = rho >> 4;
-            const int a_base = c * 2 * G::PLANE + ((Q - 1) + 16 * wave + b) * 80 + 16 * h;
+            const int row0 = (Q - 1) + 16 * wave + b; // A rows: row0 - (st >> 1); chunks h + 2 (st & 1)
+            const int a_base = c * 2 * G::PLANE + row0 * G::PITCH + 16 * h;
             f32x16 acc_hi = {};
             f32x16 acc_lo = {};
 #pragma unroll
             for (int st = 0; st < 2 * Q; ++st) {
-                const int off = a_base - (st >> 1) * 80 + 32 * (st & 1);
+                int off;
+                if (G::PITCH == 80) {
+                    off = a_base - (st >> 1) * 80 + 32 * (st & 1);
+                } else {
+                    const int row = row0 - (st >> 1);
+                    off = c * 2 * G::PLANE + row * 64 + (((h + 2 * (st & 1)) ^ ((row >> 2) & 3)) << 4);
+                }
                 const f16x8 A0 = *reinterpret_cast<const f16x8*>(lds + off);
                 const f16x8 A1 = *reinterpret_cast<const f16x8*>(lds + off + G::PLANE);
                 // taps h[t0 - j], t0 = i - 16 (st & 1) - 8 h + 32 (st >> 1): R[m0 + j], m0 = 32Q - 1 - t0
