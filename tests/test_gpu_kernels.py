@@ -592,3 +592,51 @@ def test_fir_mfma_f32_nonfinite_and_range(torch_cuda):
     fin = np.isfinite(ref)
     big = np.abs(ref[fin]).max()
     assert np.all(np.abs(y[fin] - ref[fin]) <= 1e-5 * np.abs(ref[fin]) + 1e-6 * big)
+
+
+def test_fir_headline_full_size(torch_cuda):
+    """BASELINE C3 at its full size: the default plan (k_fir_mfma12) over 2^28 samples, as
+    bench.py runs it. Oracle windows at the stream's start and end, at chunk boundaries that are
+    also XCD-range boundaries of the chunk remap (per_x chunks per XCD), and at random chunks;
+    linearity FIR(0.5 x1 + x2) == 0.5 FIR(x1) + FIR(x2) over the whole stream; outputs are
+    deterministic (a second run is bit-identical)."""
+    torch = torch_cuda
+    n = 1 << 28
+    h = _firwin127()
+    plan = nsh.FirPlan(h, 1)
+    assert plan.kernel.startswith("k_fir_mfma12")
+    x = torch.empty(n, dtype=torch.complex64, device="cuda")
+    nsh.synth(x, n, 0)
+    hout = torch.empty(126, dtype=torch.complex64, device="cuda")
+    y = torch.empty_like(x)
+    plan(x, 0, hout, y, n)  # null history: zeros before the stream
+    torch.cuda.synchronize()
+    nch = n // 2048
+    per_x = (nch + 7) // 8
+    rng = np.random.default_rng(28)
+    starts = [0, n - 6000] + [per_x * 2048 * k - 3000 for k in range(1, 8)] + \
+             [int(c) * 2048 - 100 for c in rng.integers(1, nch, 6)]
+    for a in starts:
+        m = 6000
+        xs = x[a - 126 if a >= 126 else 0:a + m].cpu().numpy()
+        hist = xs[:126] if a >= 126 else None
+        ref = orc.fir_ccf(xs[126:] if a >= 126 else xs, h, hist=hist)
+        ok, err, scale = orc.tol_ok(y[a:a + m].cpu().numpy(), ref)
+        assert ok, (a, err, scale)
+    y_again = torch.empty_like(x)
+    plan(x, 0, hout, y_again, n)
+    torch.cuda.synchronize()
+    assert torch.equal(y, y_again)
+    del y_again
+    x2 = torch.empty_like(x)
+    nsh.synth(x2, n, 1 << 30)
+    y2 = torch.empty_like(x)
+    plan(x2, 0, hout, y2, n)
+    x3 = 0.5 * x + x2
+    del x
+    y3 = torch.empty_like(x3)
+    plan(x3, 0, hout, y3, n)
+    torch.cuda.synchronize()
+    lin = (0.5 * y + y2 - y3).abs().max().item()
+    scale = y3.abs().max().item()
+    assert lin <= 2e-6 * scale, (lin, scale)

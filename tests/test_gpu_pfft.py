@@ -231,12 +231,14 @@ def test_c5_zero_and_empty(torch_cuda):
     assert y.size == 0
 
 
-def test_c5_windowed_large(torch_cuda):
-    """2^26 inputs (2^22 outputs, every workgroup busy with ~40 frames): windows at the start,
-    the middle (workgroup boundaries) and the tail against the oracle with their histories."""
+@pytest.mark.parametrize("log2n", [26, 28])
+def test_c5_windowed_large(torch_cuda, log2n):
+    """2^26 inputs (2^22 outputs, every workgroup busy with ~40 frames) and BASELINE C5's full
+    2^28 (as bench.py's c5_fused leg): windows at the start, the middle (workgroup boundaries)
+    and the tail against the oracle with their histories."""
     torch = torch_cuda
     p = nsh.FirCascadePlan(C5)
-    n_out = 1 << 22
+    n_out = 1 << (log2n - 4)
     dx = torch.empty(16 * n_out, dtype=torch.complex64, device="cuda")
     nsh.synth(dx, 16 * n_out, 0)
     dy = torch.empty(n_out, dtype=torch.complex64, device="cuda")
@@ -244,7 +246,9 @@ def test_c5_windowed_large(torch_cuda):
     p(dx, None, dho, dy, n_out)
     torch.cuda.synchronize()
     y = dy.cpu().numpy()
-    for start in (0, 393 * 164 - 7, n_out // 2 + 12345, n_out - 3000):
+    nf = (n_out + 392) // 393
+    fpw = (nf + 255) // 256  # frames per workgroup (one workgroup per CU at D = 16)
+    for start in (0, 393 * 164 - 7, 393 * fpw - 1500, 393 * fpw * 129 - 10, n_out // 2 + 12345, n_out - 3000):
         m = 3000 if start + 3000 <= n_out else n_out - start
         lo = max(0, start - 128)  # 128 outputs of lead-in cover the 1890-sample support
         xs = orc.synth(16 * (start + m - lo), 16 * lo)
