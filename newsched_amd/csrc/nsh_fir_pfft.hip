@@ -295,7 +295,7 @@ struct pfft_args {
 // probe builds: s_memtime at phase k of frame f (< 64) by wave w of workgroup 0
 #define PFFT_T(k)                                                                                      \
     do {                                                                                               \
-        if (NSH_PFFT_TRACE && blockIdx.x == 0 && f - f0 < 64 && j == 0)                                 \
+        if (NSH_PFFT_TRACE == 1 && blockIdx.x == 0 && f - f0 < 64 && j == 0)                            \
             a.trace[((f - f0) * 16 + w) * 8 + (k)] = __builtin_amdgcn_s_memtime();                     \
     } while (0)
 
@@ -389,6 +389,7 @@ __global__ __launch_bounds__(64 * P / PW, 1) void k_fir_pfft(pfft_args a)
     const int64_t n_in = a.n_out * P;
     const int L = a.L, Q = a.Q, V = a.V;
     const img_bases ib = bases_of(imgs + w * PW * IMG); // the wave's PW images; products in the first
+    if (NSH_PFFT_TRACE == 2 && tid == 0) a.trace[2 * blockIdx.x] = __builtin_amdgcn_s_memtime(); // probe: workgroup span
 
     if (a.hist_out && blockIdx.x == gridDim.x - 1) // the next call's history: the L-1 samples before x[n_in]
         for (int k = tid; k < L - 1; k += NT) a.hist_out[k] = virt(a.x, a.hist_in, n_in - (L - 1) + k, n_in, L);
@@ -539,6 +540,9 @@ __global__ __launch_bounds__(64 * P / PW, 1) void k_fir_pfft(pfft_args a)
             PFFT_T(5);
         }
     }
+    if (NSH_PFFT_TRACE == 2 && j == 0) // probe: the last wave to leave sets the workgroup's end
+        __hip_atomic_fetch_max(&a.trace[2 * blockIdx.x + 1], (unsigned long long)__builtin_amdgcn_s_memtime(),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 hipError_t set_lds_attr(const void* fn, int bytes, int dev)
