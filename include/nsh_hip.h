@@ -108,7 +108,9 @@ int nsh_synth_cf32(float* out, int64_t n, uint64_t first_index, uint64_t seed, v
  *   hist_in  : ntaps-1 samples that precede in[0] (device; zeros at stream start; NULL = zeros,
  *              which saves the stream-start memset)
  *   hist_out : receives the ntaps-1 samples that precede the NEXT call's in[0]
- *              (must not alias hist_in -- ping-pong two buffers)
+ *              (must not alias hist_in -- ping-pong two buffers; NULL is an error, returned
+ *              before any launch, except for NSH_FIR_PFFT plans, which then skip it)
+ * NULL in / out or a NULL plan return an error before any launch.
  * algo: NSH_FIR_AUTO picks by measurement (MFMA for decim 1, 2, 4 with finite
  * taps, PFFT for decim 8 and 16, else DIRECT); NSH_FIR_DIRECT is the fp32 VALU direct form
  * (decim 1, 2, 4, 8); NSH_FIR_MFMA is the split-precision Toeplitz form on the matrix

@@ -259,7 +259,7 @@ int nsh_fir_plan_destroy(void* plan)
     return 0;
 }
 
-int nsh_fir_plan_algo(void* plan) { return static_cast<nsh_fir_plan*>(plan)->algo; }
+int nsh_fir_plan_algo(void* plan) { return plan ? static_cast<nsh_fir_plan*>(plan)->algo : 0; }
 const char* nsh_fir_plan_kernel(void* plan) { return plan ? static_cast<nsh_fir_plan*>(plan)->kernel.c_str() : ""; }
 
 int nsh_fir_ccf(void* plan, const float* in, const float* hist_in, float* hist_out, float* out, int64_t n_out, void* stream)
@@ -267,9 +267,12 @@ int nsh_fir_ccf(void* plan, const float* in, const float* hist_in, float* hist_o
     auto* p = static_cast<nsh_fir_plan*>(plan);
     if (!p) return nsh::fail_msg("nsh_fir_ccf: null plan");
     if (n_out <= 0) return 0;
+    if (!in || !out) return nsh::fail_msg("nsh_fir_ccf: null input or output");
     if (hist_in == hist_out && p->L > 1) return nsh::fail_msg("nsh_fir_ccf: hist_out must not alias hist_in");
     hipStream_t s = nsh::S(stream);
     if (p->algo == NSH_FIR_PFFT) return nsh_fir_cascade_ccf(p->casc, in, hist_in, hist_out, out, n_out, stream);
+    // every kernel but the polyphase-FFT one writes the next call's history unconditionally
+    if (!hist_out && p->L > 1) return nsh::fail_msg("nsh_fir_ccf: hist_out is required (ntaps-1 samples)");
     if (p->algo == NSH_FIR_MFMA || p->algo == NSH_FIR_MFMA_BF16X3)
         return nsh_fir_mfma_run(p, (const float2*)in, (const float2*)hist_in, (float2*)hist_out, (float2*)out, n_out, s);
     if (p->algo == NSH_FIR_MFMA_F32)

@@ -702,7 +702,8 @@ int nsh_fir_cascade_ccf(void* plan, const float* in, const float* hist_in, float
     if (!p) return nsh::fail_msg("nsh_fir_cascade_ccf: null plan");
     if (n_out <= 0) return 0;
     if (n_out > ((int64_t)1 << 40)) return nsh::fail_msg("nsh_fir_cascade_ccf: n_out too large");
-    if (hist_in == hist_out && p->L > 1) return nsh::fail_msg("nsh_fir_cascade_ccf: hist_out must not alias hist_in");
+    if (!in || !out) return nsh::fail_msg("nsh_fir_cascade_ccf: null input or output");
+    if (hist_in == hist_out && hist_out && p->L > 1) return nsh::fail_msg("nsh_fir_cascade_ccf: hist_out must not alias hist_in");
     pfft_args a;
     a.x = (const float2*)in;
     a.hist_in = (const float2*)hist_in;

@@ -51,3 +51,18 @@ def test_hip_shim_is_gfx950_code_object(tmp_path):
     if out.returncode != 0:
         pytest.skip("llvm-objdump --offloading unavailable")
     assert "gfx950" in out.stdout + out.stderr
+
+
+def test_hip_shim_rejects_null_arguments_before_launch():
+    """Argument errors come back as codes with a message, before any HIP call (so they are
+    checkable here, without a GPU): a NULL plan to the FIR entry points."""
+    from newsched_amd import nsh
+
+    L = nsh.lib()
+    one = ctypes.c_void_p(1)
+    assert L.nsh_fir_ccf(None, one, None, one, one, 16, None) != 0
+    assert b"null plan" in L.nsh_last_error()
+    assert L.nsh_fir_cascade_ccf(None, one, None, one, one, 16, None) != 0
+    assert b"null plan" in L.nsh_last_error()
+    assert L.nsh_fir_plan_algo(None) == 0
+    assert L.nsh_fir_ccf(None, one, None, one, one, 0, None) != 0  # plan checked first
