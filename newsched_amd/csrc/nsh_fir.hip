@@ -295,6 +295,7 @@ int nsh_fir_cascade2_ccf(void* plan1, void* plan2, const float* in, const float*
     if (!nsh_fir_cascade2_ok(p1, p2))
         return nsh::fail_msg("nsh_fir_cascade2_ccf: plans must be decim-2 fp16x2 MFMA plans (3 <= ceil((ntaps/2+1)/16)+1 <= 6) on one device");
     if (n_out <= 0) return 0;
+    if (!in || !out || !hist1_out || !hist2_out) return nsh::fail_msg("nsh_fir_cascade2_ccf: null pointer");
     if (n_out > ((int64_t)1 << 40)) return nsh::fail_msg("nsh_fir_cascade2_ccf: n_out too large");
     if (hist1_in == hist1_out || hist2_in == hist2_out)
         return nsh::fail_msg("nsh_fir_cascade2_ccf: hist_out must not alias hist_in");

@@ -66,3 +66,17 @@ def test_hip_shim_rejects_null_arguments_before_launch():
     assert b"null plan" in L.nsh_last_error()
     assert L.nsh_fir_plan_algo(None) == 0
     assert L.nsh_fir_ccf(None, one, None, one, one, 0, None) != 0  # plan checked first
+
+
+def test_stream_and_fft_entry_points_reject_null():
+    from newsched_amd import nsh
+
+    L = nsh.lib()
+    one = ctypes.c_void_p(16)
+    assert L.nsh_copy(None, one, 64, None) != 0 and b"null" in L.nsh_last_error()
+    assert L.nsh_mul_const_cc(one, None, 8, 1.0, 0.0, None) != 0
+    assert L.nsh_add_cc(one, None, one, 8, None) != 0
+    assert L.nsh_fft1024_c2c(None, one, 1, 0, None) != 0
+    assert L.nsh_channelizer1024(one, ctypes.c_void_p(32), None, 1, None) != 0
+    assert L.nsh_synth_cf32(None, 8, 0, 1, None) != 0
+    assert L.nsh_copy(None, None, 0, None) == 0  # nothing to move: no error
