@@ -41,11 +41,17 @@ inline unsigned stream_grid(int64_t n_vec, int block)
 // address spaces, which on gfx950 waits for every outstanding global load and store
 // (s_waitcnt vmcnt(0)) -- in a streaming kernel that drains the register prefetch of the
 // next chunks at every step. Kernels whose waves share data only through LDS use this.
+// The empty asm statements with a memory clobber keep the compiler from moving LDS accesses
+// across the barrier: the fences alone did not stop it sinking loads issued before the barrier
+// into the branches after it (seen in an experimental two-wave kernel, where the partner wave
+// then overwrote the data first).
 __device__ __forceinline__ void lds_barrier()
 {
+    asm volatile("" ::: "memory");
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    asm volatile("" ::: "memory");
 }
 
 // Raw buffer resource over chunk ch of a stream of n items (8 B each), chunk = CH items:
