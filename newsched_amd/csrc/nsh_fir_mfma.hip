@@ -1200,23 +1200,44 @@ __device__ __forceinline__ void mfma_tile9(const unsigned char* lds, const f16x8
 }
 
 // The exact path on a raw fp32 chunk in LDS (local sample j at float2 index j, halo first):
-// the lane's 8 outputs by the fp32 direct form (taps in order, fmaf).
+// the lane's 8 outputs by the fp32 direct form (taps in order, fused multiply-add per component).
+// The 8 outputs are two groups of four, 32 samples apart (blocks (reg & 3) + 8 (reg >> 2) + 4 h):
+// an input sample j0 + q feeds output b of its group through tap k = 32 b - q, so each sample is
+// read from LDS once per group (L + 96 reads instead of 4 L). q = 32 c - r runs downward, so every
+// output still takes its taps in the order k = 0, 1, ..., L - 1 (bit-identical to one output at a
+// time). (c, r, b) are unrolled, so every tap index k = 32 (b - c) + r is a compile-time constant:
+// the tap loads are unconditional scalar loads the compiler batches ahead of use, and only taps of
+// the last 32-block (k > 32 (Q - 2); Q = (L + 30) / 32 + 1 makes every earlier k < L) test k < L.
+// re and im go through one v_pk_fma_f32.
 template <int Q>
 __device__ __forceinline__ void direct_tile9(const unsigned char* lds, const float* __restrict__ taps, int L, int wave, int h,
                                              int phase, nf2 (&o)[8])
 {
     using G = geom8<Q>;
-    const float2* raw = reinterpret_cast<const float2*>(lds);
-    for (int reg = 0; reg < 8; ++reg) {
-        const int blk = (reg & 3) + 8 * (reg >> 2) + 4 * h;
-        const int j = G::H + wave * TILE + 32 * blk + phase;
-        float re = 0.f, im = 0.f;
-        for (int k = 0; k < L; ++k) {
-            const float2 x = raw[j - k];
-            re = fmaf(taps[k], x.x, re);
-            im = fmaf(taps[k], x.y, im);
+    const nf2* raw = reinterpret_cast<const nf2*>(lds);
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+        const int j0 = G::H + wave * TILE + 32 * (8 * g + 4 * h) + phase;
+        nf2 acc[4] = { nf2{ 0.f, 0.f }, nf2{ 0.f, 0.f }, nf2{ 0.f, 0.f }, nf2{ 0.f, 0.f } };
+#pragma unroll
+        for (int c = 3; c >= -(Q - 1); --c) {
+#pragma unroll
+            for (int r = 0; r < 32; ++r) {
+                const int q = 32 * c - r;
+                if (q < -G::H) break;  // L - 1 <= H: no tap reaches further back
+                const nf2 x = raw[j0 + q];
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    const int k = 32 * (b - c) + r;
+                    if (k < 0 || k > G::H) continue;
+                    const float t = taps[k < L ? k : L - 1];
+                    if (k > 32 * (Q - 2) && k >= L) continue;
+                    acc[b] = __builtin_elementwise_fma(nf2{ t, t }, x, acc[b]);
+                }
+            }
         }
-        o[reg] = nf2{ re, im };
+#pragma unroll
+        for (int b = 0; b < 4; ++b) o[4 * g + b] = acc[b];
     }
 }
 
@@ -1487,7 +1508,7 @@ __device__ __forceinline__ void store_pair12(const float4& v, unsigned char* buf
 }
 
 template <int Q>
-__global__ __launch_bounds__(256) void k_fir_mfma12(const float2* __restrict__ in,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_fir_mfma12(const float2* __restrict__ in,
                                                     const float2* __restrict__ hist_in,
                                                     float2* __restrict__ hist_out,
                                                     float2* __restrict__ out,
