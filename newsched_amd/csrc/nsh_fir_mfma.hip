@@ -1209,6 +1209,28 @@ __device__ __forceinline__ void mfma_tile9(const unsigned char* lds, const f16x8
 // the tap loads are unconditional scalar loads the compiler batches ahead of use, and only taps of
 // the last 32-block (k > 32 (Q - 2); Q = (L + 30) / 32 + 1 makes every earlier k < L) test k < L.
 // re and im go through one v_pk_fma_f32.
+// The same input reuse for NG outputs SP raw samples apart (output b at raw[j0 + SP b]): taps of
+// index k > HMAX are zero (L - 1 <= HMAX), and every k <= KSAFE is below L.
+template <int NG, int SP, int HMAX, int KSAFE>
+__device__ __forceinline__ void direct_group(const nf2* raw, int j0, const float* __restrict__ taps, int L, nf2 (&acc)[NG])
+{
+#pragma unroll
+    for (int b = 0; b < NG; ++b) acc[b] = nf2{ 0.f, 0.f };
+#pragma unroll
+    for (int i = 0; i <= SP * (NG - 1) + HMAX; ++i) {
+        const int q = SP * (NG - 1) - i;
+        const nf2 x = raw[j0 + q];
+#pragma unroll
+        for (int b = 0; b < NG; ++b) {
+            const int k = SP * b - q;
+            if (k < 0 || k > HMAX) continue;
+            const float t = taps[k < L ? k : L - 1];
+            if (k > KSAFE && k >= L) continue;
+            acc[b] = __builtin_elementwise_fma(nf2{ t, t }, x, acc[b]);
+        }
+    }
+}
+
 template <int Q>
 __device__ __forceinline__ void direct_tile9(const unsigned char* lds, const float* __restrict__ taps, int L, int wave, int h,
                                              int phase, nf2 (&o)[8])
@@ -1927,18 +1949,17 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma11(const float2* __restrict_
         unscale_tile(sum, unscale, o);
     };
     // exact path: y[m] = sum_k h[k] x[D m - k] from the raw chunk (float2 index D H + D m - k)
+    // exact path: outputs 2t and 2t + 1 are 16 D input samples apart, so they share their inputs
+    // (direct_group). decim_qh gives L - 1 <= D H and every k <= D (H - 16) below L.
     auto direct_tile = [&](const unsigned char* cur, nf2 (&o)[2 * G::TILES]) {
-        const float2* raw = reinterpret_cast<const float2*>(cur);
-        for (int oi = 0; oi < 2 * G::TILES; ++oi) {
-            const int blk = (oi >> 1) * 8 + 2 * g + (oi & 1);
-            const int j = D * G::H + D * (wave * G::WAVE_OUT + blk * 16 + phase);
-            float re = 0.f, im = 0.f;
-            for (int k = 0; k < L; ++k) {
-                const float2 x = raw[j - k];
-                re = fmaf(taps[k], x.x, re);
-                im = fmaf(taps[k], x.y, im);
-            }
-            o[oi] = nf2{ re, im };
+        const nf2* raw = reinterpret_cast<const nf2*>(cur);
+#pragma unroll
+        for (int t = 0; t < G::TILES; ++t) {
+            nf2 acc[2];
+            direct_group<2, 16 * D, D * G::H, D * (G::H - 16)>(raw, D * G::H + D * (wave * G::WAVE_OUT + (8 * t + 2 * g) * 16 + phase),
+                                                              taps, L, acc);
+            o[2 * t] = acc[0];
+            o[2 * t + 1] = acc[1];
         }
     };
     auto store_tile = [&](int64_t ch, const nf2 (&o)[2 * G::TILES]) {

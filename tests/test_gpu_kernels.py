@@ -449,10 +449,11 @@ def test_fir_mfma_wide_dynamic_range(torch_cuda, v8_form):
         assert ok, (a, b, err, scale)
 
 
+@pytest.mark.parametrize("decim", [1, 2, 4])
 @pytest.mark.parametrize("ntaps", [127, 64, 9])
-def test_fir_mfma_exact_path_bit_identical(torch_cuda, v8_form, ntaps):
+def test_fir_mfma_exact_path_bit_identical(torch_cuda, v8_form, ntaps, decim):
     """A 2^40 spike in every 2048-sample chunk sends every chunk through the in-kernel fp32
-    direct form (direct_tile9: taps in order k = 0..L-1, one fused multiply-add each). That is
+    direct form (direct_tile9 / direct_group, decim 1, 2, 4: taps in order k = 0..L-1, one fused multiply-add each). That is
     the order k_fir_direct accumulates in, so the two kernels agree bit for bit on finite
     inputs -- a check on the exact path's input reuse (each sample read once per four outputs)
     that no tolerance could hide. Also within tolerance of the oracle."""
@@ -461,15 +462,20 @@ def test_fir_mfma_exact_path_bit_identical(torch_cuda, v8_form, ntaps):
     n = 9 * 2048 + 333
     x = orc.synth(n, 5)
     x[100::2048] *= np.float32(2.0 ** 40)
-    y, hy = run_fir(torch, nsh.FirPlan(h, 1, nsh.FIR_MFMA), x, n)
+    if decim > 1 and v8_form == "v9":
+        pytest.skip("decimators: one kernel form (k_fir_mfma11)")
+    plan = nsh.FirPlan(h, decim, nsh.FIR_MFMA)
     if ntaps == 127:
-        assert nsh.FirPlan(h, 1, nsh.FIR_MFMA).kernel.startswith("k_fir_mfma12" if v8_form == "v12" else "k_fir_mfma9")
-    yd, hd = run_fir(torch, nsh.FirPlan(h, 1, nsh.FIR_DIRECT), x, n)
+        assert plan.kernel.startswith({1: "k_fir_mfma12" if v8_form == "v12" else "k_fir_mfma9",
+                                       2: "k_fir_mfma11", 4: "k_fir_mfma11"}[decim]), plan.kernel
+    y, hy = run_fir(torch, plan, x, n // decim)
+    yd, hd = run_fir(torch, nsh.FirPlan(h, decim, nsh.FIR_DIRECT), x, n // decim)
     np.testing.assert_array_equal(y.view(np.uint32), yd.view(np.uint32))
     np.testing.assert_array_equal(hy.view(np.uint32), hd.view(np.uint32))
-    ref = orc.fir_ccf(x, h)
-    for a in range(0, n, 2048):   # each chunk on its own scale
-        ok, err, scale = orc.tol_ok(y[a:a + 2048], ref[a:a + 2048])
+    ref = orc.fir_ccf(x[: n // decim * decim], h, decim)
+    c = 2048 // decim
+    for a in range(0, n // decim, c):   # each chunk on its own scale
+        ok, err, scale = orc.tol_ok(y[a:a + c], ref[a:a + c])
         assert ok, (a, err, scale)
 
 

@@ -3,7 +3,7 @@ non-finite sample, or one whose range exceeds the split's (a 2^40 spike among ~1
 filtered by the fp32 direct form inside the same launch. Times 2^28-sample launches with every
 k-th chunk poisoned (k = inf, 256, 64, 16, 4, 1), HIP events, >= 1 s warm-up per case, and
 checks a window around a poisoned chunk against the oracle.
-Usage: python tools/probe/cliff.py [--log2n 28]"""
+Usage: python tools/probe/cliff.py [--log2n 28] [--decim 1|2|4]"""
 import argparse
 import json
 import math
@@ -22,14 +22,16 @@ from oracle import oracle as orc
 ap = argparse.ArgumentParser()
 ap.add_argument("--log2n", type=int, default=28)
 ap.add_argument("--reps", type=int, default=10)
+ap.add_argument("--decim", type=int, default=1)
 a = ap.parse_args()
 n = 1 << a.log2n
 h = ss.firwin(127, 0.2).astype(np.float32)
-plan = nsh.FirPlan(h, 1)
+D = a.decim
+plan = nsh.FirPlan(h, D)
 x = torch.empty(n, dtype=torch.complex64, device="cuda")
-y = torch.empty_like(x)
+y = torch.empty(n // D, dtype=torch.complex64, device="cuda")
 s = torch.cuda.Stream()
-res = {"kernel": plan.kernel, "log2n": a.log2n, "cases": []}
+res = {"kernel": plan.kernel, "decim": D, "log2n": a.log2n, "cases": []}
 for kind in ("nan", "spike"):
     for k in (0, 256, 64, 16, 4, 1):
         nsh.synth(x, n, 0)
@@ -41,25 +43,25 @@ for kind in ("nan", "spike"):
         hin = torch.zeros(126, dtype=torch.complex64, device="cuda")
         hout = torch.zeros_like(hin)
         while time.time() - t0 < 1.0:
-            plan(x, hin, hout, y, n, stream=s)
+            plan(x, hin, hout, y, n // D, stream=s)
             s.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         with torch.cuda.stream(s):
             e0.record(s)
             for _ in range(a.reps):
-                plan(x, hin, hout, y, n, stream=s)
+                plan(x, hin, hout, y, n // D, stream=s)
             e1.record(s)
         e1.synchronize()
         us = e0.elapsed_time(e1) / a.reps * 1e3
         # parity on chunks 0..2 (chunk 0 poisoned when k > 0) against the oracle
         xs = x[: 3 * 2048].cpu().numpy()
-        yr = orc.fir_ccf(xs, h)
-        yy = y[: 3 * 2048].cpu().numpy()
+        yr = orc.fir_ccf(xs, h, D)
+        yy = y[: 3 * 2048 // D].cpu().numpy()
         fin = np.isfinite(yr.real) & np.isfinite(yr.imag)
         same_nf = bool(np.array_equal(fin, np.isfinite(yy.real) & np.isfinite(yy.imag)))
         ok, err, _ = orc.tol_ok(yy[fin], yr[fin])
         res["cases"].append({"kind": kind if k else "none", "every_kth_chunk": k, "exact_fraction": (1.0 / k) if k else 0.0,
-                             "us": round(us, 1), "GSps": round(n / us / 1e3, 1),
+                             "us": round(us, 1), "GSps_in": round(n / us / 1e3, 1),
                              "parity_ok": bool(ok and same_nf)})
         print(json.dumps(res["cases"][-1]), flush=True)
 print(json.dumps(res))
