@@ -1949,17 +1949,30 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma11(const float2* __restrict_
         unscale_tile(sum, unscale, o);
     };
     // exact path: y[m] = sum_k h[k] x[D m - k] from the raw chunk (float2 index D H + D m - k)
-    // exact path: outputs 2t and 2t + 1 are 16 D input samples apart, so they share their inputs
-    // (direct_group). decim_qh gives L - 1 <= D H and every k <= D (H - 16) below L.
+    // exact path. D = 4: outputs 0 and 1 are 64 input samples apart and share their inputs
+    // (direct_group; decim_qh gives L - 1 <= D H and every k <= D (H - 16) below L): dense-exact
+    // floor 74.7 -> 97.6 GS/s input. D = 2 keeps one output at a time: its two unrolled groups
+    // cost the main path a third of its speed (594 -> 890 us per 2^28, profiles/r02o_*).
     auto direct_tile = [&](const unsigned char* cur, nf2 (&o)[2 * G::TILES]) {
-        const nf2* raw = reinterpret_cast<const nf2*>(cur);
-#pragma unroll
-        for (int t = 0; t < G::TILES; ++t) {
+        if constexpr (D == 4) {
             nf2 acc[2];
-            direct_group<2, 16 * D, D * G::H, D * (G::H - 16)>(raw, D * G::H + D * (wave * G::WAVE_OUT + (8 * t + 2 * g) * 16 + phase),
-                                                              taps, L, acc);
-            o[2 * t] = acc[0];
-            o[2 * t + 1] = acc[1];
+            direct_group<2, 16 * D, D * G::H, D * (G::H - 16)>(reinterpret_cast<const nf2*>(cur),
+                                                              D * G::H + D * (wave * G::WAVE_OUT + 2 * g * 16 + phase), taps, L, acc);
+            o[0] = acc[0];
+            o[1] = acc[1];
+        } else {
+            const float2* raw = reinterpret_cast<const float2*>(cur);
+            for (int oi = 0; oi < 2 * G::TILES; ++oi) {
+                const int blk = (oi >> 1) * 8 + 2 * g + (oi & 1);
+                const int j = D * G::H + D * (wave * G::WAVE_OUT + blk * 16 + phase);
+                float re = 0.f, im = 0.f;
+                for (int k = 0; k < L; ++k) {
+                    const float2 x = raw[j - k];
+                    re = fmaf(taps[k], x.x, re);
+                    im = fmaf(taps[k], x.y, im);
+                }
+                o[oi] = nf2{ re, im };
+            }
         }
     };
     auto store_tile = [&](int64_t ch, const nf2 (&o)[2 * G::TILES]) {
