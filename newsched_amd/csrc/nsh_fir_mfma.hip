@@ -1725,6 +1725,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
 // in LDS and filtered by the fp32 direct form, buffer loads/stores, LDS-only barriers. The halo
 // (the last D*H input samples of the previous chunk) is kept raw in an LDS stash and re-split
 // at each chunk's scale.
+#ifndef NSH_DECIM2_SHARED // A/B switch: D = 2 on the shared-input exact path (one pair at a time)
+#define NSH_DECIM2_SHARED 0
+#endif
 template <int D, int QH>
 struct geom11 {
     static constexpr int NT = 256;
@@ -1954,12 +1957,20 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma11(const float2* __restrict_
     // floor 74.7 -> 97.6 GS/s input. D = 2 keeps one output at a time: its two unrolled groups
     // cost the main path a third of its speed (594 -> 890 us per 2^28, profiles/r02o_*).
     auto direct_tile = [&](const unsigned char* cur, nf2 (&o)[2 * G::TILES]) {
-        if constexpr (D == 4) {
-            nf2 acc[2];
-            direct_group<2, 16 * D, D * G::H, D * (G::H - 16)>(reinterpret_cast<const nf2*>(cur),
-                                                              D * G::H + D * (wave * G::WAVE_OUT + 2 * g * 16 + phase), taps, L, acc);
-            o[0] = acc[0];
-            o[1] = acc[1];
+        if constexpr (D == 4 || NSH_DECIM2_SHARED) {
+#pragma unroll 1
+            for (int t = 0; t < G::TILES; ++t) {
+                nf2 acc[2];
+                direct_group<2, 16 * D, D * G::H, D * (G::H - 16)>(
+                    reinterpret_cast<const nf2*>(cur), D * G::H + D * (wave * G::WAVE_OUT + (8 * t + 2 * g) * 16 + phase), taps, L, acc);
+                if (t == 0) {
+                    o[0] = acc[0];
+                    o[1] = acc[1];
+                } else {
+                    o[2 * G::TILES - 2] = acc[0];
+                    o[2 * G::TILES - 1] = acc[1];
+                }
+            }
         } else {
             const float2* raw = reinterpret_cast<const float2*>(cur);
             for (int oi = 0; oi < 2 * G::TILES; ++oi) {
