@@ -1461,6 +1461,17 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma9(const float2* __restrict__
 // (L1/L2 hits: every workgroup reads the same bytes).
 // Scale and exact-path test cover the chunk and its halo. Results match v9 to within the
 // split's rounding (v9's scale also covered the whole previous chunk), not bit for bit.
+// Chunk order inside an XCD: workgroup k of an XCD's sequence filters chunk k (address order), or,
+// with NSH_V12_ROT (default), chunk k with its low two bits rotated by an xor-fold of k >> 2 (a
+// bijection on every full group of 4, the order still ascending group by group). Without it, chunks
+// that need the exact path every 4th or 8th chunk were as slow as all-exact streams
+// (profiles/r02t_cliff_curve.log: k = 3 1381 us, k = 4 2775, k = 6 1260, k = 8 1602): consecutive
+// workgroups of an XCD are dealt out round-robin, so a power-of-two stride landed every slow chunk
+// on the same quarter of the XCD. Rotated: k = 4 1216 us, k = 8 957, k = 2 1703; main path
+// bit-identical, 718.0 vs 721.2 us (profiles/r02u_*).
+#ifndef NSH_V12_ROT
+#define NSH_V12_ROT 1
+#endif
 #ifndef NSH_V12_LDS_PAD
 #define NSH_V12_LDS_PAD 0 // probe builds: extra LDS per workgroup (fewer resident workgroups per CU)
 #endif
@@ -1552,7 +1563,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
     const int wave = tid >> 6;
     const int64_t n_in = n_out;
     const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
-    const int64_t c_first = (int64_t)(blockIdx.x & 7) * per_x + (blockIdx.x >> 3);
+    int64_t wi = blockIdx.x >> 3; // this workgroup's place in its XCD's sequence
+#if NSH_V12_ROT
+    if ((wi | 3) < per_x) { // full aligned group of 4: rotate it by an xor-fold of the group index
+        const uint64_t grp = (uint64_t)wi >> 2;
+        unsigned r = (unsigned)grp ^ (unsigned)(grp >> 32);
+        r ^= r >> 16;
+        r ^= r >> 8;
+        r ^= r >> 4;
+        r ^= r >> 2;
+        wi = (wi & ~(int64_t)3) | ((wi - (int64_t)r) & 3);
+    }
+#endif
+    const int64_t c_first = (int64_t)(blockIdx.x & 7) * per_x + wi;
     if (c_first >= nchunks) return; // whole workgroup: before any barrier
 
     // chunk ch -> registers (nontemporal) and its halo (default policy: the previous chunk's

@@ -23,6 +23,8 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--log2n", type=int, default=28)
 ap.add_argument("--reps", type=int, default=10)
 ap.add_argument("--decim", type=int, default=1)
+ap.add_argument("--ks", default="0,256,64,16,4,1", help="every k-th chunk poisoned (0: none)")
+ap.add_argument("--kinds", default="nan,spike")
 a = ap.parse_args()
 n = 1 << a.log2n
 h = ss.firwin(127, 0.2).astype(np.float32)
@@ -32,8 +34,8 @@ x = torch.empty(n, dtype=torch.complex64, device="cuda")
 y = torch.empty(n // D, dtype=torch.complex64, device="cuda")
 s = torch.cuda.Stream()
 res = {"kernel": plan.kernel, "decim": D, "log2n": a.log2n, "cases": []}
-for kind in ("nan", "spike"):
-    for k in (0, 256, 64, 16, 4, 1):
+for kind in a.kinds.split(","):
+    for k in [int(v) for v in a.ks.split(",")]:
         nsh.synth(x, n, 0)
         if k:
             v = float("nan") if kind == "nan" else 2.0 ** 40
