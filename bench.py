@@ -307,7 +307,7 @@ def run_c5_fused_leg(a, first, device, barrier, dist, tdev, torch, orc, nsh):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None, help="ranks (default: WORLD_SIZE under a launcher, else 1)")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--min-warmup-s", type=float, default=1.0,
@@ -327,16 +327,18 @@ def main():
     ap.add_argument("--c5-steps", type=int, default=5)
     ap.add_argument("--c5-warmup", type=int, default=2)
     ap.add_argument("--c5-buf-mib", type=int, default=64)
-    ap.add_argument("--c5-transport", default="default", choices=["default", "auto", "rccl", "socket"])
+    ap.add_argument("--c5-transport", default="default", choices=["default", "auto", "rccl", "p2p", "socket"])
     ap.add_argument("--c5-timeout", type=float, default=120.0, help="deadline for the C5 leg (s)")
     ap.add_argument("--rank-check", action="store_true", help=argparse.SUPPRESS)  # launcher test (CPU, gloo)
     a = ap.parse_args()
 
-    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+    if "WORLD_SIZE" not in os.environ and (a.gpus or 1) > 1:
         sys.exit(spawn_ranks(a.gpus))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.gpus is None:  # under torchrun without --gpus: one rank per launched process
+        a.gpus = world
     if world != a.gpus:
         sys.exit("bench.py: --gpus %d but WORLD_SIZE=%d" % (a.gpus, world))
 
@@ -495,10 +497,18 @@ def main():
         ncpu = 1 << a.cpu_log2n
         xs = orc.synth(1 << 20)  # vector_source data (repeated)
         secs = nsr.cpu_fir_run(taps, xs, ncpu, fixed_buf_size=32768)
+        try:
+            affinity = len(os.sched_getaffinity(0))
+        except (AttributeError, OSError):
+            affinity = None
         out["cpu_baseline"] = {
             "value": round(ncpu / secs / 1e6, 2),
             "unit": "MSamples/s",
-            "cores": 4,
+            "cores": 4,  # threads the run used: scheduler_mt's thread per block, 4 blocks
+            "threads": 4,
+            "fir_cores": 1,  # the FIR block's work() runs on its one thread
+            "nproc": os.cpu_count(),
+            "cpus_allowed": affinity,
             "kind": "port",
             "sample": "2^%d samples through vector_source->head->fir_filter_ccf(127 taps, AVX-512 fp32)->null_sink, "
                       "scheduler_mt thread-per-block (4 threads; the FIR on one core), vmcircbuf 32768 B default buffers; "

@@ -82,6 +82,20 @@ int nsh_memset_async(void* ptr, int value, size_t bytes, void* stream);
 int nsh_ring_alloc(int dev, size_t min_bytes, void** base, size_t* actual_bytes, int* double_mapped);
 int nsh_ring_free(void* base);
 
+/* Inter-process device memory: the "p2p" transport of gr::domain_adapter_remote (a flowgraph
+ * edge between two processes whose rings are device memory). The receiving process exports a
+ * nsh_malloc'd landing area (nsh_ipc_mem_export -> NSH_IPC_HANDLE_BYTES opaque bytes sent over
+ * the edge's control socket); the sending process maps it on its own device
+ * (nsh_ipc_mem_open) and writes it with a stream-ordered nsh_memcpy_async (same GPU: a local
+ * D2D copy; different GPUs: a peer write over xGMI). Replaces the reference's direct
+ * peer-buffer access between domains, which exists only inside one process
+ * (runtime/include/gnuradio/domain_adapter_direct.hpp:156-172); the reference has no
+ * cross-process edge. */
+#define NSH_IPC_HANDLE_BYTES 64
+int nsh_ipc_mem_export(void* dev_ptr, void* handle_out);
+int nsh_ipc_mem_open(int dev, const void* handle, void** ptr);
+int nsh_ipc_mem_close(void* ptr);
+
 /* ---- stream kernels (n counts complex samples unless the name ends in _ff) --------- */
 int nsh_copy(const void* in, void* out, size_t bytes, void* stream);
 int nsh_mul_const_cc(const float* in, float* out, int64_t n, float k_re, float k_im, void* stream);

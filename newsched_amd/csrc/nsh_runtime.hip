@@ -258,4 +258,32 @@ int nsh_ring_free(void* base)
     return 0;
 }
 
+// ---- inter-process device memory (p2p edge transport) ----------------------------------
+static_assert(sizeof(hipIpcMemHandle_t) == NSH_IPC_HANDLE_BYTES, "hipIpcMemHandle_t size");
+
+int nsh_ipc_mem_export(void* dev_ptr, void* handle_out)
+{
+    if (!dev_ptr || !handle_out) return fail(hipErrorInvalidValue, "nsh_ipc_mem_export: NULL argument");
+    hipIpcMemHandle_t h;
+    NSH_CK(hipIpcGetMemHandle(&h, dev_ptr));
+    std::memcpy(handle_out, &h, sizeof(h));
+    return 0;
+}
+
+int nsh_ipc_mem_open(int dev, const void* handle, void** ptr)
+{
+    if (!handle || !ptr) return fail(hipErrorInvalidValue, "nsh_ipc_mem_open: NULL argument");
+    NSH_CK(hipSetDevice(dev));
+    hipIpcMemHandle_t h;
+    std::memcpy(&h, handle, sizeof(h));
+    NSH_CK(hipIpcOpenMemHandle(ptr, h, hipIpcMemLazyEnablePeerAccess));
+    return 0;
+}
+
+int nsh_ipc_mem_close(void* ptr)
+{
+    NSH_CK(hipIpcCloseMemHandle(ptr));
+    return 0;
+}
+
 } // extern "C"

@@ -48,6 +48,9 @@ SIGNATURES = {
     "nsh_memset_async": (_i, [_vp, _i, _sz, _vp]),
     "nsh_ring_alloc": (_i, [_i, _sz, C.POINTER(_vp), C.POINTER(_sz), C.POINTER(_i)]),
     "nsh_ring_free": (_i, [_vp]),
+    "nsh_ipc_mem_export": (_i, [_vp, _vp]),
+    "nsh_ipc_mem_open": (_i, [_i, _vp, C.POINTER(_vp)]),
+    "nsh_ipc_mem_close": (_i, [_vp]),
     "nsh_copy": (_i, [_vp, _vp, _sz, _vp]),
     "nsh_mul_const_cc": (_i, [_vp, _vp, _i64, _f, _f, _vp]),
     "nsh_mul_const_ff": (_i, [_vp, _vp, _i64, _f, _vp]),

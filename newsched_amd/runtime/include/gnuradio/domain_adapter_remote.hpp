@@ -12,17 +12,22 @@
 //
 //   process A:  blk_a -> [da_remote SEND] ~~~~ control: TCP (counts, done flags)
 //   process B:                        ~~~~~> [da_remote RECV] -> blk_b
-//                                     data:  RCCL ncclSend/ncclRecv on the partition
-//                                            streams (device buffers, different GPUs), or
-//                                            the TCP socket (host buffers; device buffers
-//                                            staged through pinned memory)
+//                                     data:  rccl   ncclSend/ncclRecv on the partition streams
+//                                                   (device rings on different GPUs)
+//                                            p2p    stream-ordered copy into IPC-mapped landing
+//                                                   slots on the receiver's GPU (device rings,
+//                                                   same GPU or two GPUs)
+//                                            socket the TCP socket (host rings; device rings
+//                                                   staged through pinned memory)
 //
 // Crossing i uses TCP port base_port + i on `host` (the receiving process listens).
 // Sender: every post_write of the upstream block is forwarded immediately (chunks of at
-// most the receiver's free ring space), stream-ordered after the producing kernel, and
-// the span is released at once (the next kernel that reuses it is stream-ordered after the
-// send). Receiver: a thread per adapter posts the matching receive into its ring, then
-// post_write + NOTIFY_INPUT wake the downstream block. Per-run DONE / READER_DONE
+// most the receiver's free ring space). The span is released by one rule for every
+// transport (remote::transport in the .cpp): at once when the transport's read of it is
+// stream-ordered after the producing kernel and before the next one (rccl, p2p) or already
+// done (socket); when the transport reports the read complete otherwise (the host-ring test
+// transport "deferred_test"). Receiver: a thread per adapter places each message into its
+// ring, then post_write + NOTIFY_INPUT wake the downstream block. Per-run DONE / READER_DONE
 // messages make drain-based termination and restarted flowgraphs work across processes.
 #pragma once
 #include <gnuradio/domain_adapter.hpp>
@@ -41,7 +46,10 @@ namespace gr {
 
 namespace remote {
 class channel;   // TCP control (and host data) socket
-class transport; // data path: "rccl" | "socket"
+class transport; // data path: "rccl" | "p2p" | "socket" | "deferred_test"
+// deferred_test transport: messages whose ring span changed between send() and the transport's
+// delayed read of it (the ring was overwritten before the transfer read it); process-wide
+uint64_t deferred_test_violations();
 } // namespace remote
 
 // Placeholder scheduler for a domain that another process runs. Never initialised or
@@ -68,7 +76,9 @@ enum class remote_role { SEND, RECV };
 struct remote_edge_options {
     std::string host = "127.0.0.1"; // address of the receiving process
     int base_port = 29650;          // crossing i listens on base_port + i
-    std::string transport = "auto"; // "auto" | "rccl" | "socket"
+    // "auto" (rccl across GPUs, p2p for two processes on one GPU, socket for host rings) |
+    // "rccl" | "p2p" | "socket" | "deferred_test" (host rings; CPU tests of the release rule)
+    std::string transport = "auto";
     int device = -1;                // GPU of this process (-1: the current thread's device)
     double timeout_s = 120.0;       // connect / accept / handshake limit
 };
@@ -110,7 +120,9 @@ public:
 private:
     domain_adapter_remote(remote_role role, int crossing, const remote_edge_options& opt);
     void pump();           // SEND: forward everything readable in the local ring
-    void poll_reverse();   // SEND: consume READER_DONE messages
+    void release_span(int m, bool deferred); // SEND: the edge's release rule (see pump)
+    bool read_reverse(int timeout_ms);       // SEND: one reverse message, if any
+    void poll_reverse();   // SEND: consume reverse messages (READER_DONE, transport credits)
     void recv_loop();      // RECV thread body
     void check_failed() const;
     void notify_downstream();
@@ -137,6 +149,10 @@ private:
     std::condition_variable _cv; // RECV: space freed by the downstream block
     std::exception_ptr _err;
     std::atomic<bool> _failed{ false };
+    std::mutex _pump_m;      // SEND: pump vs. deferred releases
+    std::mutex _rev_m;       // SEND: reverse-message reads
+    std::mutex _ring_m;      // RECV: ring writes vs. reset_flags' discard
+    uint64_t _inflight = 0;  // SEND: items handed to the transport, not yet released
     void* _stream = nullptr; // RECV thread's stream (device rings)
     void* _scratch = nullptr; // RECV: discard area after the reader finished
     size_t _scratch_bytes = 0;

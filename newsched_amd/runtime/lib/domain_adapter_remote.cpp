@@ -17,6 +17,8 @@
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
+#include <functional>
 #include <map>
 #include <stdexcept>
 
@@ -24,24 +26,50 @@ namespace gr {
 namespace remote {
 
 namespace {
-enum msg_type : uint32_t { M_HELLO = 0x4e534831u, M_DATA = 2, M_DONE = 3, M_READER_DONE = 4, M_CLOSE = 5 };
+enum msg_type : uint32_t {
+    M_HELLO = 0x4e534831u,
+    M_DATA = 2,
+    M_DONE = 3,
+    M_READER_DONE = 4,
+    M_CLOSE = 5,
+    M_SLOT_FREE = 6 // p2p: receiver -> sender, landing slot n may be written again
+};
 struct msg {
     uint32_t type;
     uint32_t aux;
     uint64_t n;
 };
+// transport codes in hello.want / hello.chosen
+enum tr_code : int32_t { T_AUTO = 0, T_RCCL = 1, T_SOCKET = 2, T_P2P = 3, T_DEFERRED_TEST = 4 };
 struct hello {
     uint32_t magic;     // M_HELLO
     int32_t crossing;
     uint64_t item_size;
     int32_t is_device;  // this side's ring end is device memory
     int32_t device;
-    int32_t want;       // 0 auto, 1 rccl, 2 socket (sender's request)
-    int32_t chosen;     // receiver's answer: 1 rccl, 2 socket
+    int32_t want;       // tr_code (sender's request)
+    int32_t chosen;     // receiver's answer (tr_code, never T_AUTO)
     int64_t max_chunk;  // receiver's answer: items per message
     char pci[32];       // PCI bus id of `device` ("" for host rings): ordinals differ per
                         // process under per-rank HIP_VISIBLE_DEVICES, bus ids do not
 };
+// p2p: the receiver's landing slots, sent after its hello; the sender answers with a u32
+// status (0 = mapped)
+struct p2p_offer {
+    uint8_t handle[NSH_IPC_HANDLE_BYTES];
+    uint32_t slots;
+    uint32_t pad;
+    uint64_t slot_bytes;
+};
+int32_t transport_code(const std::string& s)
+{
+    if (s == "auto") return T_AUTO;
+    if (s == "rccl") return T_RCCL;
+    if (s == "socket") return T_SOCKET;
+    if (s == "p2p") return T_P2P;
+    if (s == "deferred_test") return T_DEFERRED_TEST;
+    throw std::invalid_argument("remote edge: unknown transport '" + s + "'");
+}
 using clk = std::chrono::steady_clock;
 double since(clk::time_point t0) { return std::chrono::duration<double>(clk::now() - t0).count(); }
 
@@ -272,19 +300,126 @@ std::shared_ptr<channel> connect_retry(const std::string& host, int port, double
 } // namespace
 
 // ---- data transports -------------------------------------------------------------------
+//
+// Edge ordering (the one rule every transport follows, applied in domain_adapter_remote::pump):
+// a DATA message's payload is the sender's ring span [p, p + bytes). send() either
+//   * returns release::now: nothing reads the span after the next write into it. Either the
+//     payload was consumed before send() returned (socket), or its read was enqueued on the
+//     calling thread's stream (rccl, p2p): the upstream kernel that writes the span next is
+//     launched on the same partition stream, after the read; a writer on another stream waits
+//     for the event hip_buffer::post_read records there. The span is released at once, with no
+//     host wait -- the early release of the RCCL path;
+//   * or returns release::deferred: the payload is read later on another thread (the
+//     host-memory test transport below, where no stream orders the writer); `done` runs on that
+//     thread, in send order, once the read is complete, and only then is the span released.
+// The DATA header itself may go out later than send() returns (p2p: when the copy has landed);
+// send_control() keeps DONE / CLOSE behind every DATA message handed over before it.
 class transport
 {
 public:
+    enum class release { now, deferred };
     virtual ~transport() = default;
     virtual const char* kind() const = 0;
-    // bytes on the calling thread's stream (device) or directly (host)
-    virtual void send(channel& ch, const void* p, size_t bytes) = 0;
+    virtual release send(channel& ch, uint64_t n, uint32_t ntags, const std::string& blob, const void* p, size_t bytes,
+                         std::function<void()> done) = 0;
+    virtual void send_control(channel& ch, uint32_t type) { ch.send_msg(type); }
+    virtual void flush() {} // every message handed over so far is on the wire
+    // sender: a reverse message owned by the transport (M_SLOT_FREE); false if not its own
+    virtual bool on_reverse(const msg&) { return false; }
+    // receiver: the payload of one DATA message into p (device or host, as the ring)
     virtual void recv(channel& ch, void* p, size_t bytes) = 0;
 };
 
+namespace {
+// DATA header, then [u32 blob length][blob] when it has tags, then the payload
+template <typename F>
+void write_data(channel& ch, uint64_t n, uint32_t ntags, const std::string& blob, F&& payload)
+{
+    ch.send_msg_with(
+        M_DATA, n,
+        [&] {
+            if (ntags) {
+                const uint32_t len = (uint32_t)blob.size();
+                ch.send_bytes(&len, sizeof(len));
+                ch.send_bytes(blob.data(), blob.size());
+            }
+            payload();
+        },
+        ntags);
+}
+
+// FIFO of jobs run in order on one thread (deferred message sends); the first failure is kept
+// and rethrown to the producer.
+class outbox
+{
+public:
+    outbox() : _thr([this] { loop(); }) {}
+    ~outbox()
+    {
+        {
+            std::lock_guard<std::mutex> g(_m);
+            _stop = true;
+        }
+        _cv.notify_all();
+        _thr.join();
+    }
+    void push(std::function<void()> job)
+    {
+        rethrow();
+        {
+            std::lock_guard<std::mutex> g(_m);
+            _q.push_back(std::move(job));
+        }
+        _cv.notify_all();
+    }
+    void flush()
+    {
+        std::unique_lock<std::mutex> l(_m);
+        _idle_cv.wait(l, [this] { return (_q.empty() && !_busy) || _err; });
+        l.unlock();
+        rethrow();
+    }
+
+private:
+    void rethrow()
+    {
+        std::lock_guard<std::mutex> g(_m);
+        if (_err) std::rethrow_exception(_err);
+    }
+    void loop()
+    {
+        std::unique_lock<std::mutex> l(_m);
+        for (;;) {
+            _cv.wait(l, [this] { return _stop || !_q.empty(); });
+            if (_q.empty()) return; // stop requested and drained
+            auto job = std::move(_q.front());
+            _q.pop_front();
+            _busy = true;
+            l.unlock();
+            std::exception_ptr e;
+            try {
+                if (!_err) job();
+            } catch (...) {
+                e = std::current_exception();
+            }
+            l.lock();
+            _busy = false;
+            if (e && !_err) _err = e;
+            _idle_cv.notify_all();
+        }
+    }
+    std::mutex _m;
+    std::condition_variable _cv, _idle_cv;
+    std::deque<std::function<void()>> _q;
+    bool _busy = false, _stop = false;
+    std::exception_ptr _err;
+    std::thread _thr;
+};
+} // namespace
+
 // Bytes over the control socket. Device memory is staged through a pinned bounce buffer
-// (one synchronous D2H/H2D per message): the path for host rings and for two processes
-// sharing one GPU, where RCCL cannot be used.
+// (one synchronous D2H/H2D per message): the path for host rings, and the fallback for
+// device rings when neither RCCL nor the IPC mapping is available.
 class socket_transport : public transport
 {
 public:
@@ -294,17 +429,19 @@ public:
         if (_bounce) nsh_host_free(_bounce);
     }
     const char* kind() const override { return _device ? "socket(staged)" : "socket"; }
-    void send(channel& ch, const void* p, size_t bytes) override
+    release send(channel& ch, uint64_t n, uint32_t ntags, const std::string& blob, const void* p, size_t bytes,
+                 std::function<void()>) override
     {
         if (!_device) {
-            ch.send_bytes(p, bytes);
-            return;
+            write_data(ch, n, ntags, blob, [&] { ch.send_bytes(p, bytes); });
+            return release::now;
         }
         ensure(bytes);
         void* s = hip::current_stream();
         hip::check(nsh_memcpy_async(_bounce, p, bytes, NSH_D2H, s), "remote edge: stage D2H");
         hip::check(nsh_stream_sync(s), "remote edge: stage sync");
-        ch.send_bytes(_bounce, bytes);
+        write_data(ch, n, ntags, blob, [&] { ch.send_bytes(_bounce, bytes); });
+        return release::now;
     }
     void recv(channel& ch, void* p, size_t bytes) override
     {
@@ -331,6 +468,192 @@ private:
     bool _device;
     void* _bounce = nullptr;
     size_t _cap = 0;
+};
+
+// Test transport for host rings (transport "deferred_test"; CPU tests only): the payload is
+// read from the ring span on a worker thread after a delay, as an asynchronous engine would,
+// and the span is released only when that read is done (release::deferred). A checksum taken
+// when send() is called is compared with the bytes the delayed read sees; any difference means
+// the ring was overwritten before the transfer read it, and is counted
+// (deferred_test_violations()). NSH_REMOTE_TEST_EARLY_RELEASE=1 makes it claim release::now
+// instead: the negative control, which must produce violations.
+class deferred_test_transport : public transport
+{
+public:
+    deferred_test_transport()
+    {
+        const char* d = std::getenv("NSH_REMOTE_TEST_DELAY_US");
+        _delay_us = d ? std::atoi(d) : 2000;
+        const char* e = std::getenv("NSH_REMOTE_TEST_EARLY_RELEASE");
+        _early = e && *e == '1';
+    }
+    ~deferred_test_transport() override
+    {
+        try {
+            _box.flush();
+        } catch (...) {
+        }
+    }
+    const char* kind() const override { return _early ? "deferred_test(early)" : "deferred_test"; }
+    release send(channel& ch, uint64_t n, uint32_t ntags, const std::string& blob, const void* p, size_t bytes,
+                 std::function<void()> done) override
+    {
+        const uint64_t sum0 = fnv(p, bytes);
+        _box.push([this, &ch, n, ntags, blob, p, bytes, sum0, done = std::move(done)] {
+            std::this_thread::sleep_for(std::chrono::microseconds(_delay_us));
+            std::string copy(static_cast<const char*>(p), bytes); // the asynchronous read
+            if (fnv(copy.data(), bytes) != sum0) g_violations.fetch_add(1);
+            write_data(ch, n, ntags, blob, [&] { ch.send_bytes(copy.data(), bytes); });
+            if (!_early) done();
+        });
+        return _early ? release::now : release::deferred;
+    }
+    void send_control(channel& ch, uint32_t type) override
+    {
+        _box.push([&ch, type] { ch.send_msg(type); });
+    }
+    void flush() override { _box.flush(); }
+    void recv(channel& ch, void* p, size_t bytes) override
+    {
+        if (!ch.recv_bytes(p, bytes)) throw std::runtime_error("remote edge: peer closed");
+    }
+    static std::atomic<uint64_t> g_violations;
+
+private:
+    static uint64_t fnv(const void* p, size_t n)
+    {
+        uint64_t h = 1469598103934665603ull;
+        auto* c = static_cast<const uint8_t*>(p);
+        for (size_t i = 0; i < n; ++i) h = (h ^ c[i]) * 1099511628211ull;
+        return h;
+    }
+    int _delay_us;
+    bool _early;
+    outbox _box;
+};
+std::atomic<uint64_t> deferred_test_transport::g_violations{ 0 };
+uint64_t deferred_test_violations() { return deferred_test_transport::g_violations.load(); }
+
+// Device rings of two processes through an IPC-mapped landing area on the receiver's GPU:
+// K slots of one message each. Sender: a stream-ordered copy from its ring span into a free
+// slot (nsh_memcpy_async on the partition stream; same GPU: local D2D, two GPUs: a peer write
+// over xGMI), an event behind it, release::now (the copy is stream-ordered before the next
+// write into the span); the DATA header (with the slot number) goes out from the outbox
+// thread once that event has completed, so the receiver never reads a slot before it landed.
+// Receiver: one local D2D copy from the slot into its ring on its own stream, then
+// M_SLOT_FREE(slot) once that copy is done. A sender with no free slot reads reverse messages
+// until one comes back.
+class p2p_transport : public transport
+{
+public:
+    static constexpr uint32_t kSlots = 4;
+
+    // receiver side: allocate and export the slots (throws if IPC export is unavailable)
+    p2p_transport(int device, size_t slot_bytes, p2p_offer& offer) : _sender(false), _device(device), _slot_bytes(slot_bytes)
+    {
+        hip::check(nsh_malloc(device, slot_bytes * kSlots, &_local), "remote edge: p2p slots");
+        if (nsh_ipc_mem_export(_local, offer.handle) != 0) {
+            const std::string e = nsh_last_error();
+            nsh_free(_local);
+            _local = nullptr;
+            throw std::runtime_error("remote edge: p2p export: " + e);
+        }
+        offer.slots = kSlots;
+        offer.slot_bytes = slot_bytes;
+    }
+    // sender side: map the receiver's slots; read_reverse(block) reads and dispatches one
+    // reverse message (false when none arrived)
+    p2p_transport(int device, const p2p_offer& offer, std::function<bool()> read_reverse)
+        : _sender(true), _device(device), _slot_bytes(offer.slot_bytes), _read_reverse(std::move(read_reverse))
+    {
+        if (offer.slots == 0 || offer.slots > 64) throw std::runtime_error("remote edge: p2p offer");
+        hip::check(nsh_ipc_mem_open(device, offer.handle, &_remote), "remote edge: p2p map");
+        _events.resize(offer.slots, nullptr);
+        for (auto& e : _events) hip::check(nsh_event_create(&e), "remote edge: p2p event");
+        for (uint32_t s = 0; s < offer.slots; ++s) _free.push_back(s);
+        _box = std::make_unique<outbox>();
+    }
+    ~p2p_transport() override
+    {
+        if (_box) {
+            try {
+                _box->flush();
+            } catch (...) {
+            }
+            _box.reset();
+        }
+        for (void* e : _events)
+            if (e) nsh_event_destroy(e);
+        if (_remote) nsh_ipc_mem_close(_remote);
+        if (_local) nsh_free(_local);
+    }
+    const char* kind() const override { return "p2p"; }
+
+    release send(channel& ch, uint64_t n, uint32_t ntags, const std::string& blob, const void* p, size_t bytes,
+                 std::function<void()>) override
+    {
+        if (bytes > _slot_bytes) throw std::runtime_error("remote edge: p2p message larger than a slot");
+        uint32_t slot;
+        for (;;) {
+            {
+                std::lock_guard<std::mutex> g(_m);
+                if (!_free.empty()) {
+                    slot = _free.front();
+                    _free.pop_front();
+                    break;
+                }
+            }
+            _read_reverse(); // blocks briefly for a reverse message (M_SLOT_FREE)
+        }
+        void* s = hip::current_stream();
+        hip::check(nsh_memcpy_async(static_cast<char*>(_remote) + (size_t)slot * _slot_bytes, p, bytes, NSH_DEFAULT, s),
+                   "remote edge: p2p copy");
+        void* ev = _events[slot];
+        hip::check(nsh_event_record(ev, s), "remote edge: p2p event");
+        _box->push([&ch, n, ntags, blob, ev, slot] {
+            hip::check(nsh_event_sync(ev), "remote edge: p2p copy wait");
+            write_data(ch, n, ntags, blob, [&] { ch.send_bytes(&slot, sizeof(slot)); });
+        });
+        return release::now;
+    }
+    void send_control(channel& ch, uint32_t type) override
+    {
+        _box->push([&ch, type] { ch.send_msg(type); });
+    }
+    void flush() override
+    {
+        if (_box) _box->flush();
+    }
+    bool on_reverse(const msg& m) override
+    {
+        if (m.type != M_SLOT_FREE) return false;
+        std::lock_guard<std::mutex> g(_m);
+        _free.push_back((uint32_t)m.n);
+        return true;
+    }
+    void recv(channel& ch, void* p, size_t bytes) override
+    {
+        uint32_t slot = 0;
+        if (!ch.recv_bytes(&slot, sizeof(slot))) throw std::runtime_error("remote edge: peer closed");
+        if (slot >= kSlots || bytes > _slot_bytes) throw std::runtime_error("remote edge: bad p2p slot");
+        void* s = hip::current_stream();
+        hip::check(nsh_memcpy_async(p, static_cast<char*>(_local) + (size_t)slot * _slot_bytes, bytes, NSH_D2D, s),
+                   "remote edge: p2p slot copy");
+        hip::check(nsh_stream_sync(s), "remote edge: p2p slot copy wait");
+        ch.send_msg(M_SLOT_FREE, slot);
+    }
+
+private:
+    bool _sender;
+    int _device;
+    size_t _slot_bytes;
+    std::function<bool()> _read_reverse;
+    void* _local = nullptr;  // receiver: the slots
+    void* _remote = nullptr; // sender: the receiver's slots, mapped
+    std::vector<void*> _events;
+    std::mutex _m;
+    std::deque<uint32_t> _free;
+    std::unique_ptr<outbox> _box;
 };
 
 // RCCL point-to-point on the partition streams (device rings on different GPUs). librccl
@@ -397,9 +720,13 @@ public:
         if (_comm) lib().comm_destroy(_comm);
     }
     const char* kind() const override { return "rccl"; }
-    void send(channel&, const void* p, size_t bytes) override
+    release send(channel& ch, uint64_t n, uint32_t ntags, const std::string& blob, const void* p, size_t bytes,
+                 std::function<void()>) override
     {
+        // header first: the receiver posts the matching ncclRecv when it reads it
+        write_data(ch, n, ntags, blob, [] {});
         ck(lib().send(p, bytes, /*ncclInt8*/ 0, /*peer*/ 1, _comm, hip::current_stream()), "ncclSend");
+        return release::now;
     }
     void recv(channel&, void* p, size_t bytes) override
     {
@@ -443,6 +770,7 @@ domain_adapter_remote::domain_adapter_remote(remote_role role, int crossing, con
 domain_adapter_remote::sptr domain_adapter_remote::make(remote_role role, port_sptr other_port, int crossing,
                                                         const remote_edge_options& opt)
 {
+    remote::transport_code(opt.transport); // unknown names fail here, not on the setup thread
     auto p = sptr(new domain_adapter_remote(role, crossing, opt));
     const bool faces_input = other_port->direction() == port_direction_t::INPUT;
     p->add_port(untyped_port::make(faces_input ? "output" : "input",
@@ -471,7 +799,8 @@ domain_adapter_remote::~domain_adapter_remote()
         if (_thr.joinable()) _thr.join(); // setup
         if (_ch && _ready.load()) {
             try {
-                _ch->send_msg(remote::M_CLOSE);
+                _tr->send_control(*_ch, remote::M_CLOSE); // behind every DATA / DONE still queued
+                _tr->flush();
                 _ch->shutdown_write();
                 _ch->drain_until_eof(_opt.timeout_s); // receiver closes after CLOSE
             } catch (...) {
@@ -550,7 +879,7 @@ void domain_adapter_remote::buffer_ready()
         mine.item_size = _isz;
         mine.is_device = dev_side ? 1 : 0;
         mine.device = _device;
-        mine.want = _opt.transport == "rccl" ? 1 : _opt.transport == "socket" ? 2 : 0;
+        mine.want = transport_code(_opt.transport);
         if (dev_side && _device >= 0) hip::check(nsh_device_pci_id(_device, mine.pci, (int)sizeof(mine.pci)), "remote edge: pci id");
         hello peer{};
         if (_role == remote_role::SEND) {
@@ -560,10 +889,32 @@ void domain_adapter_remote::buffer_ready()
             if (peer.magic != M_HELLO || peer.crossing != _crossing || peer.item_size != _isz)
                 throw std::runtime_error("remote edge: handshake mismatch on crossing " + std::to_string(_crossing));
             _max_chunk = (int)peer.max_chunk;
-            if (peer.chosen == 1)
+            int32_t chosen = peer.chosen;
+            if (chosen == T_P2P) {
+                p2p_offer offer{};
+                if (!_ch->recv_bytes(&offer, sizeof(offer))) throw std::runtime_error("remote edge: peer closed in p2p setup");
+                uint32_t status = 0;
+                std::string why;
+                try {
+                    _tr = std::make_shared<p2p_transport>(_device, offer, [this] { return read_reverse(100); });
+                } catch (const std::exception& e) {
+                    status = 1;
+                    why = e.what();
+                }
+                _ch->send_bytes(&status, sizeof(status));
+                if (status != 0) {
+                    if (mine.want == T_P2P) throw std::runtime_error(why);
+                    chosen = T_SOCKET; // auto: the receiver falls back with us
+                }
+            }
+            if (chosen == T_RCCL)
                 _tr = std::make_shared<rccl_transport>(*_ch, true, _device);
-            else
+            else if (chosen == T_DEFERRED_TEST)
+                _tr = std::make_shared<deferred_test_transport>();
+            else if (chosen == T_SOCKET)
                 _tr = std::make_shared<socket_transport>(dev_side);
+            else if (chosen != T_P2P)
+                throw std::runtime_error("remote edge: bad transport answer");
         } else {
             int lfd;
             {
@@ -579,19 +930,47 @@ void domain_adapter_remote::buffer_ready()
             _buffer->write_info(wi);
             mine.max_chunk = wi.n_items;
             peer.pci[sizeof(peer.pci) - 1] = 0;
-            const bool rccl_ok = dev_side && peer.is_device && mine.pci[0] && peer.pci[0] &&
-                                 std::strncmp(peer.pci, mine.pci, sizeof(mine.pci)) != 0;
-            const int want = peer.want ? peer.want : mine.want;
-            if (want == 1 && !rccl_ok)
+            // transport: rccl needs device rings on two GPUs (told apart by PCI bus id), p2p
+            // device rings on one or two GPUs, deferred_test host rings; auto = rccl across
+            // GPUs, p2p on one GPU, socket otherwise
+            const bool both_dev = dev_side && peer.is_device && mine.pci[0] && peer.pci[0];
+            const bool two_gpus = both_dev && std::strncmp(peer.pci, mine.pci, sizeof(mine.pci)) != 0;
+            const int32_t want = peer.want ? peer.want : mine.want;
+            if (want == T_RCCL && !two_gpus)
                 throw std::runtime_error("remote edge: rccl transport needs device rings on two different GPUs");
-            mine.chosen = (want != 2 && rccl_ok) ? 1 : 2;
+            if (want == T_P2P && !both_dev) throw std::runtime_error("remote edge: p2p transport needs device rings");
+            if (want == T_DEFERRED_TEST && (dev_side || peer.is_device))
+                throw std::runtime_error("remote edge: deferred_test transport needs host rings");
+            mine.chosen = want != T_AUTO ? want : two_gpus ? T_RCCL : both_dev ? T_P2P : T_SOCKET;
+            p2p_offer offer{};
+            std::shared_ptr<p2p_transport> p2p;
+            if (mine.chosen == T_P2P) {
+                try {
+                    p2p = std::make_shared<p2p_transport>(_device, (size_t)mine.max_chunk * _isz, offer);
+                } catch (const std::exception&) {
+                    if (want == T_P2P) throw;
+                    mine.chosen = T_SOCKET; // auto: IPC export unavailable
+                }
+            }
             _ch->send_bytes(&mine, sizeof(mine));
             _max_chunk = (int)mine.max_chunk;
-            if (mine.chosen == 1) {
-                _tr = std::make_shared<rccl_transport>(*_ch, false, _device);
-            } else {
-                _tr = std::make_shared<socket_transport>(dev_side);
+            if (mine.chosen == T_P2P) {
+                _ch->send_bytes(&offer, sizeof(offer));
+                uint32_t status = 1;
+                if (!_ch->recv_bytes(&status, sizeof(status))) throw std::runtime_error("remote edge: peer closed in p2p setup");
+                if (status == 0) {
+                    _tr = p2p;
+                } else {
+                    if (want == T_P2P) throw std::runtime_error("remote edge: the sender could not map the p2p slots");
+                    mine.chosen = T_SOCKET;
+                }
             }
+            if (mine.chosen == T_RCCL)
+                _tr = std::make_shared<rccl_transport>(*_ch, false, _device);
+            else if (mine.chosen == T_DEFERRED_TEST)
+                _tr = std::make_shared<deferred_test_transport>();
+            else if (mine.chosen == T_SOCKET)
+                _tr = std::make_shared<socket_transport>(dev_side);
         }
         if (_max_chunk <= 0) throw std::runtime_error("remote edge: receiver ring has no space");
         _ready.store(true);
@@ -676,67 +1055,76 @@ void domain_adapter_remote::recv_loop()
         }
         // Data after the k-th DONE belongs to run k+1: it waits until this process has
         // started that run (so runs do not mix), then for n contiguous writable items, or
-        // is discarded if this run's reader has already finished.
+        // is discarded if this run's reader has already finished. The ring is written under
+        // _ring_m, which reset_flags takes to drop a finished run's unread items: a message
+        // of the old run is either in the ring before that drop or goes to the discard area.
         const uint64_t data_run = _remote_done.load() + 1;
-        void* dst = nullptr;
+        bool placed = false;
         for (;;) {
-            if (_runs.load() < data_run) {
-                std::unique_lock<std::mutex> l(_m);
-                _cv.wait_for(l, std::chrono::milliseconds(1));
-                if (_closing.load()) return;
-                continue;
-            }
-            if (_reader_finished.load() >= data_run) break;
-            buffer_info_t wi{};
-            if (_buffer->write_info(wi) && wi.n_items >= n) {
-                dst = wi.ptr;
-                break;
+            if (_runs.load() >= data_run) {
+                std::lock_guard<std::mutex> w(_ring_m);
+                if (_reader_finished.load() >= data_run) break; // discard below
+                buffer_info_t wi{};
+                if (_buffer->write_info(wi) && wi.n_items >= n) {
+                    _tr->recv(*_ch, wi.ptr, bytes);
+                    const uint64_t w0 = _buffer->total_written(); // the items' absolute offsets start here
+                    for (auto& t : tags) {
+                        t.offset += w0;
+                        _buffer->add_tag(std::move(t));
+                    }
+                    _buffer->post_write(n);
+                    placed = true;
+                    break;
+                }
             }
             std::unique_lock<std::mutex> l(_m);
             _cv.wait_for(l, std::chrono::milliseconds(1));
             if (_closing.load()) return;
         }
-        if (!dst) { // reader finished: the bytes still have to be received
-            if (_scratch_bytes < bytes) {
-                if (_scratch) {
-                    if (_stream)
-                        nsh_free(_scratch);
-                    else
-                        std::free(_scratch);
-                }
-                _scratch = nullptr;
-                if (_stream)
-                    hip::check(nsh_malloc(_device, bytes, &_scratch), "remote edge: scratch");
-                else
-                    _scratch = std::malloc(bytes);
-                _scratch_bytes = bytes;
-            }
-            _tr->recv(*_ch, _scratch, bytes);
+        if (placed) {
+            _moved.fetch_add((uint64_t)n);
+            notify_downstream();
             continue;
         }
-        _tr->recv(*_ch, dst, bytes);
-        const uint64_t w0 = _buffer->total_written(); // the items' absolute offsets start here
-        for (auto& t : tags) {
-            t.offset += w0;
-            _buffer->add_tag(std::move(t));
+        // reader finished: the bytes still have to be received
+        if (_scratch_bytes < bytes) {
+            if (_scratch) {
+                if (_stream)
+                    nsh_free(_scratch);
+                else
+                    std::free(_scratch);
+            }
+            _scratch = nullptr;
+            if (_stream)
+                hip::check(nsh_malloc(_device, bytes, &_scratch), "remote edge: scratch");
+            else
+                _scratch = std::malloc(bytes);
+            _scratch_bytes = bytes;
         }
-        _buffer->post_write(n);
-        _moved.fetch_add((uint64_t)n);
-        notify_downstream();
+        _tr->recv(*_ch, _scratch, bytes);
     }
 }
 
+// Forward everything readable in the local ring, one DATA message per contiguous span of at
+// most _max_chunk items, and release each span by the edge ordering rule
+// (remote::transport, above): at once when the transport's read of it is ordered before any
+// later write (socket: consumed; rccl / p2p: enqueued on this partition stream), else when the
+// transport reports the read done (release_span on its thread). Items handed to the transport
+// but not yet released are skipped (_inflight).
 void domain_adapter_remote::pump()
 {
     if (_thr.joinable()) _thr.join(); // setup finished (first use)
     check_failed();
+    std::lock_guard<std::mutex> g(_pump_m);
     for (;;) {
         buffer_info_t ri{};
-        if (!_buffer->read_info(ri) || ri.n_items <= 0) break;
-        const int m = std::min(ri.n_items, _max_chunk);
+        if (!_buffer->read_info(ri)) break;
+        const int64_t avail = (int64_t)ri.n_items - (int64_t)_inflight;
+        if (avail <= 0) break;
+        const int m = (int)std::min<int64_t>(avail, _max_chunk);
         // the tags of these m items travel in the same message (offsets relative to its first item)
-        const uint64_t r0 = _buffer->total_read();
-        const auto tags = _buffer->tags_in_window(0, (uint64_t)m);
+        const uint64_t r0 = _buffer->total_read() + _inflight;
+        const auto tags = _buffer->tags_in_window(_inflight, _inflight + (uint64_t)m);
         std::string blob;
         for (auto& t : tags) {
             remote::put_raw(blob, (uint64_t)(t.offset - r0));
@@ -744,31 +1132,60 @@ void domain_adapter_remote::pump()
             remote::put_pmt(blob, t.value);
             remote::put_pmt(blob, t.srcid);
         }
-        _ch->send_msg_with(
-            remote::M_DATA, (uint64_t)m,
-            [&] {
-                if (!tags.empty()) {
-                    const uint32_t len = (uint32_t)blob.size();
-                    _ch->send_bytes(&len, sizeof(len));
-                    _ch->send_bytes(blob.data(), blob.size());
-                }
-                _tr->send(*_ch, ri.ptr, (size_t)m * _isz);
-            },
-            (uint32_t)tags.size());
-        _buffer->prune_tags(m); // sent with their items
-        _buffer->post_read(m);
+        const void* p = static_cast<const char*>(ri.ptr) + _inflight * _isz;
+        const auto how = _tr->send(*_ch, (uint64_t)m, (uint32_t)tags.size(), blob, p, (size_t)m * _isz,
+                                   [this, m] { release_span(m, true); });
+        if (how == remote::transport::release::now)
+            release_span(m, false);
+        else
+            _inflight += (uint64_t)m;
         _moved.fetch_add((uint64_t)m);
     }
 }
 
+// The oldest m forwarded items leave the ring: their tags went with them. `deferred`: called on
+// the transport's thread once its read completed (wakes the upstream block, which may be
+// waiting for space); else on the partition thread inside pump().
+void domain_adapter_remote::release_span(int m, bool deferred)
+{
+    std::unique_lock<std::mutex> g(_pump_m, std::defer_lock);
+    if (deferred) g.lock();
+    _buffer->prune_tags(m);
+    _buffer->post_read(m);
+    if (!deferred) return;
+    _inflight -= (uint64_t)m;
+    g.unlock();
+    try {
+        for (auto& p : all_ports())
+            p->notify_connected_ports(std::make_shared<scheduler_action>(scheduler_action_t::NOTIFY_OUTPUT, id()));
+    } catch (const std::exception&) {
+    }
+}
+
+// SEND: handle one reverse message if one arrives within timeout_ms (READER_DONE, or a message
+// the transport owns, e.g. p2p's M_SLOT_FREE). Returns whether one was handled.
+bool domain_adapter_remote::read_reverse(int timeout_ms)
+{
+    std::lock_guard<std::mutex> g(_rev_m);
+    if (!_ch->readable(timeout_ms)) return false;
+    remote::msg m{};
+    if (!_ch->recv_msg(m)) throw std::runtime_error("remote edge: receiver closed");
+    if (m.type == remote::M_READER_DONE)
+        _remote_done.fetch_add(1);
+    else if (!_tr || !_tr->on_reverse(m))
+        throw std::runtime_error("remote edge: unexpected reverse message");
+    return true;
+}
+
 void domain_adapter_remote::poll_reverse()
 {
-    // only READER_DONE travels upstream; called on the sender's partition thread
+    // called on the sender's partition thread (reader_done)
     if (!_ready.load()) return;
-    while (_ch->readable(0)) {
-        remote::msg m{};
-        if (!_ch->recv_msg(m)) return;
-        if (m.type == remote::M_READER_DONE) _remote_done.fetch_add(1);
+    try {
+        while (read_reverse(0)) {
+        }
+    } catch (const std::exception&) {
+        // receiver gone: its READER_DONE / DONE bookkeeping no longer matters
     }
 }
 
@@ -801,7 +1218,7 @@ void domain_adapter_remote::set_writer_done()
     _buffer->set_writer_done();
     if (_role == remote_role::SEND) {
         pump();
-        _ch->send_msg(remote::M_DONE);
+        _tr->send_control(*_ch, remote::M_DONE); // behind this run's DATA messages
     }
 }
 void domain_adapter_remote::set_reader_done()
@@ -829,9 +1246,20 @@ bool domain_adapter_remote::reader_done() const
     const_cast<domain_adapter_remote*>(this)->poll_reverse();
     return _remote_done.load() >= _runs.load();
 }
+// A new run (prepare_run, every thread of the last run finished). The previous run's unread
+// items and their tags are dropped here, before _runs moves on: a RECV ring may hold the
+// remainder a decimator left below one output, and the receive thread starts writing the next
+// run's data into the ring as soon as _runs is bumped (the remote counterpart of
+// buffer::discard_unread, which prepare_run calls after reset_flags). A SEND side first lets
+// its transport finish the last run's messages (deferred releases included).
 void domain_adapter_remote::reset_flags()
 {
-    if (_buffer) _buffer->reset_flags();
+    if (_role == remote_role::SEND && _tr && _ready.load()) _tr->flush();
+    std::lock_guard<std::mutex> w(_ring_m);
+    if (_buffer) {
+        _buffer->reset_flags();
+        _buffer->discard_unread();
+    }
     _runs.fetch_add(1);
 }
 

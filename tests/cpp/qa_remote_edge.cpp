@@ -12,6 +12,7 @@
 #include <cstdlib>
 #include <gnuradio/blocklib/blocks/annotator.hpp>
 #include <gnuradio/blocklib/blocks/copy.hpp>
+#include <gnuradio/blocklib/blocks/fir_filter_ccf.hpp>
 #include <gnuradio/blocklib/blocks/head.hpp>
 #include <gnuradio/blocklib/blocks/null_sink.hpp>
 #include <gnuradio/blocklib/blocks/null_source.hpp>
@@ -42,7 +43,18 @@ static remote_edge_options opts()
     remote_edge_options o;
     o.base_port = env_int("QA_PORT", 29650);
     o.timeout_s = 60;
+    if (const char* t = std::getenv("QA_TRANSPORT")) o.transport = t; // default "auto"
     return o;
+}
+// every crossing of this process negotiated QA_EXPECT_TRANSPORT (when set)
+static void expect_transport(const domain_adapter_remote_conf::sptr& da)
+{
+    const char* want = std::getenv("QA_EXPECT_TRANSPORT");
+    for (auto& a : da->adapters()) {
+        std::printf("  crossing %d (%s): transport %s\n", a->crossing(),
+                    a->role() == remote_role::SEND ? "send" : "recv", a->transport_kind().c_str());
+        if (want) EXPECT_TRUE(a->transport_kind() == want);
+    }
 }
 // the scheduler for a domain owned by `owner`: real here, a placeholder elsewhere
 static scheduler_sptr sched_for(int owner, scheduler_sptr real)
@@ -122,6 +134,95 @@ TEST(RemoteCpu, TagsCrossProcesses)
                 EXPECT_TRUE(t.srcid && std::get<std::string>(t.srcid->value()) == "ann0");
             }
         }
+    }
+}
+
+// The CPU form of RemoteGpu.RestartDropsRemainder: host rings, fir_filter_ccf(h, 4) downstream
+// of the crossing, n = 4k + 3, three runs; each must equal the first (bit-identical) and the
+// reference.
+TEST(RemoteCpu, RestartDropsRemainder)
+{
+    const size_t n = 100003;
+    const auto h = lowpass(31, 0.1);
+    auto x = synth(n, 5);
+    auto src = blocks::vector_source_c::make(x);
+    auto cp = blocks::copy::make(sizeof(gr_complex));
+    auto fir = blocks::fir_filter_ccf::make(h, 4);
+    auto snk = blocks::vector_sink_c::make(1, n / 4);
+    auto fg = flowgraph::make();
+    fg->connect(src, 0, cp, 0);
+    fg->connect(cp, 0, fir, 0);
+    fg->connect(fir, 0, snk, 0);
+    auto s0 = sched_for(0, schedulers::scheduler_mt::make("r0", 8192));
+    auto s1 = sched_for(1, schedulers::scheduler_mt::make("r1", 8192));
+    fg->set_schedulers({ s0, s1 });
+    auto o = opts();
+    o.base_port += 80;
+    auto da = domain_adapter_remote_conf::make(o);
+    domain_conf_vec dc{ domain_conf(s0, { src, cp }, da), domain_conf(s1, { fir, snk }, da) };
+    fg->partition(dc);
+    const auto ref = fir_ref(x, h, 4);
+    std::vector<gr_complex> first;
+    for (int run = 0; run < 3; ++run) {
+        fg->run();
+        if (rank() == 1) {
+            ASSERT_TRUE(snk->data().size() == ref.size());
+            EXPECT_TRUE(close_normwise(snk->data(), ref));
+            if (run == 0)
+                first = snk->data();
+            else
+                EXPECT_TRUE(snk->data() == first);
+        }
+    }
+}
+
+// The edge's release rule with a transport whose reads complete later on another thread
+// (transport "deferred_test": the payload is read from the sender's ring span after
+// NSH_REMOTE_TEST_DELAY_US, and the span is released only then). Small rings (8192 items) so
+// the upstream block would overwrite a released span within microseconds: the transport
+// checksums each span at send() and again at its delayed read, and counts any difference.
+// Expect: no violations, the data bit-exact over three runs. With
+// NSH_REMOTE_TEST_EARLY_RELEASE=1 (QA_EXPECT_VIOLATIONS=1) the transport claims its read is
+// done at send(): the negative control, which must show violations.
+TEST(RemoteCpu, DeferredRelease)
+{
+    const bool early = env_int("QA_EXPECT_VIOLATIONS", 0) != 0;
+    const size_t n = 120000;
+    auto x = synth(n, 13);
+    const gr_complex k(1.5f, -0.5f);
+    std::vector<gr_complex> ref(x);
+    for (auto& v : ref) v = cmul(v, k);
+    {
+        auto src = blocks::vector_source_c::make(x);
+        auto mul = blocks::multiply_const_cc::make(k);
+        auto cp = blocks::copy::make(sizeof(gr_complex));
+        auto snk = blocks::vector_sink_c::make(1, n);
+        auto fg = flowgraph::make();
+        fg->connect(src, 0, mul, 0);
+        fg->connect(mul, 0, cp, 0);
+        fg->connect(cp, 0, snk, 0);
+        auto s0 = sched_for(0, schedulers::scheduler_mt::make("r0", 8192));
+        auto s1 = sched_for(1, schedulers::scheduler_mt::make("r1", 8192));
+        fg->set_schedulers({ s0, s1 });
+        auto o = opts();
+        o.base_port += 90;
+        o.transport = "deferred_test";
+        auto da = domain_adapter_remote_conf::make(o);
+        domain_conf_vec dc{ domain_conf(s0, { src, mul }, da), domain_conf(s1, { cp, snk }, da) };
+        fg->partition(dc);
+        for (int run = 0; run < (early ? 1 : 3); ++run) {
+            fg->run();
+            if (rank() == 1 && !early) EXPECT_TRUE(snk->data() == ref);
+        }
+        for (auto& a : da->adapters()) std::printf("  transport %s\n", a->transport_kind().c_str());
+    } // adapters destroyed: the sender's transport has read and sent every message
+    if (rank() == 0) {
+        const uint64_t v = remote::deferred_test_violations();
+        std::printf("  deferred_test violations: %llu\n", (unsigned long long)v);
+        if (early)
+            EXPECT_TRUE(v > 0);
+        else
+            EXPECT_EQ(v, (uint64_t)0);
     }
 }
 
@@ -213,13 +314,14 @@ TEST(RemoteGpu, DeviceChainRestart)
     fg->partition(dc);
     std::vector<gr_complex> ref(x);
     for (auto& v : ref) v = cmul(v, k);
-    for (int run = 0; run < 2; ++run) { // vector_sink clears at each start
+    for (int run = 0; run < 3; ++run) { // vector_sink clears at each start
         fg->run();
         if (rank() == 1) {
             if (snk->data().size() != n) std::fprintf(stderr, "  run %d: %zu items\n", run, snk->data().size());
             EXPECT_TRUE(snk->data() == ref);
         }
     }
+    expect_transport(da);
 }
 
 // Tags through device rings and a process crossing: host annotator -[H2D]-> hip::copy [0]
@@ -255,6 +357,7 @@ TEST(RemoteGpu, DeviceTags)
                         domain_conf(g1, { c1 }, da), domain_conf(s1, { ann1, snk }, dd) };
     fg->partition(dc);
     fg->run();
+    expect_transport(da);
     if (rank() == 1) {
         auto seen = ann1->data();
         ASSERT_TRUE(seen.size() == 4u);
@@ -288,10 +391,51 @@ TEST(RemoteGpu, DecimatingPipelineC5)
     auto da = domain_adapter_remote_conf::make(o);
     domain_conf_vec dc{ domain_conf(s0, { src, st[0], st[1] }, da), domain_conf(s1, { st[2], st[3], snk }, da) };
     fg->partition(dc);
-    fg->run();
-    if (rank() == 1) {
-        auto ref = synth(n);
-        for (int i = 0; i < 4; ++i) ref = fir_ref(ref, h, 2);
-        EXPECT_TRUE(close_normwise(snk->data(), ref));
+    auto ref = synth(n);
+    for (int i = 0; i < 4; ++i) ref = fir_ref(ref, h, 2);
+    for (int run = 0; run < 2; ++run) {
+        fg->run();
+        if (rank() == 1) EXPECT_TRUE(close_normwise(snk->data(), ref));
     }
+    expect_transport(da);
+}
+
+// A restarted two-process pipeline whose stream length is not a multiple of the downstream
+// decimation: the receiving ring keeps 3 items below one output at the end of each run,
+// which must be dropped before the next run's data arrive (they used to
+// be prepended to the next run's stream). device rings, fir/4 downstream; every run must
+// equal the single-process result.
+TEST(RemoteGpu, RestartDropsRemainder)
+{
+    const size_t n = (1u << 18) + 3;
+    const auto h = lowpass(127, 0.1);
+    auto x = synth(n, 5);
+    auto src = blocks::vector_source_c::make(x);
+    auto cp = hip::copy::make(1);
+    auto fir = hip::fir_filter_ccf::make(h, 4);
+    auto snk = blocks::vector_sink_c::make(1, n / 4);
+    auto fg = flowgraph::make();
+    fg->connect(src, 0, cp, 0)->set_custom_buffer(HIP_BUFFER_ARGS_H2D);
+    fg->connect(cp, 0, fir, 0);
+    fg->connect(fir, 0, snk, 0)->set_custom_buffer(HIP_BUFFER_ARGS_D2H);
+    auto s0 = sched_for(0, schedulers::scheduler_hip::make("g0", 0, 1u << 19));
+    auto s1 = sched_for(1, schedulers::scheduler_hip::make("g1", 0, 1u << 19));
+    fg->set_schedulers({ s0, s1 });
+    auto o = opts();
+    o.base_port += 50;
+    auto da = domain_adapter_remote_conf::make(o);
+    domain_conf_vec dc{ domain_conf(s0, { src, cp }, da), domain_conf(s1, { fir, snk }, da) };
+    fg->partition(dc);
+    const auto ref = fir_ref(x, h, 4);
+    for (int run = 0; run < 3; ++run) {
+        // not bit-identical between runs: the MFMA decimator's per-chunk scales follow how the
+        // stream was split into work() calls, which the message timing decides; a stream
+        // shifted by the 3 stale items would miss the reference by O(1)
+        fg->run();
+        if (rank() == 1) {
+            ASSERT_TRUE(snk->data().size() == ref.size());
+            EXPECT_TRUE(close_normwise(snk->data(), ref));
+        }
+    }
+    expect_transport(da);
 }

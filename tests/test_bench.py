@@ -39,6 +39,25 @@ def test_launcher_rejects_mismatched_world():
     assert out.returncode != 0 and "WORLD_SIZE" in out.stderr
 
 
+def test_launcher_without_gpus_flag_takes_world_size():
+    """`torchrun --nproc_per_node 2 bench.py` (no --gpus): each rank takes WORLD_SIZE."""
+    import socket
+
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in (0, 1):
+        env = dict(os.environ, WORLD_SIZE="2", RANK=str(r), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "bench.py", "--rank-check"], cwd=ROOT, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True, env=env))
+    outs = [p.communicate(timeout=120) for p in procs]
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0, e[-3000:]
+    assert _json_line(outs[0][0]) == {"n_gpus": 2, "world": 2}
+
+
 def test_c5_layout():
     import bench
 
@@ -95,7 +114,8 @@ def test_bench_spawns_ranks_and_c5_leg(torch_cuda):
     c5 = d["c5_pipeline"]
     assert c5["ok"] and c5["parity"]["ok"], c5
     assert c5["value"] > 0
-    assert "socket" in c5["transports"]["0"] and "socket" in c5["transports"]["1"], c5
+    # both ranks share the box's one GPU: auto negotiates the IPC landing-slot transport
+    assert "p2p" in c5["transports"]["0"] and "p2p" in c5["transports"]["1"], c5
 
 
 @pytest.mark.gpu

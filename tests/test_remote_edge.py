@@ -1,9 +1,12 @@
 """Cross-process flowgraphs (gr::domain_adapter_remote): each C++ case in
 tests/cpp/qa_remote_edge.cpp runs as TWO processes (ranks 0 and 1) that build the same
 flowgraph and domain list and each run their own domains, joined by TCP-controlled
-crossing edges -- host rings over the socket on CPU; device rings (hip_buffer) on the GPU,
-staged through pinned memory because both ranks share the box's one GPU (RCCL needs two
-devices; that transport is selected automatically on a multi-GPU node)."""
+crossing edges -- host rings over the socket on CPU (plus the "deferred_test" transport,
+whose reads of the sender's ring complete late on another thread: the edge's release rule);
+device rings (hip_buffer) on the GPU, where both ranks share the box's one GPU: the "p2p"
+transport (stream-ordered copies into IPC-mapped landing slots, auto's choice on one GPU) and
+the pinned-memory "socket" staging. RCCL needs two devices; auto selects it on a multi-GPU
+node (test_bench.py::test_bench_c5_rccl_two_gpus)."""
 import os
 import random
 import socket
@@ -36,13 +39,13 @@ def free_port_block(width=64):
     raise RuntimeError("no free port block")
 
 
-def run_pair(case, timeout=120):
+def run_pair(case, timeout=120, env_extra=None):
     if not os.path.exists(EXE):
         subprocess.run(["make", "-s", "-C", ROOT, "tests"], check=True)
-    port = free_port_block()
+    port = free_port_block(128)
     procs = []
     for r in (0, 1):
-        env = dict(os.environ, QA_RANK=str(r), QA_PORT=str(port))
+        env = dict(os.environ, QA_RANK=str(r), QA_PORT=str(port), **(env_extra or {}))
         procs.append(subprocess.Popen([EXE, case], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
     outs = []
     for p in procs:
@@ -57,16 +60,41 @@ def run_pair(case, timeout=120):
         print(f"--- rank {r} ---\n{out}")
         assert p.returncode == 0, f"rank {r} failed:\n{out}"
         assert "0 failure(s)" in out and "1 test(s)" in out, out
+    return outs
 
 
 @pytest.mark.parametrize("case", ["RemoteCpu.ChainRestart", "RemoteCpu.TwoCrossingsBothWays",
-                                  "RemoteCpu.ReaderFinishesFirst", "RemoteCpu.TagsCrossProcesses"])
+                                  "RemoteCpu.ReaderFinishesFirst", "RemoteCpu.TagsCrossProcesses",
+                                  "RemoteCpu.RestartDropsRemainder"])
 def test_remote_edges_cpu(case):
     run_pair(case)
 
 
+def test_deferred_release_keeps_span_until_read():
+    """The release rule with an asynchronous reader: no span is overwritten before the
+    transport read it (checksums at send and at the delayed read), data bit-exact, 3 runs."""
+    outs = run_pair("RemoteCpu.DeferredRelease", env_extra={"NSH_REMOTE_TEST_DELAY_US": "1500"})
+    assert "deferred_test violations: 0" in outs[0]
+
+
+def test_deferred_release_negative_control():
+    """The same transport releasing at send() (what the rule forbids for an unordered read):
+    the upstream block overwrites spans before they are read, and the checksums see it --
+    the positive test above can fail."""
+    outs = run_pair("RemoteCpu.DeferredRelease", env_extra={
+        "NSH_REMOTE_TEST_DELAY_US": "3000", "NSH_REMOTE_TEST_EARLY_RELEASE": "1", "QA_EXPECT_VIOLATIONS": "1"})
+    assert "deferred_test(early)" in outs[0]
+
+
+GPU_CASES = ["RemoteGpu.DeviceChainRestart", "RemoteGpu.DecimatingPipelineC5", "RemoteGpu.DeviceTags",
+             "RemoteGpu.RestartDropsRemainder"]
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", ["RemoteGpu.DeviceChainRestart", "RemoteGpu.DecimatingPipelineC5",
-                                  "RemoteGpu.DeviceTags"])
-def test_remote_edges_gpu(case):
-    run_pair(case, timeout=300)
+@pytest.mark.parametrize("case", GPU_CASES)
+@pytest.mark.parametrize("transport", ["auto", "p2p", "socket"])
+def test_remote_edges_gpu(case, transport):
+    """Both ranks on the box's one GPU: auto must negotiate p2p (IPC landing slots); socket is
+    the pinned-memory staging it replaces."""
+    expect = {"auto": "p2p", "p2p": "p2p", "socket": "socket(staged)"}[transport]
+    run_pair(case, timeout=300, env_extra={"QA_TRANSPORT": transport, "QA_EXPECT_TRANSPORT": expect})

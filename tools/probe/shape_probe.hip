@@ -5,7 +5,7 @@
 //   contiguous : workgroup w owns chunks [w*per, (w+1)*per), register prefetch depth 2
 //                (the FIR's shape)
 // Occupancy is forced with dynamic LDS (workgroups per CU = floor(160 KiB / lds)).
-// Usage: shape_probe [log2 samples, default 28]
+// Usage: shape_probe [log2 samples, default 28]   (build: tools/probe/build_probes.sh shape_probe)
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
