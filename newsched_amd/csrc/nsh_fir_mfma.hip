@@ -1607,14 +1607,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
     load(c_first, va, ha);
     constexpr int UPC = G::TW / 8; // 16-B units per copy
     uint4 ti[2] = {};
-#if !(NSH_FIR_ABLATE & 4096) // timing only: no tap image loads
     {   // the tap image (L1/L2 hits), both units per lane issued before any wait
         const __amdgpu_buffer_rsrc_t tr = __builtin_amdgcn_make_buffer_rsrc((void*)timg, (short)0, G::IMG_UNITS * 16, 0x00020000);
 #pragma unroll
         for (int k = 0; k < 2; ++k)
             ti[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(tr, 16 * (tid + G::NT * k), 0, 0));
     }
-#endif
     // tap image -> LDS at the padded copy pitch
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
@@ -1626,11 +1624,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
     const int h = lane >> 5;
     const int phase = rho;
     auto process = [&](int64_t ch, const float4 (&v)[4], const float4& hv) {
-#if NSH_FIR_ABLATE & 8192 // timing only: fixed scale, no reductions, no first barrier
-        const int s = 0;
-        const bool exact = false;
-        if (ch < 0) slot_max[0] = 0;
-#else
         {   // chunk + halo range -> workgroup scale and exact-path decision
             float mf = max_abs4(hv);
             unsigned z = min_nz1(hv);
@@ -1651,7 +1644,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
         const unsigned z = min(min(slot_mnz[0], slot_mnz[1]), min(slot_mnz[2], slot_mnz[3]));
         const int s = scale_of(m);
         const bool exact = chunk_needs_exact(m, z, s);
-#endif
         if (exact) {
             float4* r = reinterpret_cast<float4*>(lds);
             if (tid < G::HP) r[tid] = hv;
@@ -1703,10 +1695,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
                     B0 = __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7);
                     B1 = __builtin_shufflevector(b2, b3, 0, 1, 2, 3, 4, 5, 6, 7);
                 }
-#if NSH_FIR_ABLATE & 256 // timing only: LDS fragment reads kept, no matrix work
-                acc_hi[st & 15] += (float)A0[0] + (float)A1[1] + (float)B0[2] + (float)B1[3];
-                continue;
-#endif
                 acc_hi = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, B0, acc_hi, 0, 0, 0);
                 acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(A0, B1, acc_lo, 0, 0, 0);
                 acc_lo = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1, B0, acc_lo, 0, 0, 0);
@@ -1723,14 +1711,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
             }
         }
         const __amdgpu_buffer_rsrc_t r = chunk_rsrc<2048>(out, ch, n_out);
-#if NSH_FIR_ABLATE & 16384 // timing only: four contiguous 16-B stores per lane (a copy's store shape)
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const nf2 a = o[2 * u], bb = o[2 * u + 1];
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(nsh::u32x4, nf4{ a.x, a.y, bb.x, bb.y }), r, (tid + G::NT * u) * 16, 0, AUX_NT);
-        }
-        return;
-#endif
         const int base = wave * TILE + phase;
 #pragma unroll
         for (int reg = 0; reg < 8; ++reg) buf_store_f2(r, (base + 32 * ((reg & 3) + 8 * (reg >> 2) + 4 * h)) * 8, o[reg]);
