@@ -4,7 +4,11 @@
 // directly. The chain composes into y[m] = sum_n heq[n] x[m D - n], D = prod D_s (8 or 16),
 // computed in one pass over HBM by polyphase-FFT overlap-save (nsh_fir_cascade_ccf,
 // k_fir_pfft<D>): outputs within fp32 transform rounding of the staged chain (north-star
-// tolerance 1e-5), not bit-identical to it. State: the (len(heq) - 1)-sample input history,
+// tolerance 1e-5), not bit-identical to it. The rounding is relative to each 512-row frame's
+// input level, not to each output: |y - y_chain| <= 1e-5 |y_chain| + 1e-6 max|x in the frame|
+// sum|heq|, so a quiet stretch sharing a frame with a far louder burst is accurate to the
+// burst's level (nsh_hip.h). Frames holding inf/NaN run the staged chain itself: NaN and inf
+// outputs exactly where the chain puts them. State: the (len(heq) - 1)-sample input history,
 // ping-ponged between work() calls like fir_filter_ccf's; zeroed on every start() -- the same
 // state as a chain whose stages all start from zero history.
 // Tags: propagated as by one decimating block with D = prod D_s (the runtime's rule applied

@@ -34,9 +34,13 @@
 // Scale: the frame's input is multiplied by 2^k (k from the frame's largest magnitude, reduced
 // per wave over the rows as they arrive) so that it lies in [1, 2) before the transforms, and
 // the outputs by 2^-k: exact power-of-two scaling, so no finite input overflows or loses
-// precision to fp32's range. A frame holding inf or NaN is computed by the fp32 direct form on
-// the composite taps in the same launch (its non-finite outputs sit exactly where the
-// cascade's do: the composite support is the cascade's).
+// precision to fp32's range. A frame holding inf or NaN is computed by the staged chain itself
+// in the fp32 direct form, stage by stage over the frame's window, in the same launch: its
+// outputs carry the chain's exact NaN / inf pattern (the composite filter could give +-inf
+// where the chain's intermediate inf - inf is NaN). One-stage plans: the direct form on h.
+// Accuracy contract: transform rounding is relative to the frame's level, not to each output --
+// an output of a quiet stretch that shares its 512-row frame with a loud burst carries the
+// burst's rounding, |dy| <~ 1e-6 max|x in frame| sum|heq|.
 // Accuracy: fp32 transforms, error ~1e-7 of the frame's RMS (C5: 2.2e-7 of max|y| vs the
 // oracle's double-accumulated cascade; north-star tolerance 1e-5).
 #include "nsh_common.hpp"
@@ -79,6 +83,7 @@ __device__ __forceinline__ cf cmul_tw(cf a, cf w)
 }
 
 constexpr int M = 512;          // FFT length per phase
+constexpr int MAX_STAGES = 8;   // stages of a chain (total decimation <= 16)
 constexpr int IMG = 572;         // a wave's LDS image: the largest padded index below + 1, kept even so
                                 // every carve stays 16-B aligned (an off-alignment b64/b128 access
                                 // replays at 64-128 cycles)
@@ -287,6 +292,12 @@ struct pfft_args {
     int64_t nf;        // frames in the launch
     int64_t fpw;       // frames per workgroup
     unsigned long long* trace; // NSH_PFFT_TRACE builds only: per-frame phase timestamps of workgroup 0
+    // the stages, for frames holding inf/NaN (0 stages: the composite direct form on heq)
+    const float* stap; // concatenated stage taps
+    int nst;
+    int sl[MAX_STAGES];
+    int sd[MAX_STAGES];
+    int n1;            // entries of stage-1 output within a window (buffer A; buffer B follows it)
 };
 
 #ifndef NSH_PFFT_TRACE
@@ -480,8 +491,8 @@ __global__ __launch_bounds__(64 * P / PW, 1) void k_fir_pfft(pfft_args a)
                 for (int i = 1; i < PW; ++i) pr += cmul_tw(v[i][r], fw[i][r]);
                 if (!(NSH_PFFT_ABLATE & 128)) ib.n[64 * r] = pr;
             }
-        } else {
-            // fp32 direct form on the composite taps: y[j] = sum_n heq[n] u[P q - n], q = Q + t
+        } else if (a.nst < 2) {
+            // one stage: the fp32 direct form on its taps (heq = h): y[j] = sum_n heq[n] u[P q - n], q = Q + t
             for (int t = tid; t < V; t += NT) {
                 const int q = Q + t;
                 cf acc = cf{ 0.f, 0.f };
@@ -492,6 +503,40 @@ __global__ __launch_bounds__(64 * P / PW, 1) void k_fir_pfft(pfft_args a)
                 }
                 if (rowf + t < a.n_out) a.out[rowf + t] = make_float2(acc.x, acc.y);
             }
+        } else {
+            // The staged chain itself, stage by stage in the fp32 direct form over the window (which
+            // holds the chain's whole history: P Q >= sum_s (L_s - 1) prod_{j<s} D_j), so a frame
+            // holding inf/NaN gets the chain's non-finite pattern exactly (the composite filter can
+            // give +-inf where the chain's intermediate inf - inf gives NaN). Stage outputs ping-pong
+            // between two buffers in the wave images (free now: the barrier waits for the previous
+            // frame's inverse wave); values near the window start use a truncated history and are
+            // never read by a final output.
+            nsh::lds_barrier();
+            cf* buf[2] = { imgs, imgs + a.n1 };
+            const float* hs = a.stap;
+            int n_prev = P * M;
+            for (int st = 0; st < a.nst; ++st) {
+                const int Ds = a.sd[st], Ls = a.sl[st];
+                const int n_cur = (n_prev - 1) / Ds + 1;
+                const cf* src = buf[(st + 1) & 1];
+                cf* dst = buf[st & 1];
+                for (int i = tid; i < n_cur; i += NT) {
+                    cf acc = cf{ 0.f, 0.f };
+                    for (int k = 0; k < Ls; ++k) {
+                        const int jj = Ds * i - k;
+                        if (jj < 0) break;
+                        const cf u = st == 0 ? ring[ring_at<P>((int)((rowf + jj / P) & (M - 1)), jj % P)] : src[jj];
+                        acc = __builtin_elementwise_fma(cf{ hs[k], hs[k] }, u, acc);
+                    }
+                    dst[i] = acc;
+                }
+                hs += Ls;
+                n_prev = n_cur;
+                nsh::lds_barrier();
+            }
+            const cf* last = buf[(a.nst - 1) & 1]; // y[m] at local m = Q + t
+            for (int t = tid; t < V; t += NT)
+                if (rowf + t < a.n_out) a.out[rowf + t] = make_float2(last[Q + t].x, last[Q + t].y);
         }
         PFFT_T(1);
         nsh::lds_barrier(); // B1: window f read, images hold the per-phase products
@@ -585,6 +630,11 @@ struct nsh_fir_casc_plan {
     float2* F = nullptr;
     float2* tw = nullptr;
     float* heq = nullptr;
+    float* stap = nullptr; // stage taps, concatenated (non-finite frames)
+    int nst = 0;           // stages the non-finite path runs (0: composite direct form)
+    int sl[MAX_STAGES] = {};
+    int sd[MAX_STAGES] = {};
+    int n1 = 0;
     std::string kernel;
 };
 
@@ -658,6 +708,24 @@ int nsh_fir_cascade_plan_create(int dev, const float* const* taps_host, const in
             F[(size_t)ph * M + k] = make_float2((float)(re / M), (float)(im / M));
         }
     std::vector<float> hf(heq.begin(), heq.end());
+    // the stages for non-finite frames: stage outputs within one window ping-pong between two
+    // buffers in the wave images (stage 1's, then stage 2's size); a chain that does not fit (a
+    // leading decim-1 stage), or has one stage, uses the composite direct form instead
+    std::vector<float> st;
+    if (nstages >= 2 && nstages <= MAX_STAGES) {
+        const int n1 = (D * M - 1) / decims[0] + 1, n2 = (n1 - 1) / decims[1] + 1;
+        if ((int64_t)(n1 + n2) <= (int64_t)D * IMG) {
+            p->nst = nstages;
+            p->n1 = n1;
+            for (int s = 0; s < nstages; ++s) {
+                p->sl[s] = ntaps[s];
+                p->sd[s] = decims[s];
+                st.insert(st.end(), taps_host[s], taps_host[s] + ntaps[s]);
+            }
+        }
+    }
+    if (e == hipSuccess && !st.empty()) e = hipMalloc(&p->stap, st.size() * sizeof(float));
+    if (e == hipSuccess && !st.empty()) e = hipMemcpy(p->stap, st.data(), st.size() * sizeof(float), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMalloc(&p->F, F.size() * sizeof(float2));
     if (e == hipSuccess) e = hipMalloc(&p->tw, tw.size() * sizeof(float2));
     if (e == hipSuccess) e = hipMalloc(&p->heq, hf.size() * sizeof(float));
@@ -672,6 +740,7 @@ int nsh_fir_cascade_plan_create(int dev, const float* const* taps_host, const in
         if (p->F) (void)hipFree(p->F);
         if (p->tw) (void)hipFree(p->tw);
         if (p->heq) (void)hipFree(p->heq);
+        if (p->stap) (void)hipFree(p->stap);
         delete p;
         return nsh::fail(e, "nsh_fir_cascade_plan_create");
     }
@@ -687,6 +756,7 @@ int nsh_fir_cascade_plan_destroy(void* plan)
     if (p->F) (void)hipFree(p->F);
     if (p->tw) (void)hipFree(p->tw);
     if (p->heq) (void)hipFree(p->heq);
+    if (p->stap) (void)hipFree(p->stap);
     delete p;
     return 0;
 }
@@ -721,6 +791,13 @@ int nsh_fir_cascade_ccf(void* plan, const float* in, const float* hist_in, float
     int64_t wg = a.nf < max_wg ? a.nf : max_wg;
     a.fpw = (a.nf + wg - 1) / wg;
     a.trace = nullptr;
+    a.stap = p->stap;
+    a.nst = p->nst;
+    a.n1 = p->n1;
+    for (int k = 0; k < MAX_STAGES; ++k) {
+        a.sl[k] = p->sl[k];
+        a.sd[k] = p->sd[k];
+    }
 #if NSH_PFFT_TRACE
     {
         static unsigned long long* tr = nullptr;

@@ -14,8 +14,12 @@
 // into one block with one launch per work() call (gnuradio/hip_fusion.hpp), and
 // fft -> multiply_const_vcc -> ifft into the channelizer; those results are bit-identical.
 // Chains of decimating fir_filter_ccf blocks with total decimation 8 or 16 become one
-// fir_filter_cascade_ccf (within tolerance, not bit-identical; set_fir_fusion(false) keeps
-// them). set_fusion(false) keeps every block and edge as connected.
+// fir_filter_cascade_ccf: NOT bit-identical -- within fp32 transform rounding relative to each
+// 512-row frame's input level (nsh_hip.h, nsh_fir_cascade_ccf); inf/NaN frames reproduce the
+// chain's non-finite pattern. It is on by default and a make() argument, so a flowgraph that
+// needs the staged blocks' exact outputs says so where the scheduler is built:
+// scheduler_hip::make("hip", dev, buf, /*fir_fusion=*/false) (or set_fir_fusion(false) before
+// the flowgraph is validated). set_fusion(false) keeps every block and edge as connected.
 #pragma once
 #include <gnuradio/hip_buffer.hpp>
 #include <gnuradio/hip_fusion.hpp>
@@ -28,9 +32,12 @@ class scheduler_hip : public scheduler_mt
 {
 public:
     using sptr = std::shared_ptr<scheduler_hip>;
-    static sptr make(const std::string name = "hip", int device = 0, size_t fixed_buf_size = 64u << 20)
+    static sptr make(const std::string name = "hip", int device = 0, size_t fixed_buf_size = 64u << 20,
+                     bool fir_fusion = true)
     {
-        return std::make_shared<scheduler_hip>(name, device, fixed_buf_size);
+        auto s = std::make_shared<scheduler_hip>(name, device, fixed_buf_size);
+        s->set_fir_fusion(fir_fusion);
+        return s;
     }
     scheduler_hip(const std::string name = "hip", int device = 0, size_t fixed_buf_size = 64u << 20);
     ~scheduler_hip() override;
