@@ -13,8 +13,15 @@ CXXFLAGS := -O3 -std=c++17 -fPIC -Wall -Wextra -Wno-unused-parameter -pthread \
             -Iinclude -Inewsched_amd/runtime/include -Inewsched_amd/schedulers/include \
             -Inewsched_amd/blocklib/include
 
+# LEGACY=1 adds the superseded FIR matrix-core kernels (k_fir_mfma2/5/7/9, k_fir_casc2: A/B runs
+# and their parity tests, pytest marker `legacy`); the default library leaves them out
+LEGACY   ?= 0
 HIP_SRC  := $(wildcard newsched_amd/csrc/*.hip)
+ifeq ($(LEGACY),1)
+HIP_SRC  += newsched_amd/csrc/legacy/nsh_fir_legacy.hip
+endif
 HIP_OBJ  := $(patsubst newsched_amd/csrc/%.hip,$(OBJDIR)/hip/%.o,$(HIP_SRC))
+LEGACY_STAMP := $(OBJDIR)/legacy_$(LEGACY).stamp
 RT_SRC   := $(wildcard newsched_amd/runtime/lib/*.cpp) $(wildcard newsched_amd/schedulers/lib/*.cpp) \
             $(wildcard newsched_amd/blocklib/lib/*.cpp) $(wildcard newsched_amd/capi/*.cpp)
 RT_OBJ   := $(patsubst newsched_amd/%.cpp,$(OBJDIR)/rt/%.o,$(RT_SRC))
@@ -36,9 +43,15 @@ $(OBJDIR)/hip/%.o: newsched_amd/csrc/%.hip $(wildcard newsched_amd/csrc/*.hpp) i
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIBDIR)/libnsh_hip.so: $(HIP_OBJ)
+# relink when LEGACY changes (the object list shrinks without any object getting newer)
+$(LEGACY_STAMP):
+	@mkdir -p $(OBJDIR)
+	@rm -f $(OBJDIR)/legacy_*.stamp
+	@touch $@
+
+$(LIBDIR)/libnsh_hip.so: $(HIP_OBJ) $(LEGACY_STAMP)
 	@mkdir -p $(LIBDIR)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(HIP_OBJ)
 
 $(OBJDIR)/rt/%.o: newsched_amd/%.cpp $(RT_HDR) include/nsh_hip.h
 	@mkdir -p $(dir $@)

@@ -150,6 +150,10 @@ enum nsh_fir_algo {
     NSH_FIR_PFFT = 6
 };
 int nsh_fir_plan_create(int dev, const float* taps_host, int ntaps, int decim, int algo, void** plan);
+/* 1 when this library was built with the superseded FIR kernels (make LEGACY=1): NSH_FIR_MFMA16,
+ * NSH_FIR_MFMA_BF16X3, the NSH_FIR_MFMA_VARIANT tuning variants and nsh_fir_cascade2_ccf; else 0,
+ * and those fail with "not built" (plan creation / the call). */
+int nsh_fir_legacy_available(void);
 int nsh_fir_plan_destroy(void* plan);
 int nsh_fir_plan_algo(void* plan);          /* the algorithm AUTO resolved to */
 const char* nsh_fir_plan_kernel(void* plan); /* the kernel nsh_fir_ccf launches, e.g. "k_fir_mfma12<5>" */

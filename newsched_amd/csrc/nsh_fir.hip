@@ -203,7 +203,8 @@ int nsh_fir_plan_create(int dev, const float* taps_host, int ntaps, int decim, i
     if (resolved == NSH_FIR_MFMA16 && !nsh_fir_mfma16_supported(p)) {
         (void)hipFree(p->taps_dev);
         delete p;
-        return nsh::fail_msg("nsh_fir_plan_create: MFMA16 form needs decim 1, finite taps and ntaps <= 145");
+        return nsh::fail_msg(nsh_fir_legacy_built() ? "nsh_fir_plan_create: MFMA16 form needs decim 1, finite taps and ntaps <= 145"
+                                                    : "nsh_fir_plan_create: MFMA16 is a legacy kernel, not built (make LEGACY=1)");
     }
     if (resolved == NSH_FIR_MFMA_F32) {
         const int rc = nsh_fir_f32_supported(p) ? nsh_fir_f32_prepare(p)
@@ -241,6 +242,8 @@ int nsh_fir_plan_create(int dev, const float* taps_host, int ntaps, int decim, i
     *plan = p;
     return 0;
 }
+
+int nsh_fir_legacy_available(void) { return nsh_fir_legacy_built() ? 1 : 0; }
 
 int nsh_fir_plan_destroy(void* plan)
 {

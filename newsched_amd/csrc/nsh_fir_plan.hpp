@@ -46,6 +46,12 @@ struct nsh_fir_plan {
 };
 
 std::string nsh_fir_mfma_kernel_name(const nsh_fir_plan* p);
+// legacy/nsh_fir_legacy.hip (make LEGACY=1) defines these; nsh_fir_mfma.hip has weak stubs
+bool nsh_fir_legacy_built();
+int nsh_fir_legacy_prepare(nsh_fir_plan* p);
+int nsh_fir_legacy_run(const nsh_fir_plan* p, const float2* in, const float2* hist_in, float2* hist_out, float2* out,
+                       int64_t n_out, hipStream_t s);
+std::string nsh_fir_legacy_kernel_name(const nsh_fir_plan* p);
 
 bool nsh_fir_mfma_supported(const nsh_fir_plan* p);
 bool nsh_fir_mfma16_supported(const nsh_fir_plan* p);

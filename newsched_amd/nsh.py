@@ -16,6 +16,8 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_DIR = os.path.join(_HERE, "lib")
 HIP_LIB = os.path.join(LIB_DIR, "libnsh_hip.so")
+# NSH_HIP_LIB: another build of the library (e.g. the `make LEGACY=1` one, for its legacy tests)
+HIP_LIB = os.environ.get("NSH_HIP_LIB") or HIP_LIB
 
 NSH_H2D, NSH_D2H, NSH_D2D, NSH_DEFAULT = 0, 1, 2, 3
 FIR_AUTO, FIR_DIRECT, FIR_MFMA, FIR_MFMA16, FIR_MFMA_BF16X3, FIR_MFMA_F32, FIR_PFFT = 0, 1, 2, 3, 4, 5, 6
@@ -60,6 +62,7 @@ SIGNATURES = {
     "nsh_mul_const_vcc": (_i, [_vp, _vp, _vp, _i, _i64, _vp]),
     "nsh_synth_cf32": (_i, [_vp, _i64, _u64, _u64, _vp]),
     "nsh_fir_plan_create": (_i, [_i, C.POINTER(_f), _i, _i, _i, C.POINTER(_vp)]),
+    "nsh_fir_legacy_available": (_i, []),
     "nsh_fir_plan_destroy": (_i, [_vp]),
     "nsh_fir_plan_algo": (_i, [_vp]),
     "nsh_fir_plan_kernel": (C.c_char_p, [_vp]),
@@ -164,6 +167,11 @@ def fft1024(x, y, nframes: int, inverse: bool = False, stream=None):
 def channelizer1024(x, y, w, nframes: int, stream=None):
     check(lib().nsh_channelizer1024(ptr(x), ptr(y), ptr(w), nframes, stream_ptr(stream)),
           "nsh_channelizer1024")
+
+
+def fir_legacy_available() -> bool:
+    """True when libnsh_hip.so was built with the superseded FIR kernels (make LEGACY=1)."""
+    return lib().nsh_fir_legacy_available() == 1
 
 
 class FirPlan:

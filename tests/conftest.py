@@ -13,6 +13,25 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs on the GPU box via gpurun)")
+    config.addinivalue_line("markers", "legacy: exercises a superseded FIR kernel (libnsh_hip.so built with "
+                            "make LEGACY=1); skipped when the library was built without them")
+
+
+def _legacy_built():
+    try:
+        from newsched_amd import nsh
+
+        return nsh.fir_legacy_available()
+    except Exception:
+        return False
+
+
+def pytest_collection_modifyitems(config, items):
+    if any(it.get_closest_marker("legacy") for it in items) and not _legacy_built():
+        skip = pytest.mark.skip(reason="legacy FIR kernels not built (make LEGACY=1)")
+        for it in items:
+            if it.get_closest_marker("legacy"):
+                it.add_marker(skip)
 
 
 @pytest.fixture(scope="session")

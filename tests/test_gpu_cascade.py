@@ -10,7 +10,7 @@ import pytest
 from oracle import oracle as orc
 from newsched_amd import nsh
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.legacy]  # k_fir_casc2: make LEGACY=1
 
 
 def _firwin(n, cutoff):

@@ -131,8 +131,11 @@ def test_mul_const_vcc_bitexact(torch_cuda, vlen, nitems):
 
 # "mfma" is the default matrix-core kernel (decim 1: per-chunk scaled fp16x2, k_fir_mfma12),
 # "mfma_x3" forces the bf16x3 six-product kernel (k_fir_mfma2), "mfma16" the 16-sample form.
-ALGOS = [("direct", nsh.FIR_DIRECT), ("mfma", nsh.FIR_MFMA), ("mfma_v9", nsh.FIR_MFMA),
-         ("mfma_x3", nsh.FIR_MFMA_BF16X3), ("mfma16", nsh.FIR_MFMA16), ("mfma_f32", nsh.FIR_MFMA_F32)]
+# (k_fir_mfma9 / 2 / 5 are legacy kernels: built only with make LEGACY=1, marker `legacy`)
+ALGOS = [("direct", nsh.FIR_DIRECT), ("mfma", nsh.FIR_MFMA),
+         pytest.param("mfma_v9", nsh.FIR_MFMA, marks=pytest.mark.legacy),
+         pytest.param("mfma_x3", nsh.FIR_MFMA_BF16X3, marks=pytest.mark.legacy),
+         pytest.param("mfma16", nsh.FIR_MFMA16, marks=pytest.mark.legacy), ("mfma_f32", nsh.FIR_MFMA_F32)]
 MAX_TAPS = {"direct": 4096, "mfma": 161, "mfma_v9": 161, "mfma_x3": 161, "mfma16": 145, "mfma_f32": 257}
 VARIANT = {"mfma_v9": "9"}  # name -> NSH_FIR_MFMA_VARIANT for tuning variants under test
 
@@ -236,7 +239,7 @@ def test_fir_decim_vs_oracle(torch_cuda, decim):
         np.testing.assert_array_equal(hout, h_ref)
 
 
-@pytest.fixture(params=["v11", "v7"])
+@pytest.fixture(params=["v11", pytest.param("v7", marks=pytest.mark.legacy)])
 def dec_form(request, monkeypatch):
     """Both polyphase MFMA kernels: k_fir_mfma11 (default: fp16x2, per-chunk scale, exact
     path) and k_fir_mfma7 (bf16x3 six products; NSH_FIR_MFMA_VARIANT=7)."""
@@ -398,7 +401,7 @@ def _assert_nonfinite_pattern(y, ref):
     np.testing.assert_array_equal(np.sign(y.imag[inf]), np.sign(ref.imag[inf]))
 
 
-@pytest.fixture(params=["v12", "v9"])
+@pytest.fixture(params=["v12", pytest.param("v9", marks=pytest.mark.legacy)])
 def v8_form(request, monkeypatch):
     """The fp16x2 kernels: k_fir_mfma12 (default: one chunk per workgroup) and k_fir_mfma9
     (contiguous per-workgroup ranges, NSH_FIR_MFMA_VARIANT=9)."""
@@ -533,13 +536,29 @@ def test_fir_plan_kernels():
     h = _firwin127()
     assert nsh.FirPlan(h, 1, nsh.FIR_MFMA).kernel == "k_fir_mfma12<5>"
     assert nsh.FirPlan(h, 1, nsh.FIR_AUTO).kernel == "k_fir_mfma12<5>"
-    assert nsh.FirPlan(h, 1, nsh.FIR_MFMA_BF16X3).kernel == "k_fir_mfma2<5,2>"
-    assert nsh.FirPlan(h, 1, nsh.FIR_MFMA16).kernel == "k_fir_mfma5<9,1>"
     assert nsh.FirPlan(h, 1, nsh.FIR_DIRECT).kernel == "k_fir_direct<1,8>"
     assert nsh.FirPlan(h, 2, nsh.FIR_MFMA).kernel == "k_fir_mfma11<2,5>"
     assert nsh.FirPlan(h, 4, nsh.FIR_MFMA).kernel == "k_fir_mfma11<4,3>"
     for L in (1, 17, 33, 65, 97, 129, 161):
         assert nsh.FirPlan(np.ones(L, np.float32), 1, nsh.FIR_MFMA).kernel == "k_fir_mfma12<%d>" % ((L + 30) // 32 + 1)
+
+
+@pytest.mark.legacy
+def test_fir_plan_kernels_legacy():
+    h = _firwin127()
+    assert nsh.FirPlan(h, 1, nsh.FIR_MFMA_BF16X3).kernel == "k_fir_mfma2<5,2>"
+    assert nsh.FirPlan(h, 1, nsh.FIR_MFMA16).kernel == "k_fir_mfma5<9,1>"
+
+
+def test_fir_legacy_algorithms_fail_loudly_when_not_built():
+    """Without make LEGACY=1 the superseded forms are refused at plan creation, never silently
+    replaced by another kernel."""
+    if nsh.fir_legacy_available():
+        pytest.skip("legacy kernels built")
+    h = _firwin127()
+    for algo in (nsh.FIR_MFMA_BF16X3, nsh.FIR_MFMA16):
+        with pytest.raises(nsh.NshError, match="legacy"):
+            nsh.FirPlan(h, 1, algo)
 
 
 def test_fft_golden(torch_cuda, golden):
