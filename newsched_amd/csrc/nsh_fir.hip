@@ -81,13 +81,17 @@ __global__ __launch_bounds__(kThreads) void k_fir_direct(const float2* __restric
         const int s = base + o;
         w[o] = xs[s + s / PAD];
     }
+    // The last block's padded taps (k >= L) are skipped, not multiplied: 0 x inf / NaN would
+    // put a NaN where the L-tap sum has none (a sample L or more back is outside the window).
     const int nkb = Lp / 8;
     for (int kb = 0; kb < nkb; ++kb) {
+        const int jn = kb + 1 < nkb ? 8 : L - 8 * kb; // uniform
         float h[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) h[j] = taps[8 * kb + j];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
+            if (j >= jn) break;
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const float2 x = w[r * D + 7 - j];
@@ -255,6 +259,7 @@ int nsh_fir_plan_destroy(void* plan)
     if (p->frag8_dev) (void)hipFree(p->frag8_dev);
     if (p->frag12_dev) (void)hipFree(p->frag12_dev);
     if (p->tf32_dev) (void)hipFree(p->tf32_dev);
+    if (p->tf32q_dev) (void)hipFree(p->tf32q_dev);
     if (p->fragd_dev) (void)hipFree(p->fragd_dev);
     if (p->fragd8_dev) (void)hipFree(p->fragd8_dev);
     if (p->casc) nsh_fir_cascade_plan_destroy(p->casc);

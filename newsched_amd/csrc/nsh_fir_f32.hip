@@ -33,31 +33,24 @@
 #include <utility>
 #include <vector>
 
+#include "nsh_fir_f32_tile.hpp"
 #include "nsh_fir_plan.hpp"
 
 namespace {
 
-typedef float f32x4 __attribute__((ext_vector_type(4)));
+using nsh_f32t::f32x4;
 typedef float nf4 __attribute__((ext_vector_type(4)));
 using nsh::AUX_NT;
 
 template <int QF>
-struct geomf32 {
+struct geomf32 : nsh_f32t::geom<QF - 1, QF> {
+    using T = nsh_f32t::geom<QF - 1, QF>;
     static constexpr int NT = 256;
-    static constexpr int CHUNK = 2048;
-    static constexpr int H = 16 * (QF - 1);                       // halo samples
-    static constexpr int HP = H / 2;                              // halo sample pairs
-    static constexpr int NR = (CHUNK + H) / 16;                   // sample rows
-    static constexpr int PLANE = (NR * 80 + 255) / 256 * 256 + 128; // re plane, then im at 128 mod 256
-    static constexpr int BUF = 2 * PLANE;
-    static constexpr int TWF = 16 * QF + 16;                      // floats per tap copy
-    static constexpr int COPYF = ((4 * TWF + 191) / 256) * 256 + 64; // bytes, = 64 mod 256
-    static constexpr int TAPS = 4 * COPYF;
-    static constexpr int IMG_UNITS = TWF;                         // 16-B units of the host image [4][TWF]
-    static constexpr int SLOTS = BUF + TAPS;                      // u32 max[4]
+    static constexpr int HP = T::H / 2;                           // halo sample pairs
+    static constexpr int BUF = 2 * T::PLANE;
+    static constexpr int SLOTS = T::BYTES;                        // u32 max[4]
     static constexpr int LDS = SLOTS + 16;
-    static_assert(COPYF >= 4 * TWF && COPYF % 256 == 64, "tap copy pitch");
-    static_assert(HP <= NT && IMG_UNITS <= 2 * NT, "one halo pair / two image units per thread");
+    static_assert(HP <= NT && T::IMG_UNITS <= 2 * NT, "one halo pair / two image units per thread");
 };
 
 // wave-wide max, uniform: DPP within rows, readlane across them (as nsh_fir_mfma.hip)
@@ -92,7 +85,6 @@ __global__ __launch_bounds__(256) void k_fir_f32mfma(const float2* __restrict__ 
 {
     using G = geomf32<QF>;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    unsigned char* tl = lds + G::BUF;
     unsigned* slot = reinterpret_cast<unsigned*>(lds + G::SLOTS);
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -130,26 +122,13 @@ __global__ __launch_bounds__(256) void k_fir_f32mfma(const float2* __restrict__ 
         }
     }
     float4 ti[2];
-    {
-        const __amdgpu_buffer_rsrc_t tr = __builtin_amdgcn_make_buffer_rsrc((void*)timg, (short)0, G::IMG_UNITS * 16, 0x00020000);
-#pragma unroll
-        for (int k = 0; k < 2; ++k) ti[k] = nsh::buf_load_f4(tr, 16 * (tid + G::NT * k));
-    }
+    nsh_f32t::load_taps<G>(timg, ti, tid, G::NT);
 
-    // samples -> re / im planes (local sample s = halo first): pair (s, s+1) is one float2 per plane
-    auto put = [&](const float4& x, int s) {
-        const int off = (s >> 4) * 80 + (s & 15) * 4;
-        *reinterpret_cast<float2*>(lds + off) = make_float2(x.x, x.z);
-        *reinterpret_cast<float2*>(lds + G::PLANE + off) = make_float2(x.y, x.w);
-    };
-    if (tid < G::HP) put(hv, 2 * tid);
+    // samples -> re / im planes (local sample s = halo first), the tap image -> its copies
+    if (tid < G::HP) nsh_f32t::put<G>(lds, hv, 2 * tid);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) put(v[u], G::H + 2 * (tid + G::NT * u));
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        const int u = tid + G::NT * k;
-        if (u < G::IMG_UNITS) *reinterpret_cast<float4*>(tl + (u / (G::TWF / 4)) * G::COPYF + 16 * (u % (G::TWF / 4))) = ti[k];
-    }
+    for (int u = 0; u < 4; ++u) nsh_f32t::put<G>(lds, v[u], G::H + 2 * (tid + G::NT * u));
+    nsh_f32t::put_taps<G>(lds, ti, tid, G::NT);
     {
         unsigned m = max_mag4(hv);
 #pragma unroll
@@ -160,29 +139,12 @@ __global__ __launch_bounds__(256) void k_fir_f32mfma(const float2* __restrict__ 
     nsh::lds_barrier();
     const bool exact = max(max(slot[0], slot[1]), max(slot[2], slot[3])) >= 0x7f800000u; // inf / NaN in range
 
-    const int i = lane & 15; // A row (b, c) = (i >> 1, i & 1); B / C column = phase
-    const int g = lane >> 4;
-    f32x4 acc[4] = {};
+    f32x4 acc[4];
     if (!exact) {
-        const int b = i >> 1, c = i & 1;
-        const unsigned char* pa = lds + c * G::PLANE + (G::H / 16 + 32 * wave + b) * 80 + 16 * g;
-        const int mb = 16 * QF - 1 - i + 4 * g; // m0 at q = 0
-#pragma unroll
-        for (int q = 0; q < QF; ++q) {
-            const int m0 = mb - 16 * q;
-            const f32x4 B4 = *reinterpret_cast<const f32x4*>(tl + (m0 & 3) * G::COPYF + 4 * (m0 & ~3));
-            f32x4 A4[4];
-#pragma unroll
-            for (int t = 0; t < 4; ++t) A4[t] = *reinterpret_cast<const f32x4*>(pa + (8 * t - q) * 80);
-            // the four tiles' accumulators in turn: no MFMA waits on the one before it (40-cycle
-            // dependent latency vs 32-cycle issue)
-#pragma unroll
-            for (int s = 0; s < 4; ++s)
-#pragma unroll
-                for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(A4[t][s], B4[s], acc[t], 0, 0, 0);
-        }
+        nsh_f32t::tile<G, QF>(lds, wave, lane, acc);
     } else {
         // fp32 direct form (taps in order, fmaf) for the lane's 8 outputs, from the planes
+        const int i = lane & 15, g = lane >> 4;
 #pragma unroll
         for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -199,12 +161,7 @@ __global__ __launch_bounds__(256) void k_fir_f32mfma(const float2* __restrict__ 
                 acc[t][2 * u + 1] = im;
             }
     }
-    const __amdgpu_buffer_rsrc_t r = nsh::chunk_rsrc<2048>(out, ch, n_out);
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int u = 0; u < 2; ++u)
-            nsh::buf_store_f2(r, (16 * (32 * wave + 8 * t + 2 * g + u) + i) * 8, nsh::buf_f2{ acc[t][2 * u], acc[t][2 * u + 1] });
+    nsh_f32t::store(nsh::chunk_rsrc<2048>(out, ch, n_out), acc, wave, lane);
     if (ch == 0) // the last L-1 inputs for the next call
         for (int j = tid; j < L - 1; j += G::NT) {
             const int64_t gi = n_in - (L - 1) + j;

@@ -1,0 +1,102 @@
+// The exact-fp32 Toeplitz tile on v_mfma_f32_16x16x4_f32, shared by k_fir_f32mfma (every chunk,
+// NSH_FIR_MFMA_F32; nsh_fir_f32.hip) and k_fir_mfma12 (the finite chunks whose dynamic range the
+// fp16x2 split cannot hold; nsh_fir_mfma.hip). Geometry and algorithm: see nsh_fir_f32.hip.
+//
+// A chunk's LDS image: re and im fp32 planes of 16-sample rows at an 80-B pitch, the im plane at
+// 128 mod 256 B (every 16-lane ds_read_b128 group of the A reads hits 16 distinct 16-B slots),
+// local sample s = halo first; then the reversed taps R[m] = h[16 QF - 1 - m] as 4 copies shifted
+// by 0..3 floats at a 64 mod 256 B pitch. Lane (i = lane & 15, g = lane >> 4) of wave w computes
+// outputs 16 (32 w + 8 t + 2 g + u) + i, t < 4, u < 2, as (acc[t][2u], acc[t][2u + 1]).
+#pragma once
+#include "nsh_common.hpp"
+
+namespace nsh_f32t {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// HR halo rows of 16 samples (HR >= QF - 1), QF tap blocks of 16
+template <int HR, int QF>
+struct geom {
+    static constexpr int CHUNK = 2048;
+    static constexpr int H = 16 * HR;                             // halo samples
+    static constexpr int NR = (CHUNK + H) / 16;                   // sample rows
+    static constexpr int PLANE = (NR * 80 + 255) / 256 * 256 + 128; // re plane, then im at 128 mod 256
+    static constexpr int TWF = 16 * QF + 16;                      // floats per tap copy
+    static constexpr int COPYF = ((4 * TWF + 191) / 256) * 256 + 64; // bytes, = 64 mod 256
+    static constexpr int TAPS = 4 * COPYF;
+    static constexpr int IMG_UNITS = TWF;                         // 16-B units of the host image [4][TWF]
+    static constexpr int BYTES = 2 * PLANE + TAPS;                // planes, then the tap copies
+    static_assert(COPYF >= 4 * TWF && COPYF % 256 == 64, "tap copy pitch");
+    static_assert(HR >= QF - 1, "halo rows cover the taps");
+};
+
+// samples x = (s, s + 1) (re, im, re, im) -> the planes
+template <class G>
+__device__ __forceinline__ void put(unsigned char* lds, const float4& x, int s)
+{
+    const int off = (s >> 4) * 80 + (s & 15) * 4;
+    *reinterpret_cast<float2*>(lds + off) = make_float2(x.x, x.z);
+    *reinterpret_cast<float2*>(lds + G::PLANE + off) = make_float2(x.y, x.w);
+}
+
+// the host tap image [4][TWF] floats (global, 16-B units; thread tid moves units tid, tid + nt)
+// -> the tap copies at lds + 2 PLANE
+template <class G>
+__device__ __forceinline__ void put_taps(unsigned char* lds, const float4 (&ti)[2], int tid, int nt)
+{
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int u = tid + nt * k;
+        if (u < G::IMG_UNITS)
+            *reinterpret_cast<float4*>(lds + 2 * G::PLANE + (u / (G::TWF / 4)) * G::COPYF + 16 * (u % (G::TWF / 4))) = ti[k];
+    }
+}
+
+template <class G>
+__device__ __forceinline__ void load_taps(const float4* __restrict__ timg, float4 (&ti)[2], int tid, int nt)
+{
+    const __amdgpu_buffer_rsrc_t tr = __builtin_amdgcn_make_buffer_rsrc((void*)timg, (short)0, G::IMG_UNITS * 16, 0x00020000);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) ti[k] = nsh::buf_load_f4(tr, 16 * (tid + nt * k));
+}
+
+// the lane's 8 outputs of wave w (see the header comment)
+template <class G, int QF>
+__device__ __forceinline__ void tile(const unsigned char* lds, int wave, int lane, f32x4 (&acc)[4])
+{
+    const int i = lane & 15; // A row (b, c) = (i >> 1, i & 1); B / C column = phase
+    const int g = lane >> 4;
+    const int b = i >> 1, c = i & 1;
+    const unsigned char* tl = lds + 2 * G::PLANE;
+    const unsigned char* pa = lds + c * G::PLANE + (G::H / 16 + 32 * wave + b) * 80 + 16 * g;
+    const int mb = 16 * QF - 1 - i + 4 * g; // m0 at q = 0
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] = f32x4{ 0.f, 0.f, 0.f, 0.f };
+#pragma unroll
+    for (int q = 0; q < QF; ++q) {
+        const int m0 = mb - 16 * q;
+        const f32x4 B4 = *reinterpret_cast<const f32x4*>(tl + (m0 & 3) * G::COPYF + 4 * (m0 & ~3));
+        f32x4 A4[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) A4[t] = *reinterpret_cast<const f32x4*>(pa + (8 * t - q) * 80);
+        // the four tiles' accumulators in turn: no MFMA waits on the one before it (40-cycle
+        // dependent latency vs 32-cycle issue)
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(A4[t][s], B4[s], acc[t], 0, 0, 0);
+    }
+}
+
+// the lane's outputs -> out (chunk resource r)
+__device__ __forceinline__ void store(__amdgpu_buffer_rsrc_t r, const f32x4 (&acc)[4], int wave, int lane)
+{
+    const int i = lane & 15, g = lane >> 4;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+            nsh::buf_store_f2(r, (16 * (32 * wave + 8 * t + 2 * g + u) + i) * 8, nsh::buf_f2{ acc[t][2 * u], acc[t][2 * u + 1] });
+}
+
+} // namespace nsh_f32t

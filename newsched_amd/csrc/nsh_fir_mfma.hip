@@ -22,6 +22,7 @@
 // compiled only by `make LEGACY=1` (their algorithms / variants report "not built" otherwise;
 // tests marked `legacy`). DESIGN.md section 4 keeps their measurements.
 #include "nsh_fir_mfma_shared.hpp"
+#include "nsh_fir_f32_tile.hpp"
 
 #include <algorithm>
 #include <cmath>
@@ -66,6 +67,9 @@ namespace {
 // bit-identical, 718.0 vs 721.2 us (profiles/r02u_*).
 #ifndef NSH_V12_ROT
 #define NSH_V12_ROT 1
+#endif
+#ifndef NSH_V12_F32T
+#define NSH_V12_F32T 1 // probe builds: 0 = finite wide-range chunks on the fp32 direct form
 #endif
 #ifndef NSH_V12_LDS_PAD
 #define NSH_V12_LDS_PAD 0 // probe builds: extra LDS per workgroup (fewer resident workgroups per CU)
@@ -134,12 +138,23 @@ __device__ __forceinline__ void store_pair12(const float4& v, unsigned char* buf
     *reinterpret_cast<unsigned*>(buf + 3 * G::PLANE + off) = il;
 }
 
+// A chunk whose samples are finite but span more than the fp16x2 split holds: the exact-fp32
+// matrix tile of k_fir_f32mfma (nsh_fir_f32_tile.hpp: fp32 products and sums on
+// v_mfma_f32_16x16x4_f32, QF = 2Q - 1 tap blocks of 16 over the same 32 (Q - 1)-sample halo),
+// staged over the fp16 planes and tap image. Its outputs are bit-identical to k_fir_f32mfma's
+// wherever that kernel uses the same blocking. The three forms (split MFMA, exact-fp32 tile, fp32
+// direct form) share one staging step, one barrier and one store loop, each under a
+// workgroup-uniform branch: no value of one form is live in another's registers.
+template <int Q>
+using geom12f = nsh_f32t::geom<2 * Q - 2, 2 * Q - 1>;
+
 template <int Q>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k_fir_mfma12(const float2* __restrict__ in,
                                                     const float2* __restrict__ hist_in,
                                                     float2* __restrict__ hist_out,
                                                     float2* __restrict__ out,
                                                     const uint4* __restrict__ timg, // [2][8][TW/8]
+                                                    const float4* __restrict__ timg32, // exact-fp32 tile taps [4][TWF]
                                                     const float* __restrict__ taps,
                                                     int L,
                                                     int sh,
@@ -234,24 +249,46 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
             }
         }
         nsh::lds_barrier(); // also: every wave is done with the previous chunk's planes
-        const unsigned m = max(max(slot_max[0], slot_max[1]), max(slot_max[2], slot_max[3]));
-        const unsigned z = min(min(slot_mnz[0], slot_mnz[1]), min(slot_mnz[2], slot_mnz[3]));
+        // workgroup-uniform, and made provably so (SGPRs): the branches on it are then scalar
+        // branches, not exec-masked regions the compiler lays out one after the other (with the
+        // values of a later region live through the earlier one)
+        const unsigned m = __builtin_amdgcn_readfirstlane(max(max(slot_max[0], slot_max[1]), max(slot_max[2], slot_max[3])));
+        const unsigned z = __builtin_amdgcn_readfirstlane(min(min(slot_mnz[0], slot_mnz[1]), min(slot_mnz[2], slot_mnz[3])));
         const int s = scale_of(m);
         const bool exact = chunk_needs_exact(m, z, s);
-        if (exact) {
+        const bool f32t = NSH_V12_F32T && exact && m < 0x7f800000u; // finite: the exact-fp32 tile
+        using GF = geom12f<Q>;
+        static_assert(GF::H == G::H && GF::BYTES <= G::SLOTS, "the fp32 tile's image fits the planes + tap image");
+        if (__builtin_expect(!exact, 1)) {
+            if (tid < G::HP) store_pair12<Q>(hv, lds, 2 * tid, s);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) store_pair12<Q>(v[u], lds, G::H + 2 * (tid + G::NT * u), s);
+        } else if (f32t) {
+            float4 t32[2];
+            nsh_f32t::load_taps<GF>(timg32, t32, tid, G::NT);
+            if (tid < G::HP) nsh_f32t::put<GF>(lds, hv, 2 * tid);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) nsh_f32t::put<GF>(lds, v[u], G::H + 2 * (tid + G::NT * u));
+            nsh_f32t::put_taps<GF>(lds, t32, tid, G::NT);
+        } else { // inf / NaN in range: the fp32 direct form (exact IEEE semantics)
             float4* r = reinterpret_cast<float4*>(lds);
             if (tid < G::HP) r[tid] = hv;
 #pragma unroll
             for (int u = 0; u < 4; ++u) r[G::HP + tid + G::NT * u] = v[u];
-        } else {
-            if (tid < G::HP) store_pair12<Q>(hv, lds, 2 * tid, s);
-#pragma unroll
-            for (int u = 0; u < 4; ++u) store_pair12<Q>(v[u], lds, G::H + 2 * (tid + G::NT * u), s);
         }
         nsh::lds_barrier();
         nf2 o[8];
-        if (exact) {
-            direct_tile9<Q>(lds, taps, L, wave, h, phase, o);
+        if (__builtin_expect(exact, 0)) {
+            if (f32t) {
+                nsh_f32t::f32x4 acc[4];
+                nsh_f32t::tile<GF, 2 * Q - 1>(lds, wave, lane, acc);
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) o[2 * t + u] = nf2{ acc[t][2 * u], acc[t][2 * u + 1] };
+            } else {
+                direct_tile9<Q>(lds, taps, L, wave, h, phase, o);
+            }
         } else {
             const int b = rho & 15, c = rho >> 4;
             const int row0 = (Q - 1) + 16 * wave + b; // A rows: row0 - (st >> 1); chunks h + 2 (st & 1)
@@ -305,9 +342,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
             }
         }
         const __amdgpu_buffer_rsrc_t r = chunk_rsrc<2048>(out, ch, n_out);
-        const int base = wave * TILE + phase;
+        // one store loop for both lane maps: a lane base (one v_cndmask) plus a per-register
+        // constant chosen in SGPRs (soffset). Two loops under the branch ended in a join whose
+        // conservative s_waitcnt vmcnt(0) held every workgroup until its stores had landed.
+        // split / direct: output wave TILE + phase + 32 ((reg & 3) + 8 (reg >> 2) + 4 h);
+        // exact-fp32 tile: output 16 (32 wave + 8 t + 2 g + u) + i of o[2 t + u] (nsh_f32t::tile)
+        const int lb = f32t ? (16 * (32 * wave + 2 * (lane >> 4)) + (lane & 15)) * 8 : (wave * TILE + phase + 128 * h) * 8;
 #pragma unroll
-        for (int reg = 0; reg < 8; ++reg) buf_store_f2(r, (base + 32 * ((reg & 3) + 8 * (reg >> 2) + 4 * h)) * 8, o[reg]);
+        for (int reg = 0; reg < 8; ++reg) {
+            const int c = f32t ? 128 * (4 * reg - 3 * (reg & 1)) : 256 * ((reg & 3) + 8 * (reg >> 2));
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(nsh::u32x2, o[reg]), r, lb, c, nsh::AUX_NT);
+        }
     };
     process(c_first, va, ha);
     if (c_first == 0) // the last L-1 inputs for the next call (after this workgroup's stores)
@@ -640,7 +685,8 @@ int launch_v12(const nsh_fir_plan* p, const float2* in, const float2* hin, float
     const int64_t grid = per_x * 8;
     if (grid > 0x7fffffff) return nsh::fail_msg("nsh_fir_ccf(mfma v12): stream too long for one launch");
     hipLaunchKernelGGL((k_fir_mfma12<Q>), dim3((unsigned)grid), dim3(G::NT), G::LDS, s, in, hin, hout, out,
-                       (const uint4*)p->frag12_dev, (const float*)p->taps_dev, p->L, p->sh8, n_out, per_x);
+                       (const uint4*)p->frag12_dev, (const float4*)p->tf32q_dev, (const float*)p->taps_dev, p->L, p->sh8,
+                       n_out, per_x);
     NSH_CK_LAUNCH("nsh_fir_ccf(mfma fp16x2 v12)");
     return 0;
 }
@@ -783,6 +829,19 @@ int nsh_fir_mfma_prepare(nsh_fir_plan* p)
                 }
             NSH_CK(hipMalloc(&p->frag12_dev, f12.size() * sizeof(_Float16)));
             NSH_CK(hipMemcpy(p->frag12_dev, f12.data(), f12.size() * sizeof(_Float16), hipMemcpyHostToDevice));
+    }
+    {
+        // the exact-fp32 tile's taps (finite chunks the split cannot hold): R[m] = h[16 QF - 1 - m],
+        // QF = 2Q - 1 tap blocks of 16 (zero-padded past L), 4 copies shifted by 0..3 floats
+        const int QF = 2 * Q - 1, TWF = 16 * QF + 16, P = 16 * QF - 1;
+        std::vector<float> img((size_t)4 * TWF, 0.f);
+        for (int d = 0; d < 4; ++d)
+            for (int k = 0; k < TWF; ++k) {
+                const int t = P - (k + d);
+                img[(size_t)d * TWF + k] = (t >= 0 && t < p->L) ? p->taps_host[t] : 0.f;
+            }
+        NSH_CK(hipMalloc(&p->tf32q_dev, img.size() * sizeof(float)));
+        NSH_CK(hipMemcpy(p->tf32q_dev, img.data(), img.size() * sizeof(float), hipMemcpyHostToDevice));
     }
     return nsh_fir_legacy_prepare(p); // legacy builds: the bf16x3 / v9 / 16-sample fragments
 }

@@ -454,17 +454,25 @@ def test_fir_mfma_wide_dynamic_range(torch_cuda, v8_form):
 
 @pytest.mark.parametrize("decim", [1, 2, 4])
 @pytest.mark.parametrize("ntaps", [127, 64, 9])
-def test_fir_mfma_exact_path_bit_identical(torch_cuda, v8_form, ntaps, decim):
-    """A 2^40 spike in every 2048-sample chunk sends every chunk through the in-kernel fp32
-    direct form (direct_tile9 / direct_group, decim 1, 2, 4: taps in order k = 0..L-1, one fused multiply-add each). That is
-    the order k_fir_direct accumulates in, so the two kernels agree bit for bit on finite
-    inputs -- a check on the exact path's input reuse (each sample read once per four outputs)
-    that no tolerance could hide. Also within tolerance of the oracle."""
+@pytest.mark.parametrize("kind", ["spike", "nan"])
+def test_fir_mfma_exact_paths(torch_cuda, v8_form, ntaps, decim, kind):
+    """Every 2048-sample chunk outside the fp16x2 split's range.
+    'spike' (a finite 2^40 sample per chunk): k_fir_mfma12 (decim 1) computes such chunks with the
+    exact-fp32 matrix tile of k_fir_f32mfma (fp32 products and sums): bit-identical to the
+    NSH_FIR_MFMA_F32 kernel when both use the same tap blocking (QF = 2Q - 1: 127 and 64 taps),
+    and within tolerance of the oracle on each chunk's own scale. The decimators and the legacy
+    k_fir_mfma9 use the fp32 direct form there (taps in order k = 0..L-1, one fused multiply-add
+    each, the order k_fir_direct accumulates in): bit-identical to k_fir_direct.
+    'nan' (a NaN per chunk): every form computes such chunks with the fp32 direct form: the same
+    NaN positions as k_fir_direct and every finite output bit-identical to it."""
     torch = torch_cuda
     h = (np.hamming(ntaps) / (ntaps / 2)).astype(np.float32)
     n = 9 * 2048 + 333
     x = orc.synth(n, 5)
-    x[100::2048] *= np.float32(2.0 ** 40)
+    if kind == "spike":
+        x[100::2048] *= np.float32(2.0 ** 40)
+    else:
+        x[100::2048] = complex(np.nan, 0.5)
     if decim > 1 and v8_form == "v9":
         pytest.skip("decimators: one kernel form (k_fir_mfma11)")
     plan = nsh.FirPlan(h, decim, nsh.FIR_MFMA)
@@ -473,8 +481,20 @@ def test_fir_mfma_exact_path_bit_identical(torch_cuda, v8_form, ntaps, decim):
                                        2: "k_fir_mfma11", 4: "k_fir_mfma11"}[decim]), plan.kernel
     y, hy = run_fir(torch, plan, x, n // decim)
     yd, hd = run_fir(torch, nsh.FirPlan(h, decim, nsh.FIR_DIRECT), x, n // decim)
-    np.testing.assert_array_equal(y.view(np.uint32), yd.view(np.uint32))
     np.testing.assert_array_equal(hy.view(np.uint32), hd.view(np.uint32))
+    if kind == "nan":
+        nan = np.isnan(yd.real) | np.isnan(yd.imag)
+        np.testing.assert_array_equal(np.isnan(y.real) | np.isnan(y.imag), nan)
+        np.testing.assert_array_equal(y[~nan].view(np.uint32), yd[~nan].view(np.uint32))
+        return
+    if decim == 1 and v8_form == "v12":
+        pf = nsh.FirPlan(h, 1, nsh.FIR_MFMA_F32)
+        q12 = int(plan.kernel.split("<")[1].rstrip(">"))
+        if pf.kernel == "k_fir_f32mfma<%d>" % (2 * q12 - 1):
+            yf, _ = run_fir(torch, pf, x, n)
+            np.testing.assert_array_equal(y.view(np.uint32), yf.view(np.uint32))
+    else:
+        np.testing.assert_array_equal(y.view(np.uint32), yd.view(np.uint32))
     ref = orc.fir_ccf(x[: n // decim * decim], h, decim)
     c = 2048 // decim
     for a in range(0, n // decim, c):   # each chunk on its own scale

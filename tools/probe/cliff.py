@@ -1,6 +1,7 @@
-"""Exact-path cost of the default decim-1 FIR (k_fir_mfma12): a 2048-sample chunk holding a
-non-finite sample, or one whose range exceeds the split's (a 2^40 spike among ~1 values), is
-filtered by the fp32 direct form inside the same launch. Times 2^28-sample launches with every
+"""Exact-path cost of the default FIR kernels: in k_fir_mfma12 (decim 1) a 2048-sample chunk whose
+range exceeds the split's (a 2^40 spike among ~1 values) is filtered by the exact-fp32 matrix tile
+and one holding a non-finite sample by the fp32 direct form, inside the same launch (k_fir_mfma11,
+decim 2 / 4: the fp32 direct form for both). Times 2^28-sample launches with every
 k-th chunk poisoned (k = inf, 256, 64, 16, 4, 1), HIP events, >= 1 s warm-up per case, and
 checks a window around a poisoned chunk against the oracle.
 Usage: python tools/probe/cliff.py [--log2n 28] [--decim 1|2|4]"""
