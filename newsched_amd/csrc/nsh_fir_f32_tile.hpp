@@ -40,16 +40,20 @@ __device__ __forceinline__ void put(unsigned char* lds, const float4& x, int s)
 }
 
 // the host tap image [4][TWF] floats (global, 16-B units; thread tid moves units tid, tid + nt)
-// -> the tap copies at lds + 2 PLANE
+// -> the tap copies at tl (G::TAPS bytes; by default right after the planes, lds + 2 PLANE)
 template <class G>
-__device__ __forceinline__ void put_taps(unsigned char* lds, const float4 (&ti)[2], int tid, int nt)
+__device__ __forceinline__ void put_taps_at(unsigned char* tl, const float4 (&ti)[2], int tid, int nt)
 {
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
         const int u = tid + nt * k;
-        if (u < G::IMG_UNITS)
-            *reinterpret_cast<float4*>(lds + 2 * G::PLANE + (u / (G::TWF / 4)) * G::COPYF + 16 * (u % (G::TWF / 4))) = ti[k];
+        if (u < G::IMG_UNITS) *reinterpret_cast<float4*>(tl + (u / (G::TWF / 4)) * G::COPYF + 16 * (u % (G::TWF / 4))) = ti[k];
     }
+}
+template <class G>
+__device__ __forceinline__ void put_taps(unsigned char* lds, const float4 (&ti)[2], int tid, int nt)
+{
+    put_taps_at<G>(lds + 2 * G::PLANE, ti, tid, nt);
 }
 
 template <class G>
@@ -60,14 +64,13 @@ __device__ __forceinline__ void load_taps(const float4* __restrict__ timg, float
     for (int k = 0; k < 2; ++k) ti[k] = nsh::buf_load_f4(tr, 16 * (tid + nt * k));
 }
 
-// the lane's 8 outputs of wave w (see the header comment)
+// the lane's 8 outputs of wave w (see the header comment); planes at lds, tap copies at tl
 template <class G, int QF>
-__device__ __forceinline__ void tile(const unsigned char* lds, int wave, int lane, f32x4 (&acc)[4])
+__device__ __forceinline__ void tile_at(const unsigned char* lds, const unsigned char* tl, int wave, int lane, f32x4 (&acc)[4])
 {
     const int i = lane & 15; // A row (b, c) = (i >> 1, i & 1); B / C column = phase
     const int g = lane >> 4;
     const int b = i >> 1, c = i & 1;
-    const unsigned char* tl = lds + 2 * G::PLANE;
     const unsigned char* pa = lds + c * G::PLANE + (G::H / 16 + 32 * wave + b) * 80 + 16 * g;
     const int mb = 16 * QF - 1 - i + 4 * g; // m0 at q = 0
 #pragma unroll
@@ -86,6 +89,12 @@ __device__ __forceinline__ void tile(const unsigned char* lds, int wave, int lan
 #pragma unroll
             for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(A4[t][s], B4[s], acc[t], 0, 0, 0);
     }
+}
+
+template <class G, int QF>
+__device__ __forceinline__ void tile(const unsigned char* lds, int wave, int lane, f32x4 (&acc)[4])
+{
+    tile_at<G, QF>(lds, lds + 2 * G::PLANE, wave, lane, acc);
 }
 
 // the lane's outputs -> out (chunk resource r)

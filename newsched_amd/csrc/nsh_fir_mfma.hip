@@ -359,22 +359,47 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
         for (int j = tid; j < L - 1; j += G::NT) hist_out[j] = virt(in, hist_in, n_in - (L - 1) + j, n_in, L);
 }
 
+// k_fir_mfma11's LDS with the exact-fp32 tile: a finite chunk whose range the split cannot hold is
+// filtered as if undecimated by k_fir_f32mfma's tile (nsh_fir_f32_tile.hpp, QF = HR + 1 tap blocks
+// of 16 over the chunk's D H-sample halo) and every D-th output kept -- the same fp32 matrix work per
+// input sample as at decim 1, no polyphase form. Each plane buffer grows to hold the tile's two fp32
+// planes; the tile's taps (one copy, loaded once per workgroup) and a per-wave output scratch (the
+// tile's lane map -> the split path's, for the common store) follow the stash. LDS stays within 2
+// resident workgroups per CU (the kernel's occupancy).
+template <int D, int QH>
+struct geom11x : geom11<D, QH> {
+    using B = geom11<D, QH>;
+    static constexpr int HRF = D * (QH - 1);                     // tile halo rows (16 samples)
+    static constexpr int QF = HRF + 1;
+    using GF = nsh_f32t::geom<HRF, QF>;
+    static constexpr int BUF = (B::BUF > 2 * GF::PLANE ? B::BUF : 2 * GF::PLANE);
+    static constexpr int STASH_AT = 2 * BUF;
+    static constexpr int TAPF = STASH_AT + 2 * B::STASH;          // tile taps
+    static constexpr int SCR = TAPF + (GF::TAPS + 255) / 256 * 256; // [4 waves][WAVE_OUT] float2
+    static constexpr int SLOTS = SCR + 4 * B::WAVE_OUT * 8;
+    static constexpr int LDS = SLOTS + 64;
+    static_assert(GF::H == D * B::H && BUF % 256 == 0, "tile halo = the chunk's halo");
+    static_assert(2 * LDS <= 160 * 1024, "2 workgroups per CU");
+};
+
 template <int D, int QH>
 __global__ __launch_bounds__(256, 2) void k_fir_mfma11(const float2* __restrict__ in,
                                                       const float2* __restrict__ hist_in,
                                                       float2* __restrict__ hist_out,
                                                       float2* __restrict__ out,
                                                       const _Float16* __restrict__ frag, // per phase: [2][KS][64] x8, [2][64] x4
+                                                      const float4* __restrict__ timg32, // tile taps [4][TWF]
                                                       const float* __restrict__ taps,
                                                       int L,
                                                       int sh,
                                                       int64_t n_out)
 {
-    using G = geom11<D, QH>;
+    using G = geom11x<D, QH>;
+    using GF = typename G::GF;
     constexpr int KS = G::KS;
     typedef float f32x4 __attribute__((ext_vector_type(4)));
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    float4* stash = reinterpret_cast<float4*>(lds + 2 * G::BUF); // [2][HP] raw halo sources
+    float4* stash = reinterpret_cast<float4*>(lds + G::STASH_AT); // [2][HP] raw halo sources
     unsigned* slot_max = reinterpret_cast<unsigned*>(lds + G::SLOTS);
     unsigned* slot_mnz = slot_max + 8;
 
@@ -382,6 +407,11 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma11(const float2* __restrict_
     const int lane = tid & 63;
     const int wave = tid >> 6;
     const int64_t n_in = n_out * D;
+    {   // the tile's taps, once per workgroup (read after the prologue's barriers)
+        float4 t32[2];
+        nsh_f32t::load_taps<GF>(timg32, t32, tid, G::NT);
+        nsh_f32t::put_taps_at<GF>(lds + G::TAPF, t32, tid, G::NT);
+    }
 
     if (blockIdx.x == 0) {
         for (int j = tid; j < L - 1; j += G::NT) hist_out[j] = virt(in, hist_in, n_in - (L - 1) + j, n_in, L);
@@ -432,7 +462,15 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma11(const float2* __restrict_
         }
     };
     // chunk -> buffer: raw fp32 (halo float4 [0, HP), chunk float4 HP + j) or split phase planes
-    auto put_chunk = [&](unsigned char* buf, const float4* hsrc, const float4 (&v)[4], bool raw, int sc) {
+    auto put_chunk = [&](unsigned char* buf, const float4* hsrc, const float4 (&v)[4], bool raw, bool f32t, int sc) {
+        if (__builtin_expect(f32t, 0)) { // the tile's fp32 planes (16-sample rows), halo first
+            if (tid < G::HP) nsh_f32t::put<GF>(buf, hsrc[tid], 2 * tid);
+#pragma unroll
+            for (int u = 0; u < G::UNITS; ++u)
+#pragma unroll
+                for (int f = 0; f < D; ++f) nsh_f32t::put<GF>(buf, v[u * D + f], GF::H + 2 * ((tid + G::NT * u) * D + f));
+            return;
+        }
         if (raw) {
             float4* rb = reinterpret_cast<float4*>(buf);
             if (tid < G::HP) rb[tid] = hsrc[tid];
@@ -555,6 +593,26 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma11(const float2* __restrict_
             }
         }
     };
+    // the tile's outputs n = 16 (32 wave + 8 t + 2 g + u) + i (undecimated), the lanes with
+    // i mod D = 0 keeping theirs (m = n / D), through the wave's LDS scratch into the split
+    // path's lane map (the wave's own outputs: a wave barrier, no workgroup barrier)
+    auto f32_tile = [&](const unsigned char* cur, nf2 (&o)[2 * G::TILES]) {
+        f32x4 acc[4];
+        nsh_f32t::tile_at<GF, G::QF>(cur, lds + G::TAPF, wave, lane, acc);
+        nf2* scr = reinterpret_cast<nf2*>(lds + G::SCR) + wave * G::WAVE_OUT;
+        const int i = lane & 15;
+        if (i % D == 0) {
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+#pragma unroll
+                for (int u = 0; u < 2; ++u) scr[(16 * (8 * t + 2 * g + u) + i) / D] = nf2{ acc[t][2 * u], acc[t][2 * u + 1] };
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int oi = 0; oi < 2 * G::TILES; ++oi) o[oi] = scr[((oi >> 1) * 8 + 2 * g + (oi & 1)) * 16 + phase];
+    };
     auto store_tile = [&](int64_t ch, const nf2 (&o)[2 * G::TILES]) {
         const __amdgpu_buffer_rsrc_t r = chunk_rsrc<G::CHUNK>(out, ch, n_out);
 #pragma unroll
@@ -588,7 +646,8 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma11(const float2* __restrict_
     unsigned z_prev = min(min(slot_mnz[0], slot_mnz[1]), min(slot_mnz[2], slot_mnz[3]));
     int s_cur = scale_of(m_prev);
     bool ex_cur = chunk_needs_exact(m_prev, z_prev, s_cur);
-    put_chunk(lds, stash + G::HP, va, ex_cur, s_cur);
+    bool f32_cur = ex_cur && m_prev < 0x7f800000u; // finite: the exact-fp32 tile
+    put_chunk(lds, stash + G::HP, va, ex_cur, f32_cur, s_cur);
     stash_tail(stash, va);
     load(va, clamp(c_begin + 1));
     load(vb, clamp(c_begin + 2));
@@ -613,14 +672,19 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma11(const float2* __restrict_
         const unsigned m2 = max(m_prev, m_nxt);
         const int s_nxt = scale_of(m2);
         const bool ex_nxt = chunk_needs_exact(m2, min(z_prev, z_nxt), s_nxt);
+        const bool f32_nxt = ex_nxt && m2 < 0x7f800000u;
         load(ld, clamp(ch + 3));
-        put_chunk(nbuf, stash + pi * G::HP, nxt, ex_nxt, s_nxt);
+        put_chunk(nbuf, stash + pi * G::HP, nxt, ex_nxt, f32_nxt, s_nxt);
         stash_tail(stash + pn * G::HP, nxt);
         nf2 o[2 * G::TILES];
-        if (ex_cur)
-            direct_tile(cur, o);
-        else
+        if (__builtin_expect(ex_cur, 0)) {
+            if (f32_cur)
+                f32_tile(cur, o);
+            else
+                direct_tile(cur, o);
+        } else {
             mfma_tile(cur, -(s_cur + sh), o);
+        }
         store_tile(ch, o);
         unsigned m, z;
         reduce(nn, m, z);
@@ -631,6 +695,7 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma11(const float2* __restrict_
         m_prev = m_nxt;
         z_prev = z_nxt;
         ex_cur = ex_nxt;
+        f32_cur = f32_nxt;
         s_cur = s_nxt;
         nsh::lds_barrier();
     };
@@ -648,14 +713,16 @@ template <int D, int QH>
 int launch_v11(const nsh_fir_plan* p, const float2* in, const float2* hin, float2* hout, float2* out, int64_t n_out,
                hipStream_t s)
 {
-    using G = geom11<D, QH>;
+    using G = geom11x<D, QH>;
+    if (p->QFT != G::QF) return nsh::fail_msg("nsh_fir_ccf(mfma decim): tile tap image does not match the kernel");
     NSH_CK(set_lds_attr((const void*)k_fir_mfma11<D, QH>, G::LDS, p->dev));
     const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
     const int n_cu = plan_cus(p);
     const int64_t max_grid = (int64_t)n_cu * 2; // launch_v9's longer grids measured 4-7 % slower here
     const unsigned grid = (unsigned)(nchunks < max_grid ? nchunks : max_grid);
     hipLaunchKernelGGL((k_fir_mfma11<D, QH>), dim3(grid), dim3(G::NT), G::LDS, s, in, hin, hout, out,
-                       (const _Float16*)p->fragd8_dev, (const float*)p->taps_dev, p->L, p->sh8, n_out);
+                       (const _Float16*)p->fragd8_dev, (const float4*)p->tf32q_dev, (const float*)p->taps_dev, p->L, p->sh8,
+                       n_out);
     NSH_CK_LAUNCH("nsh_fir_ccf(mfma decim fp16x2)");
     return 0;
 }
@@ -736,6 +803,23 @@ bool nsh_fir_mfma_supported(const nsh_fir_plan* p)
     return Q <= QMAX;
 }
 
+// the exact-fp32 tile's taps (finite chunks the split cannot hold): R[m] = h[16 QF - 1 - m], QF tap
+// blocks of 16 (zero-padded past L), 4 copies shifted by 0..3 floats (nsh_fir_f32_tile.hpp)
+static hipError_t f32_tile_image(nsh_fir_plan* p, int QF)
+{
+    const int TWF = 16 * QF + 16, P = 16 * QF - 1;
+    std::vector<float> img((size_t)4 * TWF, 0.f);
+    for (int d = 0; d < 4; ++d)
+        for (int k = 0; k < TWF; ++k) {
+            const int t = P - (k + d);
+            img[(size_t)d * TWF + k] = (t >= 0 && t < p->L) ? p->taps_host[t] : 0.f;
+        }
+    p->QFT = QF;
+    hipError_t e = hipMalloc(&p->tf32q_dev, img.size() * sizeof(float));
+    if (e == hipSuccess) e = hipMemcpy(p->tf32q_dev, img.data(), img.size() * sizeof(float), hipMemcpyHostToDevice);
+    return e;
+}
+
 int nsh_fir_mfma_prepare_decim(nsh_fir_plan* p)
 {
     // polyphase taps h'_0[j] = h[D j], h'_r[j] = h[D (j - 1) + r] (r >= 1, j >= 1)
@@ -785,6 +869,7 @@ int nsh_fir_mfma_prepare_decim(nsh_fir_plan* p)
         NSH_CK(hipMalloc(&p->fragd8_dev, f8.size() * sizeof(_Float16)));
         NSH_CK(hipMemcpy(p->fragd8_dev, f8.data(), f8.size() * sizeof(_Float16), hipMemcpyHostToDevice));
     }
+    NSH_CK(f32_tile_image(p, D * (QH - 1) + 1)); // geom11x::QF: the whole D H-sample halo
     return nsh_fir_legacy_prepare(p); // legacy builds: k_fir_mfma7's bf16x3 fragments
 }
 
@@ -830,19 +915,7 @@ int nsh_fir_mfma_prepare(nsh_fir_plan* p)
             NSH_CK(hipMalloc(&p->frag12_dev, f12.size() * sizeof(_Float16)));
             NSH_CK(hipMemcpy(p->frag12_dev, f12.data(), f12.size() * sizeof(_Float16), hipMemcpyHostToDevice));
     }
-    {
-        // the exact-fp32 tile's taps (finite chunks the split cannot hold): R[m] = h[16 QF - 1 - m],
-        // QF = 2Q - 1 tap blocks of 16 (zero-padded past L), 4 copies shifted by 0..3 floats
-        const int QF = 2 * Q - 1, TWF = 16 * QF + 16, P = 16 * QF - 1;
-        std::vector<float> img((size_t)4 * TWF, 0.f);
-        for (int d = 0; d < 4; ++d)
-            for (int k = 0; k < TWF; ++k) {
-                const int t = P - (k + d);
-                img[(size_t)d * TWF + k] = (t >= 0 && t < p->L) ? p->taps_host[t] : 0.f;
-            }
-        NSH_CK(hipMalloc(&p->tf32q_dev, img.size() * sizeof(float)));
-        NSH_CK(hipMemcpy(p->tf32q_dev, img.data(), img.size() * sizeof(float), hipMemcpyHostToDevice));
-    }
+    NSH_CK(f32_tile_image(p, 2 * Q - 1)); // k_fir_mfma12's tile: v12's 32 (Q - 1)-sample halo
     return nsh_fir_legacy_prepare(p); // legacy builds: the bf16x3 / v9 / 16-sample fragments
 }
 

@@ -37,7 +37,8 @@ struct nsh_fir_plan {
     // as 4 shifted copies [4][16 QF + 16] fp32
     int QF = 0;
     void* tf32_dev = nullptr;
-    void* tf32q_dev = nullptr; // k_fir_mfma12's exact-fp32 tile taps (QF = 2Q - 1), same layout
+    void* tf32q_dev = nullptr; // the exact-fp32 tile taps of k_fir_mfma12 / k_fir_mfma11, same layout
+    int QFT = 0;               // their tap blocks: 2Q - 1 (k_fir_mfma12), D (QHD - 1) + 1 (k_fir_mfma11)
     void* casc = nullptr; // NSH_FIR_PFFT: a one-stage nsh_fir_cascade plan (k_fir_pfft)
     bool force_x3 = false; // NSH_FIR_MFMA_BF16X3: always the bf16x3 six-product kernel
     int variant = 0;      // MFMA kernel tuning variant (0 = default)

@@ -457,11 +457,12 @@ def test_fir_mfma_wide_dynamic_range(torch_cuda, v8_form):
 @pytest.mark.parametrize("kind", ["spike", "nan"])
 def test_fir_mfma_exact_paths(torch_cuda, v8_form, ntaps, decim, kind):
     """Every 2048-sample chunk outside the fp16x2 split's range.
-    'spike' (a finite 2^40 sample per chunk): k_fir_mfma12 (decim 1) computes such chunks with the
-    exact-fp32 matrix tile of k_fir_f32mfma (fp32 products and sums): bit-identical to the
-    NSH_FIR_MFMA_F32 kernel when both use the same tap blocking (QF = 2Q - 1: 127 and 64 taps),
-    and within tolerance of the oracle on each chunk's own scale. The decimators and the legacy
-    k_fir_mfma9 use the fp32 direct form there (taps in order k = 0..L-1, one fused multiply-add
+    'spike' (a finite 2^40 sample per chunk): k_fir_mfma12 (decim 1) and k_fir_mfma11 (decim 2, 4)
+    compute such chunks with the exact-fp32 matrix tile of k_fir_f32mfma (fp32 products and sums;
+    the decimators filter the chunk undecimated and keep every D-th output): within tolerance of
+    the oracle on each chunk's own scale, and at decim 1 bit-identical to the NSH_FIR_MFMA_F32
+    kernel when both use the same tap blocking (QF = 2Q - 1: 127 and 64 taps). The legacy
+    k_fir_mfma9 uses the fp32 direct form there (taps in order k = 0..L-1, one fused multiply-add
     each, the order k_fir_direct accumulates in): bit-identical to k_fir_direct.
     'nan' (a NaN per chunk): every form computes such chunks with the fp32 direct form: the same
     NaN positions as k_fir_direct and every finite output bit-identical to it."""
@@ -493,7 +494,7 @@ def test_fir_mfma_exact_paths(torch_cuda, v8_form, ntaps, decim, kind):
         if pf.kernel == "k_fir_f32mfma<%d>" % (2 * q12 - 1):
             yf, _ = run_fir(torch, pf, x, n)
             np.testing.assert_array_equal(y.view(np.uint32), yf.view(np.uint32))
-    else:
+    elif decim == 1:  # legacy k_fir_mfma9: the fp32 direct form
         np.testing.assert_array_equal(y.view(np.uint32), yd.view(np.uint32))
     ref = orc.fir_ccf(x[: n // decim * decim], h, decim)
     c = 2048 // decim
