@@ -18,8 +18,8 @@
 // Access shape as k_fir_mfma12: one 2048-sample chunk per 256-thread workgroup (a wave per
 // 512 outputs = 4 tiles of 8 blocks), chunk index remapped per XCD, the 16 (QF - 1)-sample
 // halo re-read, nontemporal loads and stores. Samples go to LDS as raw fp32 re / im planes
-// (rows of 16 samples at an 80-B pitch, im plane at 128 mod 256 B: every 16-lane
-// ds_read_b128 group hits 16 distinct 16-B slots). Taps: the reversed taps R[m] = h[P - m]
+// (rows of 16 samples at a 64-B pitch, im plane at 32 mod 256 B: conflict-free A reads,
+// nsh_fir_f32_tile.hpp). Taps: the reversed taps R[m] = h[P - m]
 // (P = 16 QF - 1) as 4 copies shifted by 0..3 floats (a lane's 4 taps of a block are one
 // aligned float4 from copy m0 mod 4; copy pitch = 64 mod 256 B: conflict-free), prepared
 // on the host and loaded per workgroup (L1/L2 hits).
@@ -153,7 +153,7 @@ __global__ __launch_bounds__(256) void k_fir_f32mfma(const float2* __restrict__ 
                 float re = 0.f, im = 0.f;
                 for (int k = 0; k < L; ++k) {
                     const int s = n - k;
-                    const int off = (s >> 4) * 80 + (s & 15) * 4;
+                    const int off = (s >> 4) * G::PITCH + (s & 15) * 4;
                     re = fmaf(taps[k], *reinterpret_cast<const float*>(lds + off), re);
                     im = fmaf(taps[k], *reinterpret_cast<const float*>(lds + G::PLANE + off), im);
                 }

@@ -362,10 +362,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
 // k_fir_mfma11's LDS with the exact-fp32 tile: a finite chunk whose range the split cannot hold is
 // filtered as if undecimated by k_fir_f32mfma's tile (nsh_fir_f32_tile.hpp, QF = HR + 1 tap blocks
 // of 16 over the chunk's D H-sample halo) and every D-th output kept -- the same fp32 matrix work per
-// input sample as at decim 1, no polyphase form. Each plane buffer grows to hold the tile's two fp32
-// planes; the tile's taps (one copy, loaded once per workgroup) and a per-wave output scratch (the
-// tile's lane map -> the split path's, for the common store) follow the stash. LDS stays within 2
-// resident workgroups per CU (the kernel's occupancy).
+// input sample as at decim 1, no polyphase form. Each plane buffer holds the tile's two fp32 planes
+// (at <2,5> and <4,3> they fit the split's buffer; other forms may grow it); the tile's taps (one
+// copy, loaded once per workgroup) and a per-wave output scratch (the tile's lane map -> the split
+// path's, for the common store) follow the stash. LDS stays within 2 resident workgroups per CU
+// (the kernel's occupancy).
 template <int D, int QH>
 struct geom11x : geom11<D, QH> {
     using B = geom11<D, QH>;
