@@ -503,6 +503,37 @@ def test_fir_mfma_exact_paths(torch_cuda, v8_form, ntaps, decim, kind):
         assert ok, (a, err, scale)
 
 
+@pytest.mark.parametrize("decim", [1, 2, 4])
+@pytest.mark.parametrize("ntaps", [127, 61])
+def test_fir_mfma_exact_tile_mixed_stream(torch_cuda, ntaps, decim):
+    """The exact-fp32 tile inside the default kernels (k_fir_mfma12, k_fir_mfma11) on a stream that
+    mixes ordinary chunks, chunks holding a finite 2^35 spike (beyond the split's range: the tile)
+    and chunks holding a sample 2^-35 below their maximum, cut into two calls at an unaligned point
+    with the history handed over, the second call ending inside a chunk. The tile's fp32 products
+    and sums carry no chunk-level scale, so every output meets the tolerance on its own block of
+    2048 / D outputs (scale = that block's largest reference output)."""
+    torch = torch_cuda
+    h = (np.hamming(ntaps) / (ntaps / 2)).astype(np.float32)
+    n_out = 23 * (2048 // decim) + 77
+    x = orc.synth(n_out * decim, 41)
+    rng = np.random.default_rng(5)
+    for c in rng.choice(23, 7, replace=False):
+        x[c * 2048 + int(rng.integers(0, 2048))] *= np.float32(2.0 ** 35)
+    for c in rng.choice(23, 4, replace=False):
+        x[c * 2048 + int(rng.integers(0, 2048))] *= np.float32(2.0 ** -35)
+    plan = nsh.FirPlan(h, decim, nsh.FIR_MFMA)
+    assert plan.kernel.startswith("k_fir_mfma12" if decim == 1 else "k_fir_mfma11"), plan.kernel
+    n1 = 9 * (2048 // decim) + 333  # first call: ends inside a chunk
+    y1, h1 = run_fir(torch, plan, x[: n1 * decim], n1)
+    y2, _ = run_fir(torch, plan, x[n1 * decim:], n_out - n1, hist=h1)
+    y = np.concatenate([y1, y2])
+    ref = orc.fir_ccf(x, h, decim)
+    blk = 2048 // decim
+    for a in range(0, n_out, blk):
+        ok, err, scale = orc.tol_ok(y[a:a + blk], ref[a:a + blk])
+        assert ok, (a, err, scale)
+
+
 def test_fir_mfma_per_chunk_scale(torch_cuda, v8_form):
     """Segments at amplitudes 1e-30, 1 and 1e30 (each far outside fp16's range unscaled):
     the per-chunk power-of-two scale keeps every segment at fp32 accuracy, checked on the
