@@ -129,9 +129,12 @@ int nsh_synth_cf32(float* out, int64_t n, uint64_t first_index, uint64_t seed, v
  * taps, PFFT for decim 8 and 16, else DIRECT); NSH_FIR_DIRECT is the fp32 VALU direct form
  * (decim 1, 2, 4, 8); NSH_FIR_MFMA is the split-precision Toeplitz form on the matrix
  * cores: decim 1 on 32-sample blocks, ntaps <= 161, fp16x2 at a per-chunk power-of-two scale
- * with three products (k_fir_mfma12; chunks holding non-finite or fp16-subnormal-range
- * samples take the fp32 direct form inside the same launch); decim 2 and 4 as the polyphase
- * fp16x2 form (k_fir_mfma11); NSH_FIR_MFMA16 is the bf16x3 form on 16-sample blocks (decim 1,
+ * with three products (k_fir_mfma12); decim 2 and 4 as the polyphase fp16x2 form
+ * (k_fir_mfma11). In both, a 2048-input chunk whose samples (with its halo) are finite but span
+ * more than the split holds takes the exact-fp32 matrix tile of NSH_FIR_MFMA_F32 (fp32 products
+ * and sums; the decimators filter it undecimated and keep every decim-th output), and one
+ * holding inf/NaN the fp32 direct form (exact IEEE semantics), inside the same launch;
+ * NSH_FIR_MFMA16 is the bf16x3 form on 16-sample blocks (decim 1,
  * ntaps <= 145); NSH_FIR_MFMA_BF16X3 forces the bf16x3 six-product kernel for decim 1;
  * NSH_FIR_MFMA_F32 is the exact-fp32 Toeplitz form on the fp32-input matrix instructions
  * (decim 1, ntaps <= 257, finite taps; no operand split: fp32 products and sums, chunks with
