@@ -15,6 +15,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--algo", default="mfma", choices=["mfma", "mfma_x3", "direct", "f32", "casc"])
 ap.add_argument("--log2n", type=int, default=25)
 ap.add_argument("--reps", type=int, default=10)
+ap.add_argument("--decim", type=int, default=1)
 a = ap.parse_args()
 n = 1 << a.log2n
 h = ss.firwin(127, 0.2).astype(np.float32)
@@ -29,10 +30,10 @@ if a.algo == "casc":  # C5's fused chain (nsh_fir_cascade_ccf): 4 x fir(firwin(1
     for _ in range(a.reps):
         p(x, None, hc, y, n // 16)
 else:
-    p = nsh.FirPlan(h, 1, {"mfma": nsh.FIR_MFMA, "mfma_x3": nsh.FIR_MFMA_BF16X3, "direct": nsh.FIR_DIRECT,
+    p = nsh.FirPlan(h, a.decim, {"mfma": nsh.FIR_MFMA, "mfma_x3": nsh.FIR_MFMA_BF16X3, "direct": nsh.FIR_DIRECT,
                                   "f32": nsh.FIR_MFMA_F32}[a.algo])
     for _ in range(a.reps):
-        p(x, hin, hout, y, n)
+        p(x, hin, hout, y, n // a.decim)
 for _ in range(a.reps):
     nsh.copy(x, y, 8 * n)  # calibration: exactly 8n B read + 8n B written per launch
 torch.cuda.synchronize()
