@@ -539,11 +539,17 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma11(const float2* __restrict_
                 }
             }
             if constexpr (G::TAIL) { // separate accumulators: see v5_compute
+                // single ds_read_b64 (the empty asm keeps the compiler from pairing the tiles'
+                // reads into ds_read2_b64, whose 16-lane groups see the re and im rows 4 apart on
+                // one bank: 4-way, 43-50 % of the kernel's LDS cycles in profiles/r03o_pmc_decim.json;
+                // as ds_read_b64, 2-way)
 #pragma unroll
                 for (int t = 0; t < G::TILES; ++t) {
                     const int off = row_base + t * 8 * 32 - (QH - 1) * 32 + g * 8;
                     const f16x4 A0 = *reinterpret_cast<const f16x4*>(ph + off);
+                    asm volatile("" ::: "memory");
                     const f16x4 A1 = *reinterpret_cast<const f16x4*>(ph + off + G::PLANE);
+                    asm volatile("" ::: "memory");
                     hi_t[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(A0, T0[r], hi_t[t], 0, 0, 0);
                     lo_t[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(A0, T1[r], lo_t[t], 0, 0, 0);
                     lo_t[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(A1, T0[r], lo_t[t], 0, 0, 0);
