@@ -218,14 +218,11 @@ def run_fp32_leg(a, n, taps, first, device, barrier, dist, tdev, torch, orc, nsr
     for _ in range(max(3, a.warmup // 2)):
         fb.run()
     barrier()
-    l0 = fb.stats()["launches"]
-    kms, samples = 0.0, 0
+    st0 = fb.stats()  # cumulative over the FIR's timed launches
+    l0 = st0["launches"]
     t0 = time.perf_counter()
     for _ in range(steps):
         fb.run()
-        st = fb.stats()
-        kms += st["kernel_ms"]
-        samples += st["samples"]
     barrier()
     el = time.perf_counter() - t0
     if dist is not None:
@@ -234,6 +231,7 @@ def run_fp32_leg(a, n, taps, first, device, barrier, dist, tdev, torch, orc, nsr
         el = float(t.item())
     st = fb.stats()
     launches = st["launches"] - l0
+    kms, samples = st["kernel_ms"] - st0["kernel_ms"], st["samples"] - st0["samples"]
     avg_ms = kms / launches
     m = 4096
     y = fb.tail(m)
@@ -398,15 +396,11 @@ def main():
         warm += 1
     warm_s = time.perf_counter() - tw
     barrier()
-    kms = 0.0
-    samples = 0
-    launches0 = fb.stats()["launches"]
+    st0 = fb.stats()  # cumulative HIP-event kernel time / samples of the FIR's timed launches
+    launches0 = st0["launches"]
     t0 = time.perf_counter()
     for _ in range(a.steps):
         fb.run()
-        st = fb.stats()  # HIP-event kernel time of this run (events re-armed at each start)
-        kms += st["kernel_ms"]
-        samples += st["samples"]
     barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
@@ -414,6 +408,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     st = fb.stats()
+    kms = st["kernel_ms"] - st0["kernel_ms"]
+    samples = st["samples"] - st0["samples"]
     algo_used = {1: "direct", 2: "mfma", 3: "mfma16", 4: "mfma_x3", 5: "mfma_f32"}.get(st["algo"], str(st["algo"]))
     kernel = st["kernel"]
     timed_launches = st["launches"] - launches0

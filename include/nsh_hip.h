@@ -57,6 +57,8 @@ int nsh_device_pci_id(int dev, char* buf, int len);
 int nsh_stream_create(int dev, void** stream);
 int nsh_stream_destroy(void* stream);
 int nsh_stream_sync(void* stream);
+/* 0: every operation on the stream has finished; 1: not yet; -1: error (hipStreamQuery, no wait). */
+int nsh_stream_query(void* stream);
 int nsh_event_create(void** event);
 int nsh_event_destroy(void* event);
 int nsh_event_record(void* event, void* stream);

@@ -31,8 +31,9 @@ const char* nsr_last_error(void);
 int nsr_fir_bench_create(int dev, const float* taps, int ntaps, int algo, int64_t n, uint64_t first_index,
                          uint64_t seed, size_t out_buf_bytes, int timing, void** handle);
 int nsr_fir_bench_run(void* handle); /* one run (start + wait); rethrown work() errors -> rc */
-/* Over the last run: summed FIR kernel time from HIP events around each launch on the
- * partition stream, FIR launches, samples, and the algorithm the plan resolved to. */
+/* Cumulative over every run since create (callers take differences around the runs they
+ * time): summed FIR kernel time from HIP events around each launch on the partition stream,
+ * FIR launches, samples, and the algorithm the plan resolved to. */
 int nsr_fir_bench_stats(void* handle, double* kernel_ms, uint64_t* launches, uint64_t* samples, int* algo);
 /* The FIR kernel the bench's block launches (after its first run), e.g. "k_fir_mfma12<5>". */
 const char* nsr_fir_bench_kernel(void* handle);

@@ -166,8 +166,8 @@ bool fir_filter_ccf::start()
         _zero_hist = false;
     }
     _cur = 0;
+    _done_ms = kernel_ms(); // the previous run's launches (finished: its run drained the stream)
     _ev_used = 0;
-    _timed_samples = 0;
     return block::start();
 }
 
@@ -202,7 +202,7 @@ work_return_code_t fir_filter_ccf::work(std::vector<block_work_input>& in, std::
 
 double fir_filter_ccf::kernel_ms()
 {
-    double total = 0;
+    double total = _done_ms;
     for (size_t i = 0; i < _ev_used; ++i) {
         float ms = 0;
         check(nsh_event_sync(_ev[i].second), "hip::fir_filter_ccf timing");

@@ -125,6 +125,7 @@ int nsr_fir_bench_create(int dev, const float* taps, int ntaps, int algo, int64_
         b->sched = schedulers::scheduler_hip::make("hip" + std::to_string(dev), dev, out_buf_bytes);
         b->fg->set_scheduler(b->sched);
         b->fg->set_wait_spin_us(5000); // one run is ~1 ms: poll for its end instead of sleeping
+        b->sched->set_flush_spin_us(5000); // and the partition stream's drain, likewise
         b->fg->validate();
 
         auto in_ring = std::dynamic_pointer_cast<hip_buffer>(b->sched->buffers()->get_input_buffer(b->fir->input_stream_ports()[0]));

@@ -81,6 +81,14 @@ int nsh_stream_sync(void* stream)
     NSH_CK(hipStreamSynchronize(S(stream)));
     return 0;
 }
+int nsh_stream_query(void* stream)
+{
+    const hipError_t e = hipStreamQuery(S(stream));
+    if (e == hipSuccess) return 0;
+    if (e == hipErrorNotReady) return 1;
+    fail(e, "hipStreamQuery");
+    return -1;
+}
 int nsh_event_create(void** event)
 {
     hipEvent_t e;

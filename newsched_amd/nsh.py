@@ -35,6 +35,7 @@ SIGNATURES = {
     "nsh_stream_create": (_i, [_i, C.POINTER(_vp)]),
     "nsh_stream_destroy": (_i, [_vp]),
     "nsh_stream_sync": (_i, [_vp]),
+    "nsh_stream_query": (_i, [_vp]),
     "nsh_event_create": (_i, [C.POINTER(_vp)]),
     "nsh_event_destroy": (_i, [_vp]),
     "nsh_event_record": (_i, [_vp, _vp]),

@@ -54,6 +54,12 @@ public:
     // or off; applies when fusion() is on.
     void set_fir_fusion(bool on) { _fir_fusion = on; }
     bool fir_fusion() const { return _fir_fusion; }
+    // End-of-run wait: poll the stream for up to `us` microseconds before blocking in
+    // hipStreamSynchronize (0 = block at once, the default). A blocking wait wakes some
+    // microseconds after the stream drains; polling sees it at once, for a busy host core during
+    // the run's last kernel. Takes effect at the next initialize().
+    void set_flush_spin_us(int us) { _flush_spin_us = us; }
+    int flush_spin_us() const { return _flush_spin_us; }
     // What the last initialize() fused: blocks that replaced chains, and the chains.
     const hip::fusion_result& fusion_plan() const { return _plan; }
 
@@ -67,6 +73,7 @@ private:
     void* _stream = nullptr;
     bool _fusion = true;
     bool _fir_fusion = true;
+    int _flush_spin_us = 0;
     hip::fusion_result _plan;
 };
 

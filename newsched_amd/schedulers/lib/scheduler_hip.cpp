@@ -1,4 +1,5 @@
 // GPU scheduler domain (see scheduler_hip.hpp).
+#include <chrono>
 #include <gnuradio/hip_context.hpp>
 #include <gnuradio/schedulers/hip/scheduler_hip.hpp>
 
@@ -75,7 +76,18 @@ thread_hooks scheduler_hip::hooks_for_group(const block_group_properties&)
     const int dev = _device;
     void* s = _stream;
     h.on_thread_start = [dev, s] { hip::bind_thread(dev, s); };
-    h.on_flush = [s] { hip::check(nsh_stream_sync(s), "scheduler_hip: flush"); };
+    const int spin_us = _flush_spin_us;
+    h.on_flush = [s, spin_us] {
+        if (spin_us > 0) {
+            const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(spin_us);
+            int q;
+            while ((q = nsh_stream_query(s)) == 1 && std::chrono::steady_clock::now() < until)
+                for (int i = 0; i < 64; ++i) __builtin_ia32_pause();
+            hip::check(q < 0 ? q : 0, "scheduler_hip: flush");
+            if (q == 0) return;
+        }
+        hip::check(nsh_stream_sync(s), "scheduler_hip: flush");
+    };
     // one thread per GPU partition: spinning briefly on its queue takes the futex wake-up out
     // of each run's start (the notification arrives within microseconds of the last one)
     h.queue_spin_us = 200;

@@ -23,13 +23,14 @@ for name, timing, per_run_stats in (("timing+stats", True, True), ("timing", Tru
     while time.perf_counter() - t0 < 1.0:
         fb.run()
     steps = 200
-    kms = 0.0
+    k0 = fb.stats()["kernel_ms"]  # cumulative
     t0 = time.perf_counter()
     for _ in range(steps):
         fb.run()
         if per_run_stats:
-            kms += fb.stats()["kernel_ms"]
+            fb.stats()
     el = time.perf_counter() - t0
+    kms = fb.stats()["kernel_ms"] - k0
     res[name] = {"us_per_run": round(el / steps * 1e6, 2), "kernel_us": round(kms / steps * 1e3, 2) if per_run_stats else None}
     fb.close() if hasattr(fb, "close") else None
 print(json.dumps(res))
