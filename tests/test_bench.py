@@ -83,6 +83,25 @@ def test_bench_one_gpu(torch_cuda):
 
 
 @pytest.mark.gpu
+def test_fir_bench_stats_cumulative(torch_cuda):
+    """nsr_fir_bench_stats counts every timed launch since create (bench.py reads it once on each
+    side of its timed loop): launches, samples and kernel time grow run by run."""
+    import numpy as np
+    from newsched_amd import nsr
+    n = 1 << 16
+    fb = nsr.FirBench(np.hamming(127).astype(np.float32) / 64, n, out_buf_bytes=8 << 20)
+    prev = fb.stats()
+    assert prev["launches"] == 0 and prev["samples"] == 0 and prev["kernel_ms"] == 0
+    for _ in range(3):
+        fb.run()
+        st = fb.stats()
+        assert st["launches"] > prev["launches"] and st["samples"] == prev["samples"] + n
+        assert st["kernel_ms"] > prev["kernel_ms"]
+        prev = st
+    fb.close()
+
+
+@pytest.mark.gpu
 def test_bench_two_ranks_rehearsal(torch_cuda):
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
