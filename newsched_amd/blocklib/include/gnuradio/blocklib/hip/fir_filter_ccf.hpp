@@ -41,10 +41,9 @@ public:
     // Per-launch kernel timing with HIP events on the launch stream (bench/profiling).
     void enable_timing(bool on) { _timing = on; }
     // Sum of kernel durations (ms) and output samples over every timed launch since the block
-    // was made (cumulative across runs: a caller takes differences around the runs it times);
-    // synchronises on the events of the current run. Each start() folds the previous run's
-    // (finished) events into the total and reuses them, so reading the totals costs nothing per
-    // run.
+    // was made (cumulative across runs: a caller takes differences around the runs it times).
+    // Reading it synchronises on the launches' events and folds them into the total; between
+    // reads a run costs only its two event records per launch.
     double kernel_ms();
     uint64_t timed_samples() const { return _timed_samples; }
 
@@ -54,7 +53,7 @@ private:
     bool _timing = false;
     std::vector<std::pair<void*, void*>> _ev;  // (start, stop) per launch, reused
     size_t _ev_used = 0;
-    double _done_ms = 0; // kernel time of the launches of earlier runs
+    double _done_ms = 0; // kernel time of the launches folded so far
     uint64_t _timed_samples = 0;
     std::vector<float> _taps;
     int _decim, _algo;

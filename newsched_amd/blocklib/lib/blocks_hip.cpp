@@ -1,5 +1,6 @@
 // gr::hip::* block work() implementations: argument plumbing from block_work_io to the
 // libnsh_hip.so C-ABI on the thread's HIP stream. Nonzero codes throw (hip::check).
+#include <gnuradio/run_trace.hpp>
 #include <gnuradio/blocklib/hip/arith.hpp>
 #include <gnuradio/blocklib/hip/copy.hpp>
 #include <gnuradio/blocklib/hip/fft.hpp>
@@ -166,8 +167,9 @@ bool fir_filter_ccf::start()
         _zero_hist = false;
     }
     _cur = 0;
-    _done_ms = kernel_ms(); // the previous run's launches (finished: its run drained the stream)
-    _ev_used = 0;
+    // the events of earlier runs are folded into the total when it is read (kernel_ms), not here:
+    // nothing per run but the two records per launch; a long unread series is folded at 4096
+    if (_ev_used >= 4096) kernel_ms();
     return block::start();
 }
 
@@ -186,6 +188,7 @@ work_return_code_t fir_filter_ccf::work(std::vector<block_work_input>& in, std::
         ev = &_ev[_ev_used++];
         check(nsh_event_record(ev->first, s), "hip::fir_filter_ccf timing");
     }
+    NSR_RT(4);
     check(nsh_fir_ccf(_plan, (const float*)in[0].buffer->read_ptr(), _zero_hist ? nullptr : (const float*)_hist[_cur],
                       (float*)_hist[_cur ^ 1], (float*)out[0].buffer->write_ptr(), n_out, s),
           "hip::fir_filter_ccf");
@@ -194,6 +197,7 @@ work_return_code_t fir_filter_ccf::work(std::vector<block_work_input>& in, std::
         check(nsh_event_record(ev->second, s), "hip::fir_filter_ccf timing");
         _timed_samples += (uint64_t)n_out;
     }
+    NSR_RT(5);
     _cur ^= 1;
     ++_launches;
     out[0].n_produced = n_out;
@@ -202,14 +206,14 @@ work_return_code_t fir_filter_ccf::work(std::vector<block_work_input>& in, std::
 
 double fir_filter_ccf::kernel_ms()
 {
-    double total = _done_ms;
     for (size_t i = 0; i < _ev_used; ++i) {
         float ms = 0;
         check(nsh_event_sync(_ev[i].second), "hip::fir_filter_ccf timing");
         check(nsh_event_elapsed_ms(_ev[i].first, _ev[i].second, &ms), "hip::fir_filter_ccf timing");
-        total += ms;
+        _done_ms += ms;
     }
-    return total;
+    _ev_used = 0; // folded: the events are reused by the next launches
+    return _done_ms;
 }
 
 // ---- fused decimating FIR chain -----------------------------------------------------

@@ -1,4 +1,5 @@
 // libnewsched.so flowgraph runners (include/nsr_flowgraph.h).
+#include <gnuradio/run_trace.hpp>
 #include "nsr_flowgraph.h"
 
 #include <chrono>
@@ -142,6 +143,14 @@ int nsr_fir_bench_create(int dev, const float* taps, int ntaps, int algo, int64_
         *handle = b;
     });
 }
+
+#if NSR_RUN_TRACE
+int nsr_run_trace(int64_t* out16) // probe builds only: the last run's stamps (ns)
+{
+    for (int k = 0; k < 16; ++k) out16[k] = gr::g_run_trace[k].load();
+    return 0;
+}
+#endif
 
 int nsr_fir_bench_run(void* handle)
 {

@@ -11,7 +11,7 @@ import numpy as np
 
 from . import nsh
 
-RT_LIB = os.path.join(nsh.LIB_DIR, "libnewsched.so")
+RT_LIB = os.environ.get("NSR_LIB") or os.path.join(nsh.LIB_DIR, "libnewsched.so")  # NSR_LIB: probe builds
 _lib = None
 
 _vp, _i, _i64, _u64, _sz, _d = C.c_void_p, C.c_int, C.c_int64, C.c_uint64, C.c_size_t, C.c_double

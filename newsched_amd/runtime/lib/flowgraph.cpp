@@ -1,5 +1,6 @@
 // flowgraph + flowgraph_monitor (reference runtime/lib/flowgraph.cpp,
 // runtime/lib/flowgraph_monitor.cpp; drain-based completion, see flowgraph_monitor.hpp).
+#include <gnuradio/run_trace.hpp>
 #include <gnuradio/domain_adapter_remote.hpp>
 #include <gnuradio/flowgraph.hpp>
 #include <gnuradio/graph_utils.hpp>
@@ -15,7 +16,10 @@ void flowgraph_monitor::push_message(fg_monitor_message msg)
     std::lock_guard<std::mutex> g(_m);
     switch (msg.type()) {
     case fg_monitor_message_t::DONE: ++_done_blocks; break;
-    case fg_monitor_message_t::FLUSHED: _flushed[msg.schedid()] = true; break;
+    case fg_monitor_message_t::FLUSHED:
+        _flushed[msg.schedid()] = true;
+        NSR_RT(8);
+        break;
     case fg_monitor_message_t::KILL: _killed = true; break;
     default: break;
     }
@@ -180,8 +184,11 @@ void flowgraph::wait()
 
 void flowgraph::run()
 {
+    NSR_RT(0);
     start();
+    NSR_RT(1);
     wait();
+    NSR_RT(9);
 }
 
 } // namespace gr

@@ -1,4 +1,5 @@
 // Block-group thread (reference schedulers/mt/lib/thread_wrapper.cpp:9-191).
+#include <gnuradio/run_trace.hpp>
 #include <gnuradio/schedulers/mt/thread_wrapper.hpp>
 
 #include <pthread.h>
@@ -46,7 +47,9 @@ bool thread_wrapper::handle_work_notification()
         if (kv.second == executor_iteration_status::READY) ready = true;
     }
     if (_run_active && _exec->all_finished(d_blocks)) {
+        NSR_RT(6);
         if (_hooks.on_flush) _hooks.on_flush(); // drain this partition's HIP stream
+        NSR_RT(7);
         _run_active = false;
         for (auto& b : d_blocks) d_fgmon->push_message(fg_monitor_message(fg_monitor_message_t::DONE, _id, b->id()));
         if (_on_finished) _on_finished(_thread_index);
@@ -80,8 +83,10 @@ void thread_wrapper::thread_body(thread_wrapper* top)
             if (msg->type() == scheduler_message_t::SCHEDULER_ACTION) {
                 switch (std::static_pointer_cast<scheduler_action>(msg)->action()) {
                 case scheduler_action_t::NOTIFY_ALL: // a run starts: re-arm on this thread
+                    NSR_RT(2);
                     top->_exec->reset_run_state();
                     for (auto& b : top->d_blocks) b->start();
+                    NSR_RT(3);
                     top->_run_active = true;
                     do_work = true;
                     break;
