@@ -68,6 +68,17 @@ namespace {
 #ifndef NSH_V12_ROT
 #define NSH_V12_ROT 1
 #endif
+// Cache policy of the decimators' chunk loads. A thread loads its D float4 (2 D consecutive
+// samples) in D instructions, so one instruction's lanes are 16 D bytes apart and D instructions
+// touch the same lines: at D = 4 nontemporal loads fetched each line from L2 four times, the
+// default policy lets the later instructions hit L1 -- 642 -> 544 us per 2^28 inputs, 52 -> 62 %;
+// at D = 2 nontemporal stays faster (591 vs 638 us; profiles/r03w_v11_load_policy_ab.log).
+#ifndef NSH_V11_AUX2
+#define NSH_V11_AUX2 2 // nt
+#endif
+#ifndef NSH_V11_AUX4
+#define NSH_V11_AUX4 0 // default
+#endif
 #ifndef NSH_V12_F32T
 #define NSH_V12_F32T 1 // probe builds: 0 = finite wide-range chunks on the fp32 direct form
 #endif
@@ -454,7 +465,11 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma11(const float2* __restrict_
 #pragma unroll
         for (int u = 0; u < G::UNITS; ++u)
 #pragma unroll
-            for (int f = 0; f < D; ++f) v[u * D + f] = buf_load_f4(r, ((tid + G::NT * u) * D + f) * 16);
+            for (int f = 0; f < D; ++f) {
+                const nsh::buf_f4 t = __builtin_bit_cast(
+                    nsh::buf_f4, __builtin_amdgcn_raw_buffer_load_b128(r, ((tid + G::NT * u) * D + f) * 16, 0, D == 2 ? NSH_V11_AUX2 : NSH_V11_AUX4));
+                v[u * D + f] = make_float4(t.x, t.y, t.z, t.w);
+            }
     };
     auto stash_tail = [&](float4* st, const float4 (&v)[4]) {
         if (tail_owner) {
