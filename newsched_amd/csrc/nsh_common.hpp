@@ -71,23 +71,31 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t chunk_rsrc(const float2* base,
     return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0, bytes, 0x00020000);
 }
 constexpr int AUX_NT = 2; // gfx950 cache policy bits: nt (streaming)
+// streaming loads / stores (ablation builds override: tools/probe/build_file_abl.sh)
+#ifndef NSH_AUX_LD
+#define NSH_AUX_LD 2
+#endif
+#ifndef NSH_AUX_ST
+#define NSH_AUX_ST 2
+#endif
+constexpr int AUX_LD = NSH_AUX_LD, AUX_ST = NSH_AUX_ST;
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef float buf_f4 __attribute__((ext_vector_type(4)));
 typedef float buf_f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ float4 buf_load_f4(__amdgpu_buffer_rsrc_t r, int byte_off)
 {
-    const buf_f4 t = __builtin_bit_cast(buf_f4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, AUX_NT));
+    const buf_f4 t = __builtin_bit_cast(buf_f4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, AUX_LD));
     return make_float4(t.x, t.y, t.z, t.w);
 }
 __device__ __forceinline__ void buf_store_f2(__amdgpu_buffer_rsrc_t r, int byte_off, buf_f2 v)
 {
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, byte_off, 0, AUX_NT);
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, byte_off, 0, AUX_ST);
 }
 
 __device__ __forceinline__ float2 buf_load_f2(__amdgpu_buffer_rsrc_t r, int byte_off)
 {
-    const buf_f2 t = __builtin_bit_cast(buf_f2, __builtin_amdgcn_raw_buffer_load_b64(r, byte_off, 0, AUX_NT));
+    const buf_f2 t = __builtin_bit_cast(buf_f2, __builtin_amdgcn_raw_buffer_load_b64(r, byte_off, 0, AUX_LD));
     return make_float2(t.x, t.y);
 }
 

@@ -156,7 +156,7 @@ __device__ __forceinline__ void load_frame16(cf (&v)[16], const float2* __restri
     const __amdgpu_buffer_rsrc_t r = nsh::chunk_rsrc<N>(in, f, nframes * N);
 #pragma unroll
     for (int m = 0; m < 16; ++m)
-        v[m] = __builtin_bit_cast(cf, __builtin_amdgcn_raw_buffer_load_b64(r, (j + 64 * m) * 8, 0, nsh::AUX_NT));
+        v[m] = __builtin_bit_cast(cf, __builtin_amdgcn_raw_buffer_load_b64(r, (j + 64 * m) * 8, 0, nsh::AUX_LD));
 }
 __device__ __forceinline__ void store_frame16(const cf (&v)[16], float2* __restrict__ out, int64_t f, int64_t nframes)
 {

@@ -362,7 +362,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
 #pragma unroll
         for (int reg = 0; reg < 8; ++reg) {
             const int c = f32t ? 128 * (4 * reg - 3 * (reg & 1)) : 256 * ((reg & 3) + 8 * (reg >> 2));
-            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(nsh::u32x2, o[reg]), r, lb, c, nsh::AUX_NT);
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(nsh::u32x2, o[reg]), r, lb, c, nsh::AUX_ST);
         }
     };
     process(c_first, va, ha);
