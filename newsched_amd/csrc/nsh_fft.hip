@@ -195,22 +195,27 @@ __global__ __launch_bounds__(NT) void k_fft1024(const float2* __restrict__ in, f
 // weights in LDS the kernel fits 168 VGPRs, i.e. 3 workgroups (12 waves) per CU, and that
 // occupancy hides the load latency better: 816 vs 858 us per 2^28 samples
 // (tools/probe/fft_ab.py history in DESIGN.md section 4).
-__global__ __launch_bounds__(NT, 2) void k_chan1024(const float2* __restrict__ in, float2* __restrict__ out, int64_t nframes,
+#ifndef NSH_CHAN_FPW
+#define NSH_CHAN_FPW 4
+#endif
+constexpr int CFPW = NSH_CHAN_FPW; // channelizer frames (waves) per workgroup
+template <int FW>
+__global__ __launch_bounds__(64 * FW, FW == 4 ? 2 : 1) void k_chan1024(const float2* __restrict__ in, float2* __restrict__ out, int64_t nframes,
                                                     const float2* __restrict__ tw_g, const float2* __restrict__ w)
 {
     __shared__ cf tw[N];
     __shared__ cf wl[N];
-    __shared__ cf img_all[FPW * WLDS];
-    for (int t = threadIdx.x; t < N; t += NT) {
+    __shared__ cf img_all[FW * WLDS];
+    for (int t = threadIdx.x; t < N; t += 64 * FW) {
         tw[t] = cf{ tw_g[t].x, tw_g[t].y };
         wl[t] = cf{ w[t].x, w[t].y };
     }
     __syncthreads();
     cf* img = img_all + (threadIdx.x >> 6) * WLDS;
     const int j = threadIdx.x & 63;
-    const int64_t stride = (int64_t)gridDim.x * FPW;
+    const int64_t stride = (int64_t)gridDim.x * FW;
     cf v[16];
-    for (int64_t f = (int64_t)blockIdx.x * FPW + (threadIdx.x >> 6); f < nframes; f += stride) {
+    for (int64_t f = (int64_t)blockIdx.x * FW + (threadIdx.x >> 6); f < nframes; f += stride) {
         load_frame16(v, in, f, nframes);
         fft_wave<false>(v, img, tw);
 #pragma unroll
@@ -242,10 +247,13 @@ int twiddles(int dev, const float2** tw)
     return 0;
 }
 
-unsigned frame_grid(int64_t nframes)
+unsigned frame_grid(int64_t nframes, int fw = FPW)
 {
-    const int64_t groups = (nframes + FPW - 1) / FPW;
-    const int64_t cap = 256 * 16;
+    const int64_t groups = (nframes + fw - 1) / fw;
+#ifndef NSH_CHAN_CAP
+#define NSH_CHAN_CAP 256
+#endif
+    const int64_t cap = fw == 4 ? 256 * 16 : NSH_CHAN_CAP;
     return (unsigned)(groups < cap ? groups : cap);
 }
 
@@ -281,7 +289,7 @@ int nsh_channelizer1024(const float* in, float* out, const float* w, int64_t nfr
     NSH_CK(hipGetDevice(&dev));
     const float2* tw = nullptr;
     if (int rc = twiddles(dev, &tw)) return rc;
-    hipLaunchKernelGGL(k_chan1024, dim3(frame_grid(nframes)), dim3(NT), 0, nsh::S(stream),
+    hipLaunchKernelGGL(k_chan1024<CFPW>, dim3(frame_grid(nframes, CFPW)), dim3(64 * CFPW), 0, nsh::S(stream),
                        (const float2*)in, (float2*)out, nframes, tw, (const float2*)w);
     NSH_CK_LAUNCH("nsh_channelizer1024");
     return 0;

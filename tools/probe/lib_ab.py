@@ -28,7 +28,7 @@ assert libs[0].nsh_synth_cf32(x.data_ptr(), n, 0, 0x6E736368, C.c_void_p(s.cuda_
 s.synchronize()
 hin = torch.zeros(126, dtype=torch.complex64, device="cuda")
 hout = torch.zeros_like(hin)
-for D in [int(d) for d in os.environ.get("DECIMS", "1,2,4").split(",")]:
+for D in [int(d) for d in os.environ.get("DECIMS", "1,2,4").split(",") if d]:
     n_out = n // D
     ys = [torch.zeros(n_out, dtype=torch.complex64, device="cuda") for _ in libs]
     plans = []
