@@ -1216,7 +1216,7 @@ void domain_adapter_remote::copy_items(buffer_sptr from, int n)
 void domain_adapter_remote::set_writer_done()
 {
     _buffer->set_writer_done();
-    if (_role == remote_role::SEND) {
+    if (_role == remote_role::SEND && !_failed.load()) { // a failed edge has nothing left to send
         pump();
         _tr->send_control(*_ch, remote::M_DONE); // behind this run's DATA messages
     }

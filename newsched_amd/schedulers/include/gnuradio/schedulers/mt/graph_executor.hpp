@@ -27,9 +27,17 @@ public:
 
     void reset_run_state() { _finished.clear(); }
     // Mark every block finished (error path): flags its buffers so neighbours drain.
+    // the error path's wind-down (a work() call threw): every block is finished even when one
+    // of them throws again on the way (a remote edge whose setup failed rethrows its error at
+    // each use); the first error is already with the flowgraph monitor
     void finish_all()
     {
-        for (auto& b : d_blocks) finish(b);
+        for (auto& b : d_blocks) {
+            try {
+                finish(b);
+            } catch (...) {
+            }
+        }
     }
     bool all_finished(const std::vector<block_sptr>& blocks) const;
     const std::vector<block_sptr>& blocks() const { return d_blocks; }

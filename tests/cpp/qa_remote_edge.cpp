@@ -93,6 +93,41 @@ TEST(RemoteCpu, ChainRestart)
     }
 }
 
+// A crossing whose setup is refused (here: "p2p" asked for host rings; on a node, "rccl" with
+// both ends on one GPU) is an error of fg->run() in BOTH processes -- the receiver's refusal,
+// and on the sender the closed handshake, raised when its upstream block first writes -- and
+// never a process abort (the error path's wind-down used to rethrow on the scheduler thread).
+TEST(RemoteCpu, SetupRefusedIsAnError)
+{
+    const size_t n = 50000;
+    auto src = blocks::vector_source_c::make(synth(n, 3));
+    auto cp0 = blocks::copy::make(sizeof(gr_complex));
+    auto cp1 = blocks::copy::make(sizeof(gr_complex));
+    auto snk = blocks::vector_sink_c::make(1, n);
+    auto fg = flowgraph::make();
+    fg->connect(src, 0, cp0, 0);
+    fg->connect(cp0, 0, cp1, 0);
+    fg->connect(cp1, 0, snk, 0);
+    auto s0 = sched_for(0, schedulers::scheduler_mt::make("r0", 8192));
+    auto s1 = sched_for(1, schedulers::scheduler_mt::make("r1", 8192));
+    fg->set_schedulers({ s0, s1 });
+    auto o = opts();
+    o.base_port += 100;
+    o.transport = "p2p";
+    auto conf = domain_adapter_remote_conf::make(o);
+    domain_conf_vec dc{ domain_conf(s0, { src, cp0 }, conf), domain_conf(s1, { cp1, snk }, conf) };
+    fg->partition(dc);
+    std::string what;
+    try {
+        fg->run();
+    } catch (const std::exception& e) {
+        what = e.what();
+    }
+    std::printf("  rank %d: run() raised: %s\n", rank(), what.empty() ? "(nothing)" : what.c_str());
+    EXPECT_TRUE(!what.empty());
+    if (rank() == 1) EXPECT_TRUE(what.find("p2p transport needs device rings") != std::string::npos);
+}
+
 // Tags across processes (reference qa_tags.cpp AcrossDomains shape, here over a process
 // boundary): src -> head -> ann0 [0] ~~> copy -> ann1 -> sink [1]. ann1 must see ann0's 4 tags
 // at their absolute offsets with their values and srcid, in each of two runs (the edge
@@ -322,6 +357,40 @@ TEST(RemoteGpu, DeviceChainRestart)
         }
     }
     expect_transport(da);
+}
+
+// "rccl" asked for with both device rings on one GPU (the 1-GPU box): the receiver refuses it
+// (RCCL cannot pair two ranks on one device) and both processes get the error from fg->run()
+// -- the sender's partition thread winds down without aborting the process.
+TEST(RemoteGpu, RcclRefusedOnOneGpu)
+{
+    const size_t n = 1u << 16;
+    auto src = blocks::vector_source_c::make(synth(n, 5));
+    auto mul = hip::multiply_const_cc::make(gr_complex(2.0f, 0.0f));
+    auto cp = hip::copy::make(1);
+    auto snk = blocks::vector_sink_c::make(1, n);
+    auto fg = flowgraph::make();
+    fg->connect(src, 0, mul, 0)->set_custom_buffer(HIP_BUFFER_ARGS_H2D);
+    fg->connect(mul, 0, cp, 0);
+    fg->connect(cp, 0, snk, 0)->set_custom_buffer(HIP_BUFFER_ARGS_D2H);
+    auto s0 = sched_for(0, schedulers::scheduler_hip::make("g0", 0, 1u << 18));
+    auto s1 = sched_for(1, schedulers::scheduler_hip::make("g1", 0, 1u << 18));
+    fg->set_schedulers({ s0, s1 });
+    auto o = opts();
+    o.base_port += 110;
+    o.transport = "rccl";
+    auto da = domain_adapter_remote_conf::make(o);
+    domain_conf_vec dc{ domain_conf(s0, { src, mul }, da), domain_conf(s1, { cp, snk }, da) };
+    fg->partition(dc);
+    std::string what;
+    try {
+        fg->run();
+    } catch (const std::exception& e) {
+        what = e.what();
+    }
+    std::printf("  rank %d: run() raised: %s\n", rank(), what.empty() ? "(nothing)" : what.c_str());
+    EXPECT_TRUE(!what.empty());
+    if (rank() == 1) EXPECT_TRUE(what.find("two different GPUs") != std::string::npos);
 }
 
 // Tags through device rings and a process crossing: host annotator -[H2D]-> hip::copy [0]

@@ -65,7 +65,7 @@ def run_pair(case, timeout=120, env_extra=None):
 
 @pytest.mark.parametrize("case", ["RemoteCpu.ChainRestart", "RemoteCpu.TwoCrossingsBothWays",
                                   "RemoteCpu.ReaderFinishesFirst", "RemoteCpu.TagsCrossProcesses",
-                                  "RemoteCpu.RestartDropsRemainder"])
+                                  "RemoteCpu.RestartDropsRemainder", "RemoteCpu.SetupRefusedIsAnError"])
 def test_remote_edges_cpu(case):
     run_pair(case)
 
@@ -98,3 +98,11 @@ def test_remote_edges_gpu(case, transport):
     the pinned-memory staging it replaces."""
     expect = {"auto": "p2p", "p2p": "p2p", "socket": "socket(staged)"}[transport]
     run_pair(case, timeout=300, env_extra={"QA_TRANSPORT": transport, "QA_EXPECT_TRANSPORT": expect})
+
+
+@pytest.mark.gpu
+def test_rccl_refused_on_one_gpu():
+    """transport "rccl" with both device rings on the one GPU: refused by the receiver, an error
+    of fg->run() in both processes (no abort, no hang)."""
+    outs = run_pair("RemoteGpu.RcclRefusedOnOneGpu", timeout=120)
+    assert "two different GPUs" in outs[1]
