@@ -116,6 +116,33 @@ def test_add_mul_cc_bit_exact(torch_cuda, n):
     np.testing.assert_array_equal(host(dy), orc.mul_cc(a, b))
 
 
+@pytest.mark.parametrize("oa,ob,oy", [(1, 0, 0), (0, 1, 1), (1, 1, 0), (3, 2, 1)])
+def test_add_mul_cc_mixed_alignment(torch_cuda, oa, ob, oy):
+    """add_cc / multiply_cc / the 4-stage chain with each operand at its own sample offset (8-B
+    but not 16-B aligned where odd), as two edges' read pointers and a write pointer of a flowgraph
+    are; bit-exact against the oracle, guard samples around the output untouched."""
+    torch = torch_cuda
+    n = 12_345
+    a, b = orc.synth(n, 3), orc.synth(n, 4)
+    da = torch.zeros(n + 4, dtype=torch.complex64, device="cuda")
+    db = torch.zeros(n + 4, dtype=torch.complex64, device="cuda")
+    da[oa:oa + n] = dev(torch, a)
+    db[ob:ob + n] = dev(torch, b)
+    guard = complex(9.0, -9.0)
+    for fn, ref in ((nsh.add_cc, orc.add_cc(a, b)), (nsh.mul_cc, orc.mul_cc(a, b))):
+        dy = torch.full((n + 4,), guard, dtype=torch.complex64, device="cuda")
+        fn(da.data_ptr() + 8 * oa, db.data_ptr() + 8 * ob, dy.data_ptr() + 8 * oy, n)
+        y = host(dy)
+        np.testing.assert_array_equal(y[oy:oy + n], ref)
+        assert np.all(y[:oy] == guard) and np.all(y[oy + n:] == guard)
+    ks = [complex(np.exp(0.1j * (i + 1))) for i in range(4)]
+    dy = torch.full((n + 4,), guard, dtype=torch.complex64, device="cuda")
+    nsh.mul_const_chain_cc(da.data_ptr() + 8 * oa, dy.data_ptr() + 8 * oy, n, ks)
+    y = host(dy)
+    np.testing.assert_array_equal(y[oy:oy + n], orc.mul_const_chain_cc(a, [np.complex64(k) for k in ks]))
+    assert np.all(y[:oy] == guard) and np.all(y[oy + n:] == guard)
+
+
 @pytest.mark.parametrize("vlen,nitems", [(1024, 37), (1, 1000), (3, 777), (1024, 0)])
 def test_mul_const_vcc_bitexact(torch_cuda, vlen, nitems):
     """multiply_const_vcc: x[i][j] * k[j], each product rounded as the oracle's mul_cc."""
@@ -349,6 +376,38 @@ def test_fir_chunked_stream_equals_one_shot(torch_cuda, name, algo):
     else:
         ok, err, scale = orc.tol_ok(np.concatenate(parts), y_all)
         assert ok and err <= 1e-6 * scale, (err, scale)
+
+
+@pytest.mark.parametrize("algo,decim,ntaps", [(nsh.FIR_DIRECT, 1, 127), (nsh.FIR_MFMA, 1, 127), (nsh.FIR_MFMA, 2, 127),
+                                               (nsh.FIR_MFMA, 4, 127), (nsh.FIR_MFMA_F32, 1, 127), (nsh.FIR_AUTO, 8, 127),
+                                               (nsh.FIR_AUTO, 16, 511), (nsh.FIR_MFMA, 1, 31)])
+def test_fir_odd_sample_offsets(torch_cuda, algo, decim, ntaps):
+    """Buffers as a flowgraph hands them over: hip_buffer read/write pointers advance by any item
+    count, so a work() call's input, output and history pointers are 8-byte (one complex sample)
+    but not 16-byte aligned as often as not. Every FIR form (16-B buffer loads, 8-B stores) over
+    pointers at odd sample offsets into larger allocations, three calls with the history handed
+    on, against the oracle; the guard samples around the output stay untouched."""
+    torch = torch_cuda
+    h = (np.hanning(ntaps + 2)[1:-1] / (ntaps / 2)).astype(np.float32)
+    plan = nsh.FirPlan(h, decim, algo)
+    sizes = [1, 2049, 70_001]  # outputs per call
+    n_in = sum(sizes) * decim
+    x = orc.synth(n_in, 7)
+    dx = torch.zeros(n_in + 3, dtype=torch.complex64, device="cuda")
+    dx[1:1 + n_in] = dev(torch, x)
+    guard = complex(123.0, -77.0)
+    dy = torch.full((sum(sizes) + 3,), guard, dtype=torch.complex64, device="cuda")
+    hl = max(plan.ntaps - 1, 1)
+    hs = [torch.zeros(hl + 1, dtype=torch.complex64, device="cuda") for _ in range(2)]
+    pos, cur = 0, 0
+    for i, m in enumerate(sizes):
+        plan(dx[1 + pos * decim:], 0 if i == 0 else hs[cur][1:], hs[cur ^ 1][1:], dy[1 + pos:], m)
+        cur ^= 1
+        pos += m
+    y = host(dy)
+    assert y[0] == guard and np.all(y[1 + pos:] == guard)
+    ok, err, scale = orc.tol_ok(y[1:1 + pos], orc.fir_ccf(x, h, decim))
+    assert ok, (err, scale)
 
 
 @pytest.mark.parametrize("name,algo", ALGOS)
