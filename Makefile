@@ -34,7 +34,7 @@ TOOL_BIN := $(patsubst tools/%.cpp,build/tools/%,$(TOOL_SRC))
 all: hip runtime tests tools oracle
 hip: $(LIBDIR)/libnsh_hip.so
 runtime: $(LIBDIR)/libnewsched.so
-tests: $(TEST_BIN)
+tests: $(TEST_BIN) build/tests/libfake_rccl.so
 tools: $(TOOL_BIN)
 oracle:
 	$(MAKE) -C oracle
@@ -63,6 +63,11 @@ $(LIBDIR)/libnewsched.so: $(RT_OBJ) $(LIBDIR)/libnsh_hip.so
 build/tests/%: tests/cpp/%.cpp $(LIBDIR)/libnewsched.so $(wildcard tests/cpp/*.hpp)
 	@mkdir -p build/tests
 	$(CXX) $(CXXFLAGS) -Itests/cpp -o $@ $< -L$(LIBDIR) -lnewsched -lnsh_hip -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)'
+
+# RCCL test double for the remote edge's rccl transport on host rings (tests/test_remote_edge.py)
+build/tests/libfake_rccl.so: tests/cpp/fake_rccl.c
+	@mkdir -p build/tests
+	$(CC) -O2 -std=gnu11 -fPIC -shared -Wall -Wextra -pthread -o $@ $< -ldl
 
 build/tools/%: tools/%.cpp $(LIBDIR)/libnewsched.so
 	@mkdir -p build/tools

@@ -657,7 +657,14 @@ private:
 };
 
 // RCCL point-to-point on the partition streams (device rings on different GPUs). librccl
-// is loaded on first use so that host-only builds and tests do not need it.
+// is loaded on first use so that host-only builds and tests do not need it. Test hook:
+// NSH_RCCL_LIB names another library with the same five entry points (the tests load
+// build/tests/libfake_rccl.so, tests/cpp/fake_rccl.c: payloads over a Unix socket, read and
+// landed in stream order on device rings), and with NSH_REMOTE_TEST_RCCL=1 the receiver accepts
+// "rccl" for any pair of rings, so this transport's protocol (id exchange, communicator per
+// crossing, DATA header then the payload's send / recv on the partition / adapter streams,
+// release at once, discarded messages still received, teardown) runs in the 2-process tests on
+// the CPU (host rings) and on one GPU (device rings); the real library needs two GPUs.
 class rccl_transport : public transport
 {
     struct api {
@@ -674,8 +681,12 @@ class rccl_transport : public transport
         static api a;
         static std::once_flag once;
         std::call_once(once, [] {
-            a.h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
-            if (!a.h) a.h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+            if (const char* t = std::getenv("NSH_RCCL_LIB"); t && *t) {
+                a.h = dlopen(t, RTLD_NOW | RTLD_LOCAL); // test double (see above); no fallback
+            } else {
+                a.h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+                if (!a.h) a.h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+            }
             if (!a.h) return;
             a.get_unique_id = (int (*)(void*))dlsym(a.h, "ncclGetUniqueId");
             a.comm_destroy = (int (*)(void*))dlsym(a.h, "ncclCommDestroy");
@@ -701,10 +712,10 @@ public:
     };
     using init_fn = int (*)(void**, int, uid, int);
 
-    rccl_transport(channel& ch, bool sender, int device) : _sender(sender)
+    rccl_transport(channel& ch, bool sender, int device, bool dev_ring) : _sender(sender), _dev(dev_ring)
     {
         auto& L = lib();
-        hip::check(nsh_set_device(device), "remote edge: set device");
+        if (_dev) hip::check(nsh_set_device(device), "remote edge: set device");
         uid id{};
         if (sender) {
             ck(L.get_unique_id(&id), "ncclGetUniqueId");
@@ -725,16 +736,18 @@ public:
     {
         // header first: the receiver posts the matching ncclRecv when it reads it
         write_data(ch, n, ntags, blob, [] {});
-        ck(lib().send(p, bytes, /*ncclInt8*/ 0, /*peer*/ 1, _comm, hip::current_stream()), "ncclSend");
+        ck(lib().send(p, bytes, /*ncclInt8*/ 0, /*peer*/ 1, _comm, stream()), "ncclSend");
         return release::now;
     }
     void recv(channel&, void* p, size_t bytes) override
     {
-        ck(lib().recv(p, bytes, /*ncclInt8*/ 0, /*peer*/ 0, _comm, hip::current_stream()), "ncclRecv");
+        ck(lib().recv(p, bytes, /*ncclInt8*/ 0, /*peer*/ 0, _comm, stream()), "ncclRecv");
     }
 
 private:
+    void* stream() const { return _dev ? hip::current_stream() : nullptr; }
     bool _sender;
+    bool _dev; // device ring (always, but for the host-ring test double)
     void* _comm = nullptr;
 };
 
@@ -908,7 +921,7 @@ void domain_adapter_remote::buffer_ready()
                 }
             }
             if (chosen == T_RCCL)
-                _tr = std::make_shared<rccl_transport>(*_ch, true, _device);
+                _tr = std::make_shared<rccl_transport>(*_ch, true, _device, dev_side);
             else if (chosen == T_DEFERRED_TEST)
                 _tr = std::make_shared<deferred_test_transport>();
             else if (chosen == T_SOCKET)
@@ -936,7 +949,9 @@ void domain_adapter_remote::buffer_ready()
             const bool both_dev = dev_side && peer.is_device && mine.pci[0] && peer.pci[0];
             const bool two_gpus = both_dev && std::strncmp(peer.pci, mine.pci, sizeof(mine.pci)) != 0;
             const int32_t want = peer.want ? peer.want : mine.want;
-            if (want == T_RCCL && !two_gpus)
+            const char* tr = std::getenv("NSH_REMOTE_TEST_RCCL"); // the test double (rccl_transport)
+            const bool rccl_test = tr && *tr == '1' && dev_side == (peer.is_device != 0);
+            if (want == T_RCCL && !two_gpus && !rccl_test)
                 throw std::runtime_error("remote edge: rccl transport needs device rings on two different GPUs");
             if (want == T_P2P && !both_dev) throw std::runtime_error("remote edge: p2p transport needs device rings");
             if (want == T_DEFERRED_TEST && (dev_side || peer.is_device))
@@ -966,7 +981,7 @@ void domain_adapter_remote::buffer_ready()
                 }
             }
             if (mine.chosen == T_RCCL)
-                _tr = std::make_shared<rccl_transport>(*_ch, false, _device);
+                _tr = std::make_shared<rccl_transport>(*_ch, false, _device, dev_side);
             else if (mine.chosen == T_DEFERRED_TEST)
                 _tr = std::make_shared<deferred_test_transport>();
             else if (mine.chosen == T_SOCKET)

@@ -91,13 +91,14 @@ TEST(RemoteCpu, ChainRestart)
             EXPECT_TRUE(snk->data() == ref);
         }
     }
+    expect_transport(da);
 }
 
 // A crossing whose setup is refused (here: "p2p" asked for host rings; on a node, "rccl" with
 // both ends on one GPU) is an error of fg->run() in BOTH processes -- the receiver's refusal,
 // and on the sender the closed handshake, raised when its upstream block first writes -- and
 // never a process abort (the error path's wind-down used to rethrow on the scheduler thread).
-TEST(RemoteCpu, SetupRefusedIsAnError)
+static void setup_refused(const char* transport, int port_offset, const char* why)
 {
     const size_t n = 50000;
     auto src = blocks::vector_source_c::make(synth(n, 3));
@@ -112,8 +113,8 @@ TEST(RemoteCpu, SetupRefusedIsAnError)
     auto s1 = sched_for(1, schedulers::scheduler_mt::make("r1", 8192));
     fg->set_schedulers({ s0, s1 });
     auto o = opts();
-    o.base_port += 100;
-    o.transport = "p2p";
+    o.base_port += port_offset;
+    o.transport = transport;
     auto conf = domain_adapter_remote_conf::make(o);
     domain_conf_vec dc{ domain_conf(s0, { src, cp0 }, conf), domain_conf(s1, { cp1, snk }, conf) };
     fg->partition(dc);
@@ -125,7 +126,13 @@ TEST(RemoteCpu, SetupRefusedIsAnError)
     }
     std::printf("  rank %d: run() raised: %s\n", rank(), what.empty() ? "(nothing)" : what.c_str());
     EXPECT_TRUE(!what.empty());
-    if (rank() == 1) EXPECT_TRUE(what.find("p2p transport needs device rings") != std::string::npos);
+    if (rank() == 1) EXPECT_TRUE(what.find(why) != std::string::npos);
+}
+TEST(RemoteCpu, SetupRefusedIsAnError) { setup_refused("p2p", 100, "p2p transport needs device rings"); }
+// "rccl" on host rings without the test double's hook (NSH_REMOTE_TEST_RCCL)
+TEST(RemoteCpu, RcclRefusedOnHostRings)
+{
+    setup_refused("rccl", 110, "rccl transport needs device rings on two different GPUs");
 }
 
 // Tags across processes (reference qa_tags.cpp AcrossDomains shape, here over a process
@@ -170,6 +177,7 @@ TEST(RemoteCpu, TagsCrossProcesses)
             }
         }
     }
+    expect_transport(da);
 }
 
 // The CPU form of RemoteGpu.RestartDropsRemainder: host rings, fir_filter_ccf(h, 4) downstream
@@ -209,6 +217,7 @@ TEST(RemoteCpu, RestartDropsRemainder)
                 EXPECT_TRUE(snk->data() == first);
         }
     }
+    expect_transport(da);
 }
 
 // The edge's release rule with a transport whose reads complete later on another thread
@@ -291,6 +300,7 @@ TEST(RemoteCpu, TwoCrossingsBothWays)
         for (auto& v : ref) v = cmul(cmul(v, k1), k2);
         EXPECT_TRUE(snk->data() == ref);
     }
+    expect_transport(da);
 }
 
 // endless source [0] ~~> head(n) -> sink [1]: the reader finishing first must stop the
@@ -321,6 +331,7 @@ TEST(RemoteCpu, ReaderFinishesFirst)
         for (size_t i = 0; i < n; ++i) ok = ok && got[i] == x[i % x.size()];
         EXPECT_TRUE(ok);
     }
+    expect_transport(da);
 }
 
 // GPU: vector_source -[H2D]-> hip::multiply_const [rank 0, scheduler_hip] ~~> hip::copy

@@ -121,7 +121,7 @@ def test_bench_two_ranks_rehearsal(torch_cuda):
 def test_bench_spawns_ranks_and_c5_leg(torch_cuda):
     """The driver's N>1 form without torchrun: bench.py starts the ranks itself; both shards'
     tails pass; the C5 pipeline leg ({1,2}|{3,4} over domain_adapter_remote; two ranks on one
-    GPU negotiate the staged socket transport, RCCL needs two GPUs) is parity-green."""
+    GPU negotiate the p2p transport, RCCL needs two GPUs) is parity-green."""
     env = dict(os.environ, NSH_BENCH_BACKEND="gloo")
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         env.pop(k, None)
@@ -135,6 +135,25 @@ def test_bench_spawns_ranks_and_c5_leg(torch_cuda):
     assert c5["value"] > 0
     # both ranks share the box's one GPU: auto negotiates the IPC landing-slot transport
     assert "p2p" in c5["transports"]["0"] and "p2p" in c5["transports"]["1"], c5
+
+
+@pytest.mark.gpu
+def test_bench_c5_leg_rccl_transport_with_test_double(torch_cuda):
+    """The driver's multi-GPU C5 leg as it will run there (--c5-transport rccl: the ranks' edges on
+    domain_adapter_remote's rccl transport, stream-ordered sends / receives on the partition and
+    adapter streams) with the RCCL test double (tests/cpp/fake_rccl.c) standing in for the
+    library, which refuses two ranks on one GPU: parity-green, every rank reports rccl."""
+    fake = os.path.join(ROOT, "build", "tests", "libfake_rccl.so")
+    assert os.path.exists(fake), "make tests builds the RCCL test double"
+    env = dict(os.environ, NSH_BENCH_BACKEND="gloo", NSH_RCCL_LIB=fake, NSH_REMOTE_TEST_RCCL="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    out = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--c5-log2n", "20", "--c5-transport", "rccl"] + ARGS,
+                         cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    c5 = _json_line(out.stdout)["c5_pipeline"]
+    assert c5["ok"] and c5["parity"]["ok"], c5
+    assert len(c5["transports"]) == 2 and all(t.endswith(":rccl") for t in c5["transports"].values()), c5
 
 
 @pytest.mark.gpu

@@ -17,6 +17,7 @@ import pytest
 from tests.conftest import ROOT
 
 EXE = os.path.join(ROOT, "build", "tests", "qa_remote_edge")
+FAKE_RCCL = os.path.join(ROOT, "build", "tests", "libfake_rccl.so")
 
 
 def free_port_block(width=64):
@@ -40,7 +41,7 @@ def free_port_block(width=64):
 
 
 def run_pair(case, timeout=120, env_extra=None):
-    if not os.path.exists(EXE):
+    if not (os.path.exists(EXE) and os.path.exists(FAKE_RCCL)):
         subprocess.run(["make", "-s", "-C", ROOT, "tests"], check=True)
     port = free_port_block(128)
     procs = []
@@ -68,6 +69,29 @@ def run_pair(case, timeout=120, env_extra=None):
                                   "RemoteCpu.RestartDropsRemainder", "RemoteCpu.SetupRefusedIsAnError"])
 def test_remote_edges_cpu(case):
     run_pair(case)
+
+
+@pytest.mark.parametrize("case", ["RemoteCpu.ChainRestart", "RemoteCpu.TwoCrossingsBothWays",
+                                  "RemoteCpu.ReaderFinishesFirst", "RemoteCpu.TagsCrossProcesses",
+                                  "RemoteCpu.RestartDropsRemainder"])
+def test_remote_edges_cpu_rccl_protocol(case):
+    """The "rccl" transport's own code path -- unique-id exchange over the control channel, a
+    2-rank communicator per crossing, the DATA header then the payload's ncclSend / ncclRecv, the
+    span released at send (RCCL reads it stream-ordered), discarded messages still received,
+    restarts, two crossings between one pair of processes, teardown -- over host rings, through
+    the RCCL test double tests/cpp/fake_rccl.c (NSH_RCCL_LIB; NSH_REMOTE_TEST_RCCL=1 lets the
+    receiver accept rccl without two GPUs). The real library needs two GPUs, so this is what
+    runs the transport before a multi-GPU node does; every crossing must report "rccl"."""
+    outs = run_pair(case, env_extra={"QA_TRANSPORT": "rccl", "QA_EXPECT_TRANSPORT": "rccl",
+                                     "NSH_RCCL_LIB": FAKE_RCCL, "NSH_REMOTE_TEST_RCCL": "1"})
+    assert all("transport rccl" in o for o in outs)
+
+
+def test_rccl_on_host_rings_refused_without_the_test_double():
+    """Without the test hook, "rccl" asked for host rings is refused by the receiver: an error of
+    fg->run() in both processes (the real library would be handed host pointers)."""
+    outs = run_pair("RemoteCpu.RcclRefusedOnHostRings")
+    assert "two different GPUs" in outs[1]
 
 
 def test_deferred_release_keeps_span_until_read():
@@ -98,6 +122,19 @@ def test_remote_edges_gpu(case, transport):
     the pinned-memory staging it replaces."""
     expect = {"auto": "p2p", "p2p": "p2p", "socket": "socket(staged)"}[transport]
     run_pair(case, timeout=300, env_extra={"QA_TRANSPORT": transport, "QA_EXPECT_TRANSPORT": expect})
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", GPU_CASES)
+def test_remote_edges_gpu_rccl_protocol(case):
+    """The "rccl" transport on device rings, both ranks on the box's one GPU, with the RCCL test
+    double in place of the library (which refuses two ranks on one device): the sender's payload
+    read in stream order on its partition stream and the span released at once, the receiver's
+    landing in stream order on its adapter stream ahead of post_write's event -- the ordering the
+    real library gives -- through every GPU case (restarts, tags, the C5 {1,2}|{3,4} split,
+    a decimator's remainder dropped across runs)."""
+    run_pair(case, timeout=300, env_extra={"QA_TRANSPORT": "rccl", "QA_EXPECT_TRANSPORT": "rccl",
+                                           "NSH_RCCL_LIB": FAKE_RCCL, "NSH_REMOTE_TEST_RCCL": "1"})
 
 
 @pytest.mark.gpu
