@@ -322,6 +322,32 @@ def test_c5_windowed_large(torch_cuda, log2n):
         assert ok, (start, err, scale)
 
 
+def test_c5_odd_sample_offsets(torch_cuda):
+    """The fused chain on input, output and history pointers at odd sample offsets (8-B but not
+    16-B aligned) into larger buffers, three calls with the history handed on, output guards
+    untouched; against the oracle's staged chain."""
+    torch = torch_cuda
+    p = nsh.FirCascadePlan(C5)
+    sizes = [3, 1000, 40_001]
+    n_total = sum(sizes)
+    x = orc.synth(16 * n_total, 91)
+    dx = torch.zeros(16 * n_total + 3, dtype=torch.complex64, device="cuda")
+    dx[1:1 + 16 * n_total] = torch.from_numpy(x).cuda()
+    guard = complex(7.0, -7.0)
+    dy = torch.full((n_total + 3,), guard, dtype=torch.complex64, device="cuda")
+    hs = [torch.zeros(1891, dtype=torch.complex64, device="cuda") for _ in range(2)]
+    pos, cur = 0, 0
+    for i, m in enumerate(sizes):
+        p(dx[1 + 16 * pos:], None if i == 0 else hs[cur][1:], hs[cur ^ 1][1:], dy[1 + pos:], m)
+        cur ^= 1
+        pos += m
+    torch.cuda.synchronize()
+    y = dy.cpu().numpy()
+    assert y[0] == guard and np.all(y[1 + n_total:] == guard)
+    ok, err, scale = orc.tol_ok(y[1:1 + n_total], ref_chain(x, C5))
+    assert ok, (err, scale)
+
+
 def test_c5_many_calls_ring_offsets(torch_cuda):
     """The flowgraph pattern: one device input buffer read at advancing offsets (multiples of 16
     samples), outputs written at arbitrary 8-B-aligned offsets of one buffer, ping-pong
