@@ -13,15 +13,8 @@ CXXFLAGS := -O3 -std=c++17 -fPIC -Wall -Wextra -Wno-unused-parameter -pthread \
             -Iinclude -Inewsched_amd/runtime/include -Inewsched_amd/schedulers/include \
             -Inewsched_amd/blocklib/include
 
-# LEGACY=1 adds the superseded FIR matrix-core kernels (k_fir_mfma2/5/7/9, k_fir_casc2: A/B runs
-# and their parity tests, pytest marker `legacy`); the default library leaves them out
-LEGACY   ?= 0
 HIP_SRC  := $(wildcard newsched_amd/csrc/*.hip)
-ifeq ($(LEGACY),1)
-HIP_SRC  += newsched_amd/csrc/legacy/nsh_fir_legacy.hip
-endif
 HIP_OBJ  := $(patsubst newsched_amd/csrc/%.hip,$(OBJDIR)/hip/%.o,$(HIP_SRC))
-LEGACY_STAMP := $(OBJDIR)/legacy_$(LEGACY).stamp
 RT_SRC   := $(wildcard newsched_amd/runtime/lib/*.cpp) $(wildcard newsched_amd/schedulers/lib/*.cpp) \
             $(wildcard newsched_amd/blocklib/lib/*.cpp) $(wildcard newsched_amd/capi/*.cpp)
 RT_OBJ   := $(patsubst newsched_amd/%.cpp,$(OBJDIR)/rt/%.o,$(RT_SRC))
@@ -43,13 +36,7 @@ $(OBJDIR)/hip/%.o: newsched_amd/csrc/%.hip $(wildcard newsched_amd/csrc/*.hpp) i
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-# relink when LEGACY changes (the object list shrinks without any object getting newer)
-$(LEGACY_STAMP):
-	@mkdir -p $(OBJDIR)
-	@rm -f $(OBJDIR)/legacy_*.stamp
-	@touch $@
-
-$(LIBDIR)/libnsh_hip.so: $(HIP_OBJ) $(LEGACY_STAMP)
+$(LIBDIR)/libnsh_hip.so: $(HIP_OBJ)
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(HIP_OBJ)
 
@@ -64,10 +51,11 @@ build/tests/%: tests/cpp/%.cpp $(LIBDIR)/libnewsched.so $(wildcard tests/cpp/*.h
 	@mkdir -p build/tests
 	$(CXX) $(CXXFLAGS) -Itests/cpp -o $@ $< -L$(LIBDIR) -lnewsched -lnsh_hip -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)'
 
-# RCCL test double for the remote edge's rccl transport on host rings (tests/test_remote_edge.py)
-build/tests/libfake_rccl.so: tests/cpp/fake_rccl.c
+# RCCL test double for the remote edge's rccl transport (rendezvous semantics on device rings,
+# tests/test_remote_edge.py, tests/test_bench.py)
+build/tests/libfake_rccl.so: tests/cpp/fake_rccl.hip
 	@mkdir -p build/tests
-	$(CC) -O2 -std=gnu11 -fPIC -shared -Wall -Wextra -pthread -o $@ $< -ldl
+	$(HIPCC) --offload-arch=$(ARCH) -O2 -std=c++17 -fPIC -shared -Wall -pthread -o $@ $<
 
 build/tools/%: tools/%.cpp $(LIBDIR)/libnewsched.so
 	@mkdir -p build/tools

@@ -166,7 +166,10 @@ def run_c5(a, dist, backend, rank, world, device, torch, orc, nsr):
                 for _ in range(4):
                     y_ref = orc.fir_ccf(y_ref, taps, decim=2)
                 ok, err, _ = orc.tol_ok(pipe.tail(m), y_ref[-m:])
-            box.update(ok=ok, err=err, tr=pipe.transport(), status=0.0)
+            tr = pipe.transport()
+            if "rccl" in tr:
+                tr += " [%s]" % (nsr.rccl_library() or "?")
+            box.update(ok=ok, err=err, tr=tr, status=0.0)
         except Exception as e:  # reported, not fatal: the headline is already measured
             box.update(status=1.0, error=str(e)[:300])
 
@@ -311,7 +314,7 @@ def main():
     ap.add_argument("--min-warmup-s", type=float, default=1.0,
                     help="keep warming up (untimed runs) until this long has passed: clocks settle")
     ap.add_argument("--log2n", type=int, default=28)
-    ap.add_argument("--algo", default="auto", choices=["auto", "mfma", "mfma_x3", "mfma16", "mfma_f32", "direct"])
+    ap.add_argument("--algo", default="auto", choices=["auto", "mfma", "mfma_f32", "direct"])
     ap.add_argument("--fp32-leg", choices=["on", "off"], default="on",
                     help="also time the exact-fp32 matrix form (NSH_FIR_MFMA_F32) on the same flowgraph")
     ap.add_argument("--out-buf-mib", type=int, default=2048, help="FIR output hip_buffer (default: one launch per 2^28-sample step)")
@@ -375,8 +378,7 @@ def main():
     from newsched_amd import nsh, nsr
     from oracle import oracle as orc  # checker only: tail parity + CPU-baseline inputs
 
-    algo = {"auto": nsh.FIR_AUTO, "mfma": nsh.FIR_MFMA, "mfma16": nsh.FIR_MFMA16, "mfma_x3": nsh.FIR_MFMA_BF16X3,
-            "mfma_f32": nsh.FIR_MFMA_F32, "direct": nsh.FIR_DIRECT}[a.algo]
+    algo = {"auto": nsh.FIR_AUTO, "mfma": nsh.FIR_MFMA, "mfma_f32": nsh.FIR_MFMA_F32, "direct": nsh.FIR_DIRECT}[a.algo]
     n = 1 << a.log2n
     taps = firwin(127, 0.2)
     first = rank * n  # this rank's time shard
@@ -399,8 +401,7 @@ def main():
     st0 = fb.stats()  # cumulative HIP-event kernel time / samples of the FIR's timed launches
     launches0 = st0["launches"]
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        fb.run()
+    fb.run(a.steps)  # K complete flowgraph runs, looped in C (no Python between steps)
     barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
@@ -410,7 +411,7 @@ def main():
     st = fb.stats()
     kms = st["kernel_ms"] - st0["kernel_ms"]
     samples = st["samples"] - st0["samples"]
-    algo_used = {1: "direct", 2: "mfma", 3: "mfma16", 4: "mfma_x3", 5: "mfma_f32"}.get(st["algo"], str(st["algo"]))
+    algo_used = {1: "direct", 2: "mfma", 5: "mfma_f32"}.get(st["algo"], str(st["algo"]))
     kernel = st["kernel"]
     timed_launches = st["launches"] - launches0
     launches_per_run = timed_launches / a.steps
@@ -431,6 +432,9 @@ def main():
         ok, err = r[0].item() == 0.0, float(r[1].item())
 
     value = world * n * a.steps / elapsed / 1e6  # MSamples/s, whole job
+    step_us = elapsed / a.steps * 1e6
+    # the flowgraph's own fraction (16 B x samples per step over the whole step, host overhead
+    # included) next to the kernel's; the difference is the per-run start / drain overhead
     out = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -467,6 +471,9 @@ def main():
             "avg_launch_us": round(avg_launch_ms * 1e3, 2),
             "algorithmic_bytes_per_launch": int(BYTES_PER_SAMPLE * per_launch_samples),
             "kernel_gflops": round(FLOP_PER_SAMPLE * per_launch_samples / (avg_launch_ms * 1e-3) / 1e9, 1),
+            "flowgraph_achieved": round(BYTES_PER_SAMPLE * n / (step_us * 1e-6) / 1e9, 1),
+            "flowgraph_frac": round(BYTES_PER_SAMPLE * n / (step_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+            "overhead_us_per_step": round(step_us - avg_launch_ms * 1e3 * launches_per_run, 2),
         },
         "parity": {"check": "last 4096 outputs of the last step vs oracle (double accumulation), every rank",
                    "max_abs_err": err, "scale": scale, "ok": bool(ok)},
@@ -492,7 +499,7 @@ def main():
     if rank == 0 and world == 1 and not a.no_cpu:
         ncpu = 1 << a.cpu_log2n
         xs = orc.synth(1 << 20)  # vector_source data (repeated)
-        secs = nsr.cpu_fir_run(taps, xs, ncpu, fixed_buf_size=32768)
+        secs, threads = nsr.cpu_fir_run(taps, xs, ncpu, fixed_buf_size=32768, with_threads=True)
         try:
             affinity = len(os.sched_getaffinity(0))
         except (AttributeError, OSError):
@@ -500,15 +507,15 @@ def main():
         out["cpu_baseline"] = {
             "value": round(ncpu / secs / 1e6, 2),
             "unit": "MSamples/s",
-            "cores": 4,  # threads the run used: scheduler_mt's thread per block, 4 blocks
-            "threads": 4,
+            "cores": threads,  # threads the run used (scheduler_mt: one per block), as the run reports them
+            "threads": threads,
             "fir_cores": 1,  # the FIR block's work() runs on its one thread
             "nproc": os.cpu_count(),
             "cpus_allowed": affinity,
             "kind": "port",
             "sample": "2^%d samples through vector_source->head->fir_filter_ccf(127 taps, AVX-512 fp32)->null_sink, "
-                      "scheduler_mt thread-per-block (4 threads; the FIR on one core), vmcircbuf 32768 B default buffers; "
-                      "%.2f s on %s" % (a.cpu_log2n, secs, cpu_model()),
+                      "scheduler_mt thread-per-block (%d threads; the FIR on one core), vmcircbuf 32768 B default buffers; "
+                      "%.2f s on %s" % (a.cpu_log2n, threads, secs, cpu_model()),
         }
     if dist is not None and not abandoned:
         dist.barrier()

@@ -136,9 +136,8 @@ int nsh_synth_cf32(float* out, int64_t n, uint64_t first_index, uint64_t seed, v
  * more than the split holds takes the exact-fp32 matrix tile of NSH_FIR_MFMA_F32 (fp32 products
  * and sums; the decimators filter it undecimated and keep every decim-th output), and one
  * holding inf/NaN the fp32 direct form (exact IEEE semantics), inside the same launch;
- * NSH_FIR_MFMA16 is the bf16x3 form on 16-sample blocks (decim 1,
- * ntaps <= 145); NSH_FIR_MFMA_BF16X3 forces the bf16x3 six-product kernel for decim 1;
- * NSH_FIR_MFMA_F32 is the exact-fp32 Toeplitz form on the fp32-input matrix instructions
+ * NSH_FIR_MFMA16 (3) and NSH_FIR_MFMA_BF16X3 (4) name bf16x3 kernels retired in round 4: plan
+ * creation refuses them; NSH_FIR_MFMA_F32 is the exact-fp32 Toeplitz form on the fp32-input matrix instructions
  * (decim 1, ntaps <= 257, finite taps; no operand split: fp32 products and sums, chunks with
  * inf/NaN through the fp32 direct form in the same launch). NSH_FIR_PFFT (decim 8 and 16; AUTO
  * picks it there when ceil((ntaps-1)/decim) <= 256 and the taps are finite): the polyphase-FFT
@@ -155,28 +154,11 @@ enum nsh_fir_algo {
     NSH_FIR_PFFT = 6
 };
 int nsh_fir_plan_create(int dev, const float* taps_host, int ntaps, int decim, int algo, void** plan);
-/* 1 when this library was built with the superseded FIR kernels (make LEGACY=1): NSH_FIR_MFMA16,
- * NSH_FIR_MFMA_BF16X3, the NSH_FIR_MFMA_VARIANT tuning variants and nsh_fir_cascade2_ccf; else 0,
- * and those fail with "not built" (plan creation / the call). */
-int nsh_fir_legacy_available(void);
 int nsh_fir_plan_destroy(void* plan);
 int nsh_fir_plan_algo(void* plan);          /* the algorithm AUTO resolved to */
 const char* nsh_fir_plan_kernel(void* plan); /* the kernel nsh_fir_ccf launches, e.g. "k_fir_mfma12<5>" */
 int nsh_fir_ccf(void* plan, const float* in, const float* hist_in, float* hist_out,
                 float* out, int64_t n_out, void* stream);
-
-/* Two decimate-by-2 FIRs in one pass (the fused form of fir_filter_ccf(h1, 2) ->
- * fir_filter_ccf(h2, 2); replaces two nsh_fir_ccf calls; scheduler_hip's fusion pass does not
- * use it: it measured no faster than the two launches): y1[i] = sum_k h1[k] x[2i - k], y2[m] = sum_k h2[k] y1[2m - k].
- * plan1/plan2 are decim-2 NSH_FIR_MFMA (or AUTO-resolved MFMA) plans on the same device;
- * in = 4 n_out samples; hist1 = ntaps1-1 x samples, hist2 = ntaps2-1 y1 samples, each an
- * in/out pair as for nsh_fir_ccf (no aliasing). Outputs within the fp16x2 MFMA tolerance of
- * the two-call chain (stage 1's outputs are not rounded through HBM: they are the same fp32
- * values; a NULL hist*_in reads as zeros). nsh_fir_cascade2_supported returns 1 when the pair
- * qualifies. */
-int nsh_fir_cascade2_supported(void* plan1, void* plan2);
-int nsh_fir_cascade2_ccf(void* plan1, void* plan2, const float* in, const float* hist1_in, float* hist1_out,
-                         const float* hist2_in, float* hist2_out, float* out, int64_t n_out, void* stream);
 
 /* Decimating FIR chain in one pass (the fused form of nstages fir_filter_ccf(h_s, D_s) blocks in
  * a chain; BASELINE config C5 = 4 x fir_filter_ccf(firwin(127, 0.45), 2); replaces nstages

@@ -31,6 +31,8 @@ const char* nsr_last_error(void);
 int nsr_fir_bench_create(int dev, const float* taps, int ntaps, int algo, int64_t n, uint64_t first_index,
                          uint64_t seed, size_t out_buf_bytes, int timing, void** handle);
 int nsr_fir_bench_run(void* handle); /* one run (start + wait); rethrown work() errors -> rc */
+/* `count` runs back to back (each a complete fg->run(): start, every work(), drain), looped in C. */
+int nsr_fir_bench_runs(void* handle, int64_t count);
 /* Cumulative over every run since create (callers take differences around the runs they
  * time): summed FIR kernel time from HIP events around each launch on the partition stream,
  * FIR launches, samples, and the algorithm the plan resolved to. */
@@ -57,6 +59,8 @@ int nsr_c5_create(int group, int n_groups, int dev, const float* taps, int ntaps
 int nsr_c5_run(void* handle);
 /* The transports this process's crossings negotiated, e.g. "send1:rccl,recv0:rccl". */
 int nsr_c5_transport(void* handle, char* buf, int len);
+/* The librccl file this process's rccl crossings bound (dladdr of ncclSend), "" if none. */
+int nsr_rccl_library(char* buf, int len);
 /* The last `count` outputs of the last run -> host (only the process of group n_groups-1). */
 int nsr_c5_tail(void* handle, int64_t count, float* out_host);
 int nsr_c5_destroy(void* handle);
@@ -66,7 +70,7 @@ int nsr_c5_destroy(void* handle);
  *   vector_source(x[0..nx), repeat) -> head(n) -> blocks::fir_filter_ccf -> null_sink
  * *seconds = wall time of fg->run() (threads already created). */
 int nsr_cpu_fir_run(const float* taps, int ntaps, const float* x, int64_t nx, int64_t n, size_t fixed_buf_size,
-                    double* seconds);
+                    double* seconds, int* threads);  /* *threads: scheduler_mt threads the run used */
 
 #ifdef __cplusplus
 }

@@ -157,6 +157,14 @@ int nsr_fir_bench_run(void* handle)
     return guarded([&] { static_cast<fir_bench*>(handle)->fg->run(); });
 }
 
+int nsr_fir_bench_runs(void* handle, int64_t count)
+{
+    return guarded([&] {
+        auto fg = static_cast<fir_bench*>(handle)->fg;
+        for (int64_t i = 0; i < count; ++i) fg->run();
+    });
+}
+
 int nsr_fir_bench_stats(void* handle, double* kernel_ms, uint64_t* launches, uint64_t* samples, int* algo)
 {
     return guarded([&] {
@@ -274,6 +282,16 @@ int nsr_c5_transport(void* handle, char* buf, int len)
     });
 }
 
+int nsr_rccl_library(char* buf, int len)
+{
+    return guarded([&] {
+        if (len <= 0 || !buf) throw std::invalid_argument("nsr_rccl_library: len");
+        const std::string p = domain_adapter_remote::rccl_library();
+        std::strncpy(buf, p.c_str(), (size_t)len - 1);
+        buf[len - 1] = 0;
+    });
+}
+
 int nsr_c5_tail(void* handle, int64_t count, float* out_host)
 {
     return guarded([&] {
@@ -289,7 +307,7 @@ int nsr_c5_destroy(void* handle)
 }
 
 int nsr_cpu_fir_run(const float* taps, int ntaps, const float* x, int64_t nx, int64_t n, size_t fixed_buf_size,
-                    double* seconds)
+                    double* seconds, int* threads)
 {
     return guarded([&] {
         std::vector<gr_complex> xv((const gr_complex*)x, (const gr_complex*)x + nx);
@@ -301,8 +319,10 @@ int nsr_cpu_fir_run(const float* taps, int ntaps, const float* x, int64_t nx, in
         fg->connect(src, 0, head, 0);
         fg->connect(head, 0, fir, 0);
         fg->connect(fir, 0, snk, 0);
-        fg->set_scheduler(schedulers::scheduler_mt::make("mt", (unsigned)fixed_buf_size));
+        auto sched = schedulers::scheduler_mt::make("mt", (unsigned)fixed_buf_size);
+        fg->set_scheduler(sched);
         fg->validate();
+        if (threads) *threads = (int)sched->num_threads(); // thread per block (reference scheduler_mt)
         const auto t0 = std::chrono::steady_clock::now();
         fg->run();
         *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();

@@ -14,10 +14,12 @@
 //    staged samples; taps come from the scalar cache (s_load, uniform index). LDS rows
 //    are padded by one sample every R*D samples so the per-lane ds_read_b64 of the window
 //    is bank-conflict-free. Exact fp32 products, fp32 accumulation in tap order.
-//  * MFMA / MFMA16 / MFMA_BF16X3 -- split-precision Toeplitz MFMA (nsh_fir_mfma.hip):
-//    decim 1 on 32-sample blocks as scaled fp16x2 (default, k_fir_mfma12; k_fir_mfma9 as
-//    NSH_FIR_MFMA_VARIANT=9) or bf16x3, on 16-sample blocks as bf16x3; decim 2 and 4 as the
-//    polyphase fp16x2 form (k_fir_mfma11). Decim 8 and above: DIRECT.
+//  * MFMA -- split-precision Toeplitz MFMA (nsh_fir_mfma.hip): decim 1 on 32-sample blocks as
+//    scaled fp16x2 (k_fir_mfma12), decim 2 and 4 as the polyphase fp16x2 form (k_fir_mfma11).
+//  * MFMA_F32 -- exact fp32 Toeplitz MFMA (nsh_fir_f32.hip); PFFT -- decim 8 / 16 by
+//    polyphase-FFT overlap-save (nsh_fir_pfft.hip). Decim 8 otherwise: DIRECT.
+//  NSH_FIR_MFMA16 / NSH_FIR_MFMA_BF16X3 name kernels retired in round 4 (DESIGN.md section 4
+//  keeps their measurements): plan creation refuses them.
 #include "nsh_common.hpp"
 
 #include <algorithm>
@@ -173,11 +175,13 @@ int nsh_fir_plan_create(int dev, const float* taps_host, int ntaps, int decim, i
         delete p;
         return nsh::fail_msg("nsh_fir_plan_create: unknown algorithm");
     }
-    int resolved = algo;
-    if (algo == NSH_FIR_MFMA_BF16X3) {
-        resolved = NSH_FIR_MFMA;
-        p->force_x3 = true;
+    if (algo == NSH_FIR_MFMA16 || algo == NSH_FIR_MFMA_BF16X3) {
+        (void)hipFree(p->taps_dev);
+        delete p;
+        return nsh::fail_msg("nsh_fir_plan_create: the MFMA16 / MFMA_BF16X3 kernels were retired (use NSH_FIR_MFMA or "
+                             "NSH_FIR_MFMA_F32)");
     }
+    int resolved = algo;
     // decim 8 and 16: the polyphase-FFT kernel (k_fir_pfft; 2x the direct form at 127 taps, 5x at
     // 511) when the filter fits its 256 overlap rows, else the direct form (decim 8 only)
     const bool pfft_ok = (decim == 8 || decim == 16) && (ntaps - 1 + decim - 1) / decim <= 256 &&
@@ -204,12 +208,6 @@ int nsh_fir_plan_create(int dev, const float* taps_host, int ntaps, int decim, i
         *plan = p;
         return 0;
     }
-    if (resolved == NSH_FIR_MFMA16 && !nsh_fir_mfma16_supported(p)) {
-        (void)hipFree(p->taps_dev);
-        delete p;
-        return nsh::fail_msg(nsh_fir_legacy_built() ? "nsh_fir_plan_create: MFMA16 form needs decim 1, finite taps and ntaps <= 145"
-                                                    : "nsh_fir_plan_create: MFMA16 is a legacy kernel, not built (make LEGACY=1)");
-    }
     if (resolved == NSH_FIR_MFMA_F32) {
         const int rc = nsh_fir_f32_supported(p) ? nsh_fir_f32_prepare(p)
                                                 : nsh::fail_msg("nsh_fir_plan_create: MFMA_F32 form needs decim 1, finite taps and ntaps <= 257");
@@ -220,8 +218,8 @@ int nsh_fir_plan_create(int dev, const float* taps_host, int ntaps, int decim, i
             return rc;
         }
     }
-    if (resolved == NSH_FIR_MFMA || resolved == NSH_FIR_MFMA16) {
-        if (resolved == NSH_FIR_MFMA && !nsh_fir_mfma_supported(p)) {
+    if (resolved == NSH_FIR_MFMA) {
+        if (!nsh_fir_mfma_supported(p)) {
             (void)hipFree(p->taps_dev);
             delete p;
             return nsh::fail_msg("nsh_fir_plan_create: MFMA form needs finite taps and decim 1 with ntaps <= 161, "
@@ -234,7 +232,7 @@ int nsh_fir_plan_create(int dev, const float* taps_host, int ntaps, int decim, i
             return rc;
         }
     }
-    p->algo = p->force_x3 ? NSH_FIR_MFMA_BF16X3 : resolved;
+    p->algo = resolved;
     if (resolved == NSH_FIR_DIRECT) {
         static const int R[9] = { 0, 8, 8, 0, 4, 0, 0, 0, 2 };
         p->kernel = "k_fir_direct<" + std::to_string(p->D) + "," + std::to_string(R[p->D]) + ">";
@@ -247,20 +245,14 @@ int nsh_fir_plan_create(int dev, const float* taps_host, int ntaps, int decim, i
     return 0;
 }
 
-int nsh_fir_legacy_available(void) { return nsh_fir_legacy_built() ? 1 : 0; }
-
 int nsh_fir_plan_destroy(void* plan)
 {
     auto* p = static_cast<nsh_fir_plan*>(plan);
     if (!p) return 0;
     if (p->taps_dev) (void)hipFree(p->taps_dev);
-    if (p->frag_dev) (void)hipFree(p->frag_dev);
-    if (p->frag16_dev) (void)hipFree(p->frag16_dev);
-    if (p->frag8_dev) (void)hipFree(p->frag8_dev);
     if (p->frag12_dev) (void)hipFree(p->frag12_dev);
     if (p->tf32_dev) (void)hipFree(p->tf32_dev);
     if (p->tf32q_dev) (void)hipFree(p->tf32q_dev);
-    if (p->fragd_dev) (void)hipFree(p->fragd_dev);
     if (p->fragd8_dev) (void)hipFree(p->fragd8_dev);
     if (p->casc) nsh_fir_cascade_plan_destroy(p->casc);
     delete p;
@@ -281,34 +273,11 @@ int nsh_fir_ccf(void* plan, const float* in, const float* hist_in, float* hist_o
     if (p->algo == NSH_FIR_PFFT) return nsh_fir_cascade_ccf(p->casc, in, hist_in, hist_out, out, n_out, stream);
     // every kernel but the polyphase-FFT one writes the next call's history unconditionally
     if (!hist_out && p->L > 1) return nsh::fail_msg("nsh_fir_ccf: hist_out is required (ntaps-1 samples)");
-    if (p->algo == NSH_FIR_MFMA || p->algo == NSH_FIR_MFMA_BF16X3)
+    if (p->algo == NSH_FIR_MFMA)
         return nsh_fir_mfma_run(p, (const float2*)in, (const float2*)hist_in, (float2*)hist_out, (float2*)out, n_out, s);
     if (p->algo == NSH_FIR_MFMA_F32)
         return nsh_fir_f32_run(p, (const float2*)in, (const float2*)hist_in, (float2*)hist_out, (float2*)out, n_out, s);
-    if (p->algo == NSH_FIR_MFMA16)
-        return nsh_fir_mfma16_run(p, (const float2*)in, (const float2*)hist_in, (float2*)hist_out, (float2*)out, n_out, s);
     return run_direct(p, (const float2*)in, (const float2*)hist_in, (float2*)hist_out, (float2*)out, n_out, s);
-}
-
-int nsh_fir_cascade2_supported(void* plan1, void* plan2)
-{
-    return nsh_fir_cascade2_ok(static_cast<nsh_fir_plan*>(plan1), static_cast<nsh_fir_plan*>(plan2)) ? 1 : 0;
-}
-
-int nsh_fir_cascade2_ccf(void* plan1, void* plan2, const float* in, const float* hist1_in, float* hist1_out,
-                         const float* hist2_in, float* hist2_out, float* out, int64_t n_out, void* stream)
-{
-    auto* p1 = static_cast<nsh_fir_plan*>(plan1);
-    auto* p2 = static_cast<nsh_fir_plan*>(plan2);
-    if (!nsh_fir_cascade2_ok(p1, p2))
-        return nsh::fail_msg("nsh_fir_cascade2_ccf: plans must be decim-2 fp16x2 MFMA plans (3 <= ceil((ntaps/2+1)/16)+1 <= 6) on one device");
-    if (n_out <= 0) return 0;
-    if (!in || !out || !hist1_out || !hist2_out) return nsh::fail_msg("nsh_fir_cascade2_ccf: null pointer");
-    if (n_out > ((int64_t)1 << 40)) return nsh::fail_msg("nsh_fir_cascade2_ccf: n_out too large");
-    if (hist1_in == hist1_out || hist2_in == hist2_out)
-        return nsh::fail_msg("nsh_fir_cascade2_ccf: hist_out must not alias hist_in");
-    return nsh_fir_cascade2_run(p1, p2, (const float2*)in, (const float2*)hist1_in, (float2*)hist1_out,
-                                (const float2*)hist2_in, (float2*)hist2_out, (float2*)out, n_out, nsh::S(stream));
 }
 
 } // extern "C"

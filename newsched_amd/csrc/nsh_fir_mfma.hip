@@ -18,9 +18,8 @@
 //
 // The forms this file superseded -- k_fir_mfma2 (bf16x3, six products), k_fir_mfma5 (16-sample
 // blocks), k_fir_mfma7 (bf16x3 decimator), k_fir_mfma9 (v12's predecessor) and k_fir_casc2 (two
-// decimators fused) -- and their timing-only ablation hooks live in legacy/nsh_fir_legacy.hip,
-// compiled only by `make LEGACY=1` (their algorithms / variants report "not built" otherwise;
-// tests marked `legacy`). DESIGN.md section 4 keeps their measurements.
+// decimators fused) -- were retired in round 4 (git history before that round has them);
+// DESIGN.md section 4 keeps their measurements.
 #include "nsh_fir_mfma_shared.hpp"
 #include "nsh_fir_f32_tile.hpp"
 
@@ -781,40 +780,7 @@ int launch_v12(const nsh_fir_plan* p, const float2* in, const float2* hin, float
 }
 
 
-// A plan runs a legacy kernel (legacy/nsh_fir_legacy.hip) when it asks for the 16-sample form,
-// the bf16x3 form, or a tuning variant other than the default (NSH_FIR_MFMA_VARIANT = 0 / 12 for
-// decim 1; 7 selects k_fir_mfma7 for decim 2 / 4).
-bool uses_legacy(const nsh_fir_plan* p)
-{
-    if (p->algo == NSH_FIR_MFMA16 || p->force_x3) return true;
-    if (p->D > 1) return p->variant == 7;
-    return p->variant != 0 && p->variant != 12;
-}
-
 } // namespace
-
-// Legacy hooks: weak stubs here, the real definitions in legacy/nsh_fir_legacy.hip (linked only
-// by `make LEGACY=1`, where its strong symbols take precedence).
-__attribute__((weak)) bool nsh_fir_legacy_built() { return false; }
-__attribute__((weak)) int nsh_fir_legacy_prepare(nsh_fir_plan*) { return 0; }
-__attribute__((weak)) int nsh_fir_legacy_run(const nsh_fir_plan*, const float2*, const float2*, float2*, float2*, int64_t,
-                                             hipStream_t)
-{
-    return nsh::fail_msg("nsh_fir_ccf: legacy FIR kernels are not built (make LEGACY=1)");
-}
-__attribute__((weak)) std::string nsh_fir_legacy_kernel_name(const nsh_fir_plan*) { return "(legacy kernel not built)"; }
-__attribute__((weak)) bool nsh_fir_mfma16_supported(const nsh_fir_plan*) { return false; }
-__attribute__((weak)) int nsh_fir_mfma16_run(const nsh_fir_plan*, const float2*, const float2*, float2*, float2*, int64_t,
-                                             hipStream_t)
-{
-    return nsh::fail_msg("nsh_fir_ccf: the MFMA16 form is a legacy kernel, not built (make LEGACY=1)");
-}
-__attribute__((weak)) bool nsh_fir_cascade2_ok(const nsh_fir_plan*, const nsh_fir_plan*) { return false; }
-__attribute__((weak)) int nsh_fir_cascade2_run(const nsh_fir_plan*, const nsh_fir_plan*, const float2*, const float2*,
-                                               float2*, const float2*, float2*, float2*, int64_t, hipStream_t)
-{
-    return nsh::fail_msg("nsh_fir_cascade2_ccf: k_fir_casc2 is a legacy kernel, not built (make LEGACY=1)");
-}
 
 bool nsh_fir_mfma_supported(const nsh_fir_plan* p)
 {
@@ -892,19 +858,11 @@ int nsh_fir_mfma_prepare_decim(nsh_fir_plan* p)
         NSH_CK(hipMemcpy(p->fragd8_dev, f8.data(), f8.size() * sizeof(_Float16), hipMemcpyHostToDevice));
     }
     NSH_CK(f32_tile_image(p, D * (QH - 1) + 1)); // geom11x::QF: the whole D H-sample halo
-    return nsh_fir_legacy_prepare(p); // legacy builds: k_fir_mfma7's bf16x3 fragments
+    return 0;
 }
 
 int nsh_fir_mfma_prepare(nsh_fir_plan* p)
 {
-    if (const char* v = std::getenv("NSH_FIR_MFMA_VARIANT")) p->variant = std::atoi(v);
-    if (const char* v = std::getenv("NSH_FIR_WG_PER_CU")) { // A/B only
-        const int w = std::atoi(v);
-        if (w >= 1 && w <= 64) p->wg_per_cu = w;
-    }
-    if (uses_legacy(p) && !nsh_fir_legacy_built())
-        return nsh::fail_msg("nsh_fir_plan_create: this algorithm / NSH_FIR_MFMA_VARIANT is a legacy kernel, not built "
-                             "(make LEGACY=1)");
     if (p->D > 1) return nsh_fir_mfma_prepare_decim(p);
     const int Q = (p->L + 30) / 32 + 1;
     p->Q = Q;
@@ -938,12 +896,11 @@ int nsh_fir_mfma_prepare(nsh_fir_plan* p)
             NSH_CK(hipMemcpy(p->frag12_dev, f12.data(), f12.size() * sizeof(_Float16), hipMemcpyHostToDevice));
     }
     NSH_CK(f32_tile_image(p, 2 * Q - 1)); // k_fir_mfma12's tile: v12's 32 (Q - 1)-sample halo
-    return nsh_fir_legacy_prepare(p); // legacy builds: the bf16x3 / v9 / 16-sample fragments
+    return 0;
 }
 
 std::string nsh_fir_mfma_kernel_name(const nsh_fir_plan* p)
 {
-    if (uses_legacy(p)) return nsh_fir_legacy_kernel_name(p);
     auto t = [](const char* k, int a, int b = -1) {
         return std::string(k) + "<" + std::to_string(a) + (b >= 0 ? "," + std::to_string(b) : std::string()) + ">";
     };
@@ -953,7 +910,6 @@ std::string nsh_fir_mfma_kernel_name(const nsh_fir_plan* p)
 
 int nsh_fir_mfma_run(const nsh_fir_plan* p, const float2* in, const float2* hist_in, float2* hist_out, float2* out, int64_t n_out, hipStream_t s)
 {
-    if (uses_legacy(p)) return nsh_fir_legacy_run(p, in, hist_in, hist_out, out, n_out, s);
     if (p->D == 2) return launch_dec<2>(p, in, hist_in, hist_out, out, n_out, s);
     if (p->D == 4) return launch_dec<4>(p, in, hist_in, hist_out, out, n_out, s);
     switch (p->Q) {

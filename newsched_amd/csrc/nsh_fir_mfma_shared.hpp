@@ -1,7 +1,5 @@
-// Helpers shared by the FIR matrix-core kernels: nsh_fir_mfma.hip (the product kernels,
-// k_fir_mfma12 for decim 1 and k_fir_mfma11 for decim 2 / 4) and legacy/nsh_fir_legacy.hip
-// (superseded forms, built only with `make LEGACY=1`). Device helpers only, in an anonymous
-// namespace: each translation unit gets its own copy.
+// Helpers of the FIR matrix-core kernels (nsh_fir_mfma.hip: k_fir_mfma12 for decim 1 and
+// k_fir_mfma11 for decim 2 / 4). Device helpers only, in an anonymous namespace.
 #pragma once
 #include "nsh_common.hpp"
 #include "nsh_fir_plan.hpp"

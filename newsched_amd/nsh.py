@@ -16,7 +16,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_DIR = os.path.join(_HERE, "lib")
 HIP_LIB = os.path.join(LIB_DIR, "libnsh_hip.so")
-# NSH_HIP_LIB: another build of the library (e.g. the `make LEGACY=1` one, for its legacy tests)
+# NSH_HIP_LIB: another build of the library (A/B probes)
 HIP_LIB = os.environ.get("NSH_HIP_LIB") or HIP_LIB
 
 NSH_H2D, NSH_D2H, NSH_D2D, NSH_DEFAULT = 0, 1, 2, 3
@@ -63,13 +63,10 @@ SIGNATURES = {
     "nsh_mul_const_vcc": (_i, [_vp, _vp, _vp, _i, _i64, _vp]),
     "nsh_synth_cf32": (_i, [_vp, _i64, _u64, _u64, _vp]),
     "nsh_fir_plan_create": (_i, [_i, C.POINTER(_f), _i, _i, _i, C.POINTER(_vp)]),
-    "nsh_fir_legacy_available": (_i, []),
     "nsh_fir_plan_destroy": (_i, [_vp]),
     "nsh_fir_plan_algo": (_i, [_vp]),
     "nsh_fir_plan_kernel": (C.c_char_p, [_vp]),
     "nsh_fir_ccf": (_i, [_vp, _vp, _vp, _vp, _vp, _i64, _vp]),
-    "nsh_fir_cascade2_supported": (_i, [_vp, _vp]),
-    "nsh_fir_cascade2_ccf": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp]),
     "nsh_fir_cascade_plan_create": (_i, [_i, C.POINTER(C.POINTER(_f)), C.POINTER(_i), C.POINTER(_i), _i,
                                          C.POINTER(_vp)]),
     "nsh_fir_cascade_plan_destroy": (_i, [_vp]),
@@ -170,11 +167,6 @@ def channelizer1024(x, y, w, nframes: int, stream=None):
           "nsh_channelizer1024")
 
 
-def fir_legacy_available() -> bool:
-    """True when libnsh_hip.so was built with the superseded FIR kernels (make LEGACY=1)."""
-    return lib().nsh_fir_legacy_available() == 1
-
-
 class FirPlan:
     """Device-resident FIR plan (taps uploaded/split once); see nsh_fir_ccf."""
 
@@ -195,16 +187,6 @@ class FirPlan:
     def __call__(self, x, hist_in, hist_out, y, n_out: int, stream=None):
         check(lib().nsh_fir_ccf(self._h, ptr(x), ptr(hist_in), ptr(hist_out), ptr(y), n_out,
                                 stream_ptr(stream)), "nsh_fir_ccf")
-
-    def cascade2_supported(self, stage2: "FirPlan") -> bool:
-        return bool(lib().nsh_fir_cascade2_supported(self._h, stage2._h))
-
-    def cascade2(self, stage2: "FirPlan", x, hist1_in, hist1_out, hist2_in, hist2_out, y, n_out: int,
-                 stream=None):
-        """self (decim 2) then stage2 (decim 2) in one launch: n_out outputs from 4 n_out inputs."""
-        check(lib().nsh_fir_cascade2_ccf(self._h, stage2._h, ptr(x), ptr(hist1_in), ptr(hist1_out),
-                                         ptr(hist2_in), ptr(hist2_out), ptr(y), n_out,
-                                         stream_ptr(stream)), "nsh_fir_cascade2_ccf")
 
     def close(self):
         if getattr(self, "_h", None):

@@ -19,6 +19,7 @@ SIGNATURES = {
     "nsr_last_error": (C.c_char_p, []),
     "nsr_fir_bench_create": (_i, [_i, C.POINTER(C.c_float), _i, _i, _i64, _u64, _u64, _sz, _i, C.POINTER(_vp)]),
     "nsr_fir_bench_run": (_i, [_vp]),
+    "nsr_fir_bench_runs": (_i, [_vp, _i64]),
     "nsr_fir_bench_stats": (_i, [_vp, C.POINTER(_d), C.POINTER(_u64), C.POINTER(_u64), C.POINTER(_i)]),
     "nsr_fir_bench_kernel": (C.c_char_p, [_vp]),
     "nsr_fir_bench_tail": (_i, [_vp, _i64, C.POINTER(C.c_float)]),
@@ -29,7 +30,9 @@ SIGNATURES = {
     "nsr_c5_transport": (_i, [_vp, C.c_char_p, _i]),
     "nsr_c5_tail": (_i, [_vp, _i64, C.POINTER(C.c_float)]),
     "nsr_c5_destroy": (_i, [_vp]),
-    "nsr_cpu_fir_run": (_i, [C.POINTER(C.c_float), _i, C.POINTER(C.c_float), _i64, _i64, _sz, C.POINTER(_d)]),
+    "nsr_cpu_fir_run": (_i, [C.POINTER(C.c_float), _i, C.POINTER(C.c_float), _i64, _i64, _sz, C.POINTER(_d),
+                             C.POINTER(_i)]),
+    "nsr_rccl_library": (_i, [C.c_char_p, _i]),
 }
 
 
@@ -69,8 +72,13 @@ class FirBench:
                                          out_buf_bytes, 1 if timing else 0, C.byref(h)), "nsr_fir_bench_create")
         self._h = h
 
-    def run(self):
-        check(lib().nsr_fir_bench_run(self._h), "nsr_fir_bench_run")
+    def run(self, count: int = 1):
+        """count back-to-back flowgraph runs (fg->run() each; a loop in C for count > 1: no
+        Python between runs)."""
+        if count == 1:
+            check(lib().nsr_fir_bench_run(self._h), "nsr_fir_bench_run")
+        else:
+            check(lib().nsr_fir_bench_runs(self._h, int(count)), "nsr_fir_bench_runs")
 
     def stats(self):
         ms, la, sa, al = C.c_double(), C.c_uint64(), C.c_uint64(), C.c_int()
@@ -133,10 +141,19 @@ class C5Pipeline:
             pass
 
 
-def cpu_fir_run(taps, x, n, fixed_buf_size=32768) -> float:
+def cpu_fir_run(taps, x, n, fixed_buf_size=32768, with_threads=False):
+    """Seconds of the CPU scheduler_mt FIR run (and the threads it used, with_threads=True)."""
     t = np.ascontiguousarray(np.asarray(taps, np.float32))
     xv = np.ascontiguousarray(np.asarray(x, np.complex64))
     s = C.c_double()
+    th = C.c_int()
     check(lib().nsr_cpu_fir_run(_f32p(t), t.size, _f32p(xv.view(np.float32)), xv.size, int(n), fixed_buf_size,
-                                C.byref(s)), "nsr_cpu_fir_run")
-    return s.value
+                                C.byref(s), C.byref(th)), "nsr_cpu_fir_run")
+    return (s.value, th.value) if with_threads else s.value
+
+
+def rccl_library() -> str:
+    """The librccl file this process's rccl crossings bound ("" if none)."""
+    buf = C.create_string_buffer(1024)
+    check(lib().nsr_rccl_library(buf, 1024), "nsr_rccl_library")
+    return buf.value.decode()

@@ -116,10 +116,14 @@ public:
     int crossing() const { return _crossing; }
     std::string transport_kind() const;
     uint64_t items_moved() const { return _moved.load(); }
+    // The librccl file the rccl transport bound in this process (dladdr of ncclSend; "" before
+    // the first rccl crossing): an already-loaded copy (torch's) if any, else /opt/rocm's.
+    static std::string rccl_library();
 
 private:
     domain_adapter_remote(remote_role role, int crossing, const remote_edge_options& opt);
     void pump();           // SEND: forward everything readable in the local ring
+    void pump_locked();    // SEND: pump's loop (under _pump_m)
     void release_span(int m, bool deferred); // SEND: the edge's release rule (see pump)
     bool read_reverse(int timeout_ms);       // SEND: one reverse message, if any
     void poll_reverse();   // SEND: consume reverse messages (READER_DONE, transport credits)

@@ -20,6 +20,8 @@
 #include <deque>
 #include <functional>
 #include <map>
+#include <set>
+#include <cstdio>
 #include <stdexcept>
 
 namespace gr {
@@ -72,6 +74,15 @@ int32_t transport_code(const std::string& s)
 }
 using clk = std::chrono::steady_clock;
 double since(clk::time_point t0) { return std::chrono::duration<double>(clk::now() - t0).count(); }
+
+// Test hooks are environment-gated; each one says so on stderr once per process when it acts.
+void test_hook_notice(const char* var, const char* value)
+{
+    static std::mutex m;
+    static std::set<std::string> seen;
+    std::lock_guard<std::mutex> g(m);
+    if (seen.insert(var).second) std::fprintf(stderr, "newsched remote edge: test hook %s=%s active\n", var, value);
+}
 
 // ---- tags on the wire: the tags of a DATA message's items travel with it ----------------
 // record = u64 offset relative to the message's first item, then key, value, srcid as
@@ -379,13 +390,14 @@ public:
         l.unlock();
         rethrow();
     }
-
-private:
+    // the first failed job's exception, if any (a failed job skips every later one)
     void rethrow()
     {
         std::lock_guard<std::mutex> g(_m);
         if (_err) std::rethrow_exception(_err);
     }
+
+private:
     void loop()
     {
         std::unique_lock<std::mutex> l(_m);
@@ -486,6 +498,7 @@ public:
         _delay_us = d ? std::atoi(d) : 2000;
         const char* e = std::getenv("NSH_REMOTE_TEST_EARLY_RELEASE");
         _early = e && *e == '1';
+        if (_early) test_hook_notice("NSH_REMOTE_TEST_EARLY_RELEASE", "1 (negative control: unsafe release)");
     }
     ~deferred_test_transport() override
     {
@@ -542,7 +555,9 @@ uint64_t deferred_test_violations() { return deferred_test_transport::g_violatio
 // thread once that event has completed, so the receiver never reads a slot before it landed.
 // Receiver: one local D2D copy from the slot into its ring on its own stream, then
 // M_SLOT_FREE(slot) once that copy is done. A sender with no free slot reads reverse messages
-// until one comes back.
+// until one comes back -- and fails instead of waiting forever when the outbox has failed (its
+// DATA headers are then skipped, so no slot would ever be freed), the adapter is closing, or
+// no slot came back within the edge's timeout.
 class p2p_transport : public transport
 {
 public:
@@ -563,9 +578,15 @@ public:
     }
     // sender side: map the receiver's slots; read_reverse(block) reads and dispatches one
     // reverse message (false when none arrived)
-    p2p_transport(int device, const p2p_offer& offer, std::function<bool()> read_reverse)
-        : _sender(true), _device(device), _slot_bytes(offer.slot_bytes), _read_reverse(std::move(read_reverse))
+    p2p_transport(int device, const p2p_offer& offer, std::function<bool()> read_reverse,
+                  const std::atomic<bool>* closing, double timeout_s)
+        : _sender(true), _device(device), _slot_bytes(offer.slot_bytes), _read_reverse(std::move(read_reverse)),
+          _closing(closing), _timeout_s(timeout_s)
     {
+        if (const char* f = std::getenv("NSH_REMOTE_TEST_FAIL_OUTBOX"); f && *f) { // test hook (see send)
+            _fail_after = std::atoi(f);
+            test_hook_notice("NSH_REMOTE_TEST_FAIL_OUTBOX", f);
+        }
         if (offer.slots == 0 || offer.slots > 64) throw std::runtime_error("remote edge: p2p offer");
         hip::check(nsh_ipc_mem_open(device, offer.handle, &_remote), "remote edge: p2p map");
         _events.resize(offer.slots, nullptr);
@@ -594,6 +615,7 @@ public:
     {
         if (bytes > _slot_bytes) throw std::runtime_error("remote edge: p2p message larger than a slot");
         uint32_t slot;
+        const auto t0 = clk::now();
         for (;;) {
             {
                 std::lock_guard<std::mutex> g(_m);
@@ -603,6 +625,9 @@ public:
                     break;
                 }
             }
+            _box->rethrow(); // a failed DATA job: the receiver will never free a slot
+            if (_closing && _closing->load()) throw std::runtime_error("remote edge: p2p send while closing");
+            if (since(t0) > _timeout_s) throw std::runtime_error("remote edge: p2p: no landing slot freed within the timeout");
             _read_reverse(); // blocks briefly for a reverse message (M_SLOT_FREE)
         }
         void* s = hip::current_stream();
@@ -610,7 +635,9 @@ public:
                    "remote edge: p2p copy");
         void* ev = _events[slot];
         hip::check(nsh_event_record(ev, s), "remote edge: p2p event");
-        _box->push([&ch, n, ntags, blob, ev, slot] {
+        const bool fail = _fail_after >= 0 && _sent++ >= _fail_after; // test hook: this job fails
+        _box->push([&ch, n, ntags, blob, ev, slot, fail] {
+            if (fail) throw std::runtime_error("remote edge: p2p DATA job failed (NSH_REMOTE_TEST_FAIL_OUTBOX)");
             hip::check(nsh_event_sync(ev), "remote edge: p2p copy wait");
             write_data(ch, n, ntags, blob, [&] { ch.send_bytes(&slot, sizeof(slot)); });
         });
@@ -648,6 +675,10 @@ private:
     int _device;
     size_t _slot_bytes;
     std::function<bool()> _read_reverse;
+    const std::atomic<bool>* _closing = nullptr;
+    double _timeout_s = 120.0;
+    int _fail_after = -1; // test hook: DATA jobs from this one on fail
+    int _sent = 0;
     void* _local = nullptr;  // receiver: the slots
     void* _remote = nullptr; // sender: the receiver's slots, mapped
     std::vector<void*> _events;
@@ -656,8 +687,17 @@ private:
     std::unique_ptr<outbox> _box;
 };
 
+std::mutex g_rccl_path_m;
+std::string g_rccl_path;
+
 // RCCL point-to-point on the partition streams (device rings on different GPUs). librccl
-// is loaded on first use so that host-only builds and tests do not need it. Test hook:
+// is loaded on first use so that host-only builds and tests do not need it, deliberately: the
+// copy this process has already loaded if there is one (under torch that is torch's bundled
+// librccl, built against the HIP runtime torch loaded -- libamdhip64.so.7 has one SONAME, so that
+// is the runtime this library runs on too), else /opt/rocm's; the file actually bound is recorded
+// (dladdr of ncclSend, domain_adapter_remote::rccl_library(), bench's c5_pipeline). Asynchronous
+// communicator errors (ncclCommGetAsyncError) are checked before every call and at DONE / CLOSE,
+// so a failed transfer is an error of fg->run(), not a hang. Test hook:
 // NSH_RCCL_LIB names another library with the same five entry points (the tests load
 // build/tests/libfake_rccl.so, tests/cpp/fake_rccl.c: payloads over a Unix socket, read and
 // landed in stream order on device rings), and with NSH_REMOTE_TEST_RCCL=1 the receiver accepts
@@ -675,6 +715,8 @@ class rccl_transport : public transport
         int (*recv)(void*, size_t, int, int, void*, void*) = nullptr;
         int (*comm_destroy)(void*) = nullptr;
         const char* (*err_str)(int) = nullptr;
+        int (*async_error)(void*, int*) = nullptr; // ncclCommGetAsyncError (optional)
+        std::string path;                          // the file ncclSend came from
     };
     static api& lib()
     {
@@ -682,10 +724,12 @@ class rccl_transport : public transport
         static std::once_flag once;
         std::call_once(once, [] {
             if (const char* t = std::getenv("NSH_RCCL_LIB"); t && *t) {
+                test_hook_notice("NSH_RCCL_LIB", t);
                 a.h = dlopen(t, RTLD_NOW | RTLD_LOCAL); // test double (see above); no fallback
             } else {
-                a.h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+                a.h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD); // already in the process (torch's)
                 if (!a.h) a.h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+                if (!a.h) a.h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
             }
             if (!a.h) return;
             a.get_unique_id = (int (*)(void*))dlsym(a.h, "ncclGetUniqueId");
@@ -694,6 +738,11 @@ class rccl_transport : public transport
             a.send = (int (*)(const void*, size_t, int, int, void*, void*))dlsym(a.h, "ncclSend");
             a.recv = (int (*)(void*, size_t, int, int, void*, void*))dlsym(a.h, "ncclRecv");
             a.comm_init_rank = dlsym(a.h, "ncclCommInitRank");
+            a.async_error = (int (*)(void*, int*))dlsym(a.h, "ncclCommGetAsyncError");
+            Dl_info di{};
+            if (a.send && dladdr((void*)a.send, &di) && di.dli_fname) a.path = di.dli_fname;
+            std::lock_guard<std::mutex> g(g_rccl_path_m);
+            g_rccl_path = a.path;
         });
         if (!a.h || !a.get_unique_id || !a.send || !a.recv || !a.comm_destroy || !a.comm_init_rank)
             throw std::runtime_error("remote edge: librccl.so.1 not loadable");
@@ -704,6 +753,13 @@ class rccl_transport : public transport
         if (r != 0)
             throw std::runtime_error(std::string("remote edge: ") + what + ": " +
                                      (lib().err_str ? lib().err_str(r) : std::to_string(r)));
+    }
+    // an asynchronous failure of an earlier send / receive (ncclInProgress = 7 is not one)
+    void check_async()
+    {
+        int e = 0;
+        if (_comm && lib().async_error && lib().async_error(_comm, &e) == 0 && e != 0 && e != 7)
+            ck(e, "asynchronous communicator error");
     }
 
 public:
@@ -734,13 +790,24 @@ public:
     release send(channel& ch, uint64_t n, uint32_t ntags, const std::string& blob, const void* p, size_t bytes,
                  std::function<void()>) override
     {
+        check_async();
         // header first: the receiver posts the matching ncclRecv when it reads it
         write_data(ch, n, ntags, blob, [] {});
         ck(lib().send(p, bytes, /*ncclInt8*/ 0, /*peer*/ 1, _comm, stream()), "ncclSend");
         return release::now;
     }
+    void send_control(channel& ch, uint32_t type) override
+    {
+        // a run whose transfers failed must end in an error, not a DONE: at the end of a run the
+        // sends are drained first (the partition stream: the flush that ends the run waits for it
+        // anyway), so an asynchronous failure of any of them is seen here
+        if (type == M_DONE && stream()) hip::check(nsh_stream_sync(stream()), "remote edge: rccl drain");
+        check_async();
+        ch.send_msg(type);
+    }
     void recv(channel&, void* p, size_t bytes) override
     {
+        check_async();
         ck(lib().recv(p, bytes, /*ncclInt8*/ 0, /*peer*/ 0, _comm, stream()), "ncclRecv");
     }
 
@@ -752,6 +819,12 @@ private:
 };
 
 } // namespace remote
+
+std::string domain_adapter_remote::rccl_library()
+{
+    std::lock_guard<std::mutex> g(remote::g_rccl_path_m);
+    return remote::g_rccl_path;
+}
 
 // ---- adapter ---------------------------------------------------------------------------
 namespace {
@@ -909,7 +982,8 @@ void domain_adapter_remote::buffer_ready()
                 uint32_t status = 0;
                 std::string why;
                 try {
-                    _tr = std::make_shared<p2p_transport>(_device, offer, [this] { return read_reverse(100); });
+                    _tr = std::make_shared<p2p_transport>(_device, offer, [this] { return read_reverse(100); }, &_closing,
+                                                          _opt.timeout_s);
                 } catch (const std::exception& e) {
                     status = 1;
                     why = e.what();
@@ -949,8 +1023,12 @@ void domain_adapter_remote::buffer_ready()
             const bool both_dev = dev_side && peer.is_device && mine.pci[0] && peer.pci[0];
             const bool two_gpus = both_dev && std::strncmp(peer.pci, mine.pci, sizeof(mine.pci)) != 0;
             const int32_t want = peer.want ? peer.want : mine.want;
-            const char* tr = std::getenv("NSH_REMOTE_TEST_RCCL"); // the test double (rccl_transport)
-            const bool rccl_test = tr && *tr == '1' && dev_side == (peer.is_device != 0);
+            // test hook: with the RCCL test double loaded (NSH_RCCL_LIB), NSH_REMOTE_TEST_RCCL=1 accepts rccl
+            // without two PCI bus ids; the real library is never handed host rings or one GPU twice
+            const char* tr = std::getenv("NSH_REMOTE_TEST_RCCL");
+            const char* tl = std::getenv("NSH_RCCL_LIB");
+            const bool rccl_test = tr && *tr == '1' && tl && *tl && dev_side == (peer.is_device != 0);
+            if (tr && *tr == '1') test_hook_notice("NSH_REMOTE_TEST_RCCL", rccl_test ? "1 (accepted)" : "1 (ignored: NSH_RCCL_LIB unset)");
             if (want == T_RCCL && !two_gpus && !rccl_test)
                 throw std::runtime_error("remote edge: rccl transport needs device rings on two different GPUs");
             if (want == T_P2P && !both_dev) throw std::runtime_error("remote edge: p2p transport needs device rings");
@@ -1130,6 +1208,17 @@ void domain_adapter_remote::pump()
 {
     if (_thr.joinable()) _thr.join(); // setup finished (first use)
     check_failed();
+    try {
+        pump_locked();
+    } catch (...) { // a failed transfer fails the edge: no later call retries it
+        _err = std::current_exception();
+        _failed.store(true);
+        throw;
+    }
+}
+
+void domain_adapter_remote::pump_locked()
+{
     std::lock_guard<std::mutex> g(_pump_m);
     for (;;) {
         buffer_info_t ri{};
@@ -1269,7 +1358,7 @@ bool domain_adapter_remote::reader_done() const
 // its transport finish the last run's messages (deferred releases included).
 void domain_adapter_remote::reset_flags()
 {
-    if (_role == remote_role::SEND && _tr && _ready.load()) _tr->flush();
+    if (_role == remote_role::SEND && _ready.load() && _tr) _tr->flush(); // _ready first: _tr is set before it
     std::lock_guard<std::mutex> w(_ring_m);
     if (_buffer) {
         _buffer->reset_flags();

@@ -21,17 +21,29 @@ bool graph_executor::all_finished(const std::vector<block_sptr>& blocks) const
     return true;
 }
 
+// Every step runs even if an earlier one throws (a failed cross-process edge throws from
+// set_writer_done): an input left without its reader-done flag would hold the upstream block
+// forever. The first error is rethrown at the end.
 void graph_executor::finish(const block_sptr& b)
 {
     if (!_finished.insert(b->id()).second) return;
+    std::exception_ptr first;
+    auto step = [&first](auto&& f) {
+        try {
+            f();
+        } catch (...) {
+            if (!first) first = std::current_exception();
+        }
+    };
     for (auto& p : b->output_stream_ports()) {
-        for (auto& buf : _bufman->get_output_buffers(p)) buf->set_writer_done();
-        notify(p, scheduler_action_t::NOTIFY_INPUT, b->id());
+        for (auto& buf : _bufman->get_output_buffers(p)) step([&] { buf->set_writer_done(); });
+        step([&] { notify(p, scheduler_action_t::NOTIFY_INPUT, b->id()); });
     }
     for (auto& p : b->input_stream_ports()) {
-        _bufman->get_input_buffer(p)->set_reader_done();
-        notify(p, scheduler_action_t::NOTIFY_OUTPUT, b->id());
+        step([&] { _bufman->get_input_buffer(p)->set_reader_done(); });
+        step([&] { notify(p, scheduler_action_t::NOTIFY_OUTPUT, b->id()); });
     }
+    if (first) std::rethrow_exception(first);
 }
 
 std::map<nodeid_t, executor_iteration_status> graph_executor::run_one_iteration(std::vector<block_sptr> blocks)

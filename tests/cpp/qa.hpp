@@ -80,6 +80,7 @@ inline void on_alarm(int)
 int main(int argc, char** argv)
 {
     int run = 0;
+    std::setvbuf(stdout, nullptr, _IOLBF, 0); // lines reach a pipe / file as they are printed
     const char* tmo = std::getenv("QA_CASE_TIMEOUT");
     const unsigned case_timeout = tmo ? (unsigned)std::atoi(tmo) : 240u;
     std::signal(SIGALRM, qa::on_alarm);

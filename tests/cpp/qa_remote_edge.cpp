@@ -9,7 +9,10 @@
 #include "qa.hpp"
 #include "qa_ref.hpp"
 
+#include <chrono>
 #include <cstdlib>
+#include <dlfcn.h>
+#include <thread>
 #include <gnuradio/blocklib/blocks/annotator.hpp>
 #include <gnuradio/blocklib/blocks/copy.hpp>
 #include <gnuradio/blocklib/blocks/fir_filter_ccf.hpp>
@@ -61,6 +64,44 @@ static scheduler_sptr sched_for(int owner, scheduler_sptr real)
 {
     return owner == rank() ? real : std::static_pointer_cast<scheduler>(remote_domain::make(owner));
 }
+
+// The RCCL test double's counters (tests/cpp/fake_rccl.hip), when it is the loaded transport
+// library: sends completed, sends that waited > 200 us for their receive, the longest wait.
+static bool fake_rccl_stats(unsigned long long& sends, unsigned long long& waited, unsigned long long& max_us)
+{
+    const char* lib = std::getenv("NSH_RCCL_LIB");
+    if (!lib || !*lib) return false;
+    void* h = dlopen(lib, RTLD_NOW | RTLD_NOLOAD); // the instance the adapter loaded
+    if (!h) return false;
+    auto f = (void (*)(unsigned long long*, unsigned long long*, unsigned long long*))dlsym(h, "fake_rccl_stats");
+    if (f) f(&sends, &waited, &max_us);
+    dlclose(h);
+    return f != nullptr;
+}
+
+// A host block that copies slowly (sleeps per work() call): a slow consumer, so a receiving ring
+// upstream of it fills.
+class slow_copy : public blocks::copy
+{
+public:
+    static std::shared_ptr<slow_copy> make(size_t itemsize, int sleep_us)
+    {
+        auto p = std::make_shared<slow_copy>(itemsize, sleep_us);
+        p->add_port(untyped_port::make("input", port_direction_t::INPUT, itemsize));
+        p->add_port(untyped_port::make("out", port_direction_t::OUTPUT, itemsize));
+        return p;
+    }
+    slow_copy(size_t itemsize, int sleep_us) : blocks::copy(itemsize), _us(sleep_us) {}
+    work_return_code_t work(std::vector<block_work_input>& in, std::vector<block_work_output>& out) override
+    {
+        std::this_thread::sleep_for(std::chrono::microseconds(_us));
+        out[0].n_items = std::min(out[0].n_items, 4096);
+        return blocks::copy::work(in, out);
+    }
+
+private:
+    int _us;
+};
 
 // src -> *k [rank 0] ~~> copy -> sink [rank 1], run twice (restart across processes)
 TEST(RemoteCpu, ChainRestart)
@@ -518,4 +559,150 @@ TEST(RemoteGpu, RestartDropsRemainder)
         }
     }
     expect_transport(da);
+}
+
+// BASELINE C5 at G = 4: one decimating stage per process, 4 processes, 3 crossings; ranks 1 and 2
+// each hold a receiving crossing (adapter stream) and a sending one (partition stream) at once --
+// with the rccl transport, two communicators in one process on two streams. synth -> fir/2 [0]
+// ~~> fir/2 [1] ~~> fir/2 [2] ~~> fir/2 -[D2H]-> sink [3]; three runs, each within 1e-5
+// (norm-wise) of the double-precision chain.
+TEST(RemoteGpu, FourStagePipeline)
+{
+    const size_t n = 1u << 20;
+    const auto h = lowpass(127, 0.225);
+    auto src = hip::synth_source::make(0, n);
+    std::vector<hip::fir_filter_ccf::sptr> st;
+    for (int i = 0; i < 4; ++i) st.push_back(hip::fir_filter_ccf::make(h, 2));
+    auto snk = blocks::vector_sink_c::make(1, n / 16);
+    auto fg = flowgraph::make();
+    fg->connect(src, 0, st[0], 0);
+    for (int i = 1; i < 4; ++i) fg->connect(st[i - 1], 0, st[i], 0);
+    fg->connect(st[3], 0, snk, 0)->set_custom_buffer(HIP_BUFFER_ARGS_D2H);
+    std::vector<scheduler_sptr> sc;
+    for (int g = 0; g < 4; ++g)
+        sc.push_back(sched_for(g, schedulers::scheduler_hip::make("g" + std::to_string(g), 0, 1u << 19)));
+    fg->set_schedulers(sc);
+    auto o = opts();
+    o.base_port += 120;
+    auto da = domain_adapter_remote_conf::make(o);
+    domain_conf_vec dc{ domain_conf(sc[0], { src, st[0] }, da), domain_conf(sc[1], { st[1] }, da),
+                        domain_conf(sc[2], { st[2] }, da), domain_conf(sc[3], { st[3], snk }, da) };
+    fg->partition(dc);
+    auto ref = synth(n);
+    for (int i = 0; i < 4; ++i) ref = fir_ref(ref, h, 2);
+    for (int run = 0; run < 3; ++run) {
+        fg->run();
+        if (rank() == 3) {
+            ASSERT_TRUE(snk->data().size() == ref.size());
+            EXPECT_TRUE(close_normwise(snk->data(), ref));
+        }
+    }
+    if (rank() == 1 || rank() == 2) EXPECT_EQ(da->adapters().size(), (size_t)2); // one in, one out
+    expect_transport(da);
+}
+
+// A full receiving ring while the sender's stream is inside the send: hip::synth_source ->
+// hip::copy [0] ~~> hip::copy -[D2H]-> slow host copy (1 ms per 4096 items) -> sink [1], small
+// rings (64 KiB on the GPU side), so the receiver posts each receive only when its ring has drained
+// enough. The data must arrive bit-exact over two runs; with the RCCL test double the sends must
+// have waited for their receives (rendezvous held the sender's partition stream).
+TEST(RemoteGpu, FullRingBackpressure)
+{
+    const size_t n = 1u << 19;
+    auto src = hip::synth_source::make(0, n);
+    auto c0 = hip::copy::make(1);
+    auto c1 = hip::copy::make(1);
+    auto slow = slow_copy::make(sizeof(gr_complex), 1000);
+    auto snk = blocks::vector_sink_c::make(1, n);
+    auto fg = flowgraph::make();
+    fg->connect(src, 0, c0, 0);
+    fg->connect(c0, 0, c1, 0);
+    fg->connect(c1, 0, slow, 0)->set_custom_buffer(HIP_BUFFER_ARGS_D2H);
+    fg->connect(slow, 0, snk, 0);
+    auto g0 = sched_for(0, schedulers::scheduler_hip::make("g0", 0, 1u << 16));
+    auto g1 = sched_for(1, schedulers::scheduler_hip::make("g1", 0, 1u << 16));
+    auto h1 = sched_for(1, schedulers::scheduler_mt::make("h1", 1u << 16));
+    fg->set_schedulers({ g0, g1, h1 });
+    auto o = opts();
+    o.base_port += 130;
+    auto da = domain_adapter_remote_conf::make(o);
+    auto dd = domain_adapter_direct_conf::make(buffer_preference_t::DOWNSTREAM);
+    domain_conf_vec dc{ domain_conf(g0, { src, c0 }, dd), domain_conf(g1, { c1 }, da), domain_conf(h1, { slow, snk }, dd) };
+    fg->partition(dc);
+    const auto ref = synth(n);
+    for (int run = 0; run < 2; ++run) {
+        fg->run();
+        if (rank() == 1) EXPECT_TRUE(snk->data() == ref);
+    }
+    expect_transport(da);
+    unsigned long long sends = 0, waited = 0, max_us = 0;
+    if (rank() == 0 && fake_rccl_stats(sends, waited, max_us)) {
+        std::printf("  fake rccl: %llu sends, %llu waited > 200 us for their receive, longest %llu us\n", sends, waited,
+                    max_us);
+        EXPECT_TRUE(sends > 0);
+        EXPECT_TRUE(waited > 0 && max_us > 1000);
+    }
+}
+
+// The negative control of the RCCL test double's rendezvous (FAKE_RCCL_MISORDER=1: the receiver
+// posts READY only after the payload arrived, which a rendezvous never satisfies): the first
+// message deadlocks until the double's bounded wait gives up, and fg->run() raises in both
+// processes. With a double that never blocks the sender (before round 4) this case passed.
+TEST(RemoteGpu, RendezvousMisorderTimesOut)
+{
+    const size_t n = 1u << 18;
+    auto src = hip::synth_source::make(0, n);
+    auto c0 = hip::copy::make(1);
+    auto c1 = hip::copy::make(1);
+    auto snk = blocks::vector_sink_c::make(1, n);
+    auto fg = flowgraph::make();
+    fg->connect(src, 0, c0, 0);
+    fg->connect(c0, 0, c1, 0);
+    fg->connect(c1, 0, snk, 0)->set_custom_buffer(HIP_BUFFER_ARGS_D2H);
+    auto s0 = sched_for(0, schedulers::scheduler_hip::make("g0", 0, 1u << 18));
+    auto s1 = sched_for(1, schedulers::scheduler_hip::make("g1", 0, 1u << 18));
+    fg->set_schedulers({ s0, s1 });
+    auto o = opts();
+    o.base_port += 140;
+    auto da = domain_adapter_remote_conf::make(o);
+    domain_conf_vec dc{ domain_conf(s0, { src, c0 }, da), domain_conf(s1, { c1, snk }, da) };
+    fg->partition(dc);
+    std::string what;
+    try {
+        fg->run();
+    } catch (const std::exception& e) {
+        what = e.what();
+    }
+    std::printf("  rank %d: run() raised: %s\n", rank(), what.empty() ? "(nothing)" : what.c_str());
+    EXPECT_TRUE(what.find("rendezvous timed out") != std::string::npos);
+}
+
+// The same negative control on host rings (CPU; the double's synchronous receive).
+TEST(RemoteCpu, RendezvousMisorderTimesOut)
+{
+    const size_t n = 100000;
+    auto src = blocks::vector_source_c::make(synth(n, 3));
+    auto cp0 = blocks::copy::make(sizeof(gr_complex));
+    auto cp1 = blocks::copy::make(sizeof(gr_complex));
+    auto snk = blocks::vector_sink_c::make(1, n);
+    auto fg = flowgraph::make();
+    fg->connect(src, 0, cp0, 0);
+    fg->connect(cp0, 0, cp1, 0);
+    fg->connect(cp1, 0, snk, 0);
+    auto s0 = sched_for(0, schedulers::scheduler_mt::make("r0", 8192));
+    auto s1 = sched_for(1, schedulers::scheduler_mt::make("r1", 8192));
+    fg->set_schedulers({ s0, s1 });
+    auto o = opts();
+    o.base_port += 150;
+    auto conf = domain_adapter_remote_conf::make(o);
+    domain_conf_vec dc{ domain_conf(s0, { src, cp0 }, conf), domain_conf(s1, { cp1, snk }, conf) };
+    fg->partition(dc);
+    std::string what;
+    try {
+        fg->run();
+    } catch (const std::exception& e) {
+        what = e.what();
+    }
+    std::printf("  rank %d: run() raised: %s\n", rank(), what.empty() ? "(nothing)" : what.c_str());
+    EXPECT_TRUE(what.find("rendezvous timed out") != std::string::npos);
 }

@@ -153,7 +153,30 @@ def test_bench_c5_leg_rccl_transport_with_test_double(torch_cuda):
     assert out.returncode == 0, out.stderr[-3000:]
     c5 = _json_line(out.stdout)["c5_pipeline"]
     assert c5["ok"] and c5["parity"]["ok"], c5
-    assert len(c5["transports"]) == 2 and all(t.endswith(":rccl") for t in c5["transports"].values()), c5
+    assert len(c5["transports"]) == 2 and all(":rccl" in t for t in c5["transports"].values()), c5
+    assert all("libfake_rccl.so" in t for t in c5["transports"].values()), c5  # the library bound, recorded
+
+
+@pytest.mark.gpu
+def test_bench_c5_leg_g4_rccl_transport_with_test_double(torch_cuda):
+    """The driver's 4-GPU C5 layout (G = 4: one stage per rank, the middle ranks holding a receiving
+    and a sending communicator at once) on the rendezvous test double, 4 ranks on the one GPU."""
+    fake = os.path.join(ROOT, "build", "tests", "libfake_rccl.so")
+    env = dict(os.environ, NSH_BENCH_BACKEND="gloo", NSH_RCCL_LIB=fake, NSH_REMOTE_TEST_RCCL="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    out = subprocess.run([sys.executable, "bench.py", "--gpus", "4", "--c5-log2n", "20", "--c5-transport", "rccl",
+                          "--fp32-leg", "off", "--c5-fused", "off"] + ARGS,
+                         cwd=ROOT, capture_output=True, text=True, timeout=400, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    d = _json_line(out.stdout)
+    c5 = d["c5_pipeline"]
+    assert c5["layout"].startswith("G=4"), c5
+    assert c5["ok"] and c5["parity"]["ok"], c5
+    assert len(c5["transports"]) == 4 and all(":rccl" in t for t in c5["transports"].values()), c5
+    # the middle ranks: one receiving and one sending crossing each
+    for r in ("1", "2"):
+        assert "send" in c5["transports"][r] and "recv" in c5["transports"][r], c5
 
 
 @pytest.mark.gpu

@@ -20,10 +20,9 @@ def _tree(pattern):
 def test_meson_lists_every_source():
     listed = _meson_paths()
     expected = (_tree("newsched_amd/csrc/*.hip") | _tree("newsched_amd/csrc/*.hpp")
-                | _tree("newsched_amd/csrc/legacy/*.hip")
                 | _tree("newsched_amd/runtime/lib/*.cpp") | _tree("newsched_amd/schedulers/lib/*.cpp")
                 | _tree("newsched_amd/blocklib/lib/*.cpp") | _tree("newsched_amd/capi/*.cpp")
-                | _tree("tests/cpp/*.cpp") | _tree("tests/cpp/*.c") | {"oracle/nsh_oracle.c", "include/nsh_hip.h",
+                | _tree("tests/cpp/*.cpp") | _tree("tests/cpp/*.c") | _tree("tests/cpp/*.hip") | {"oracle/nsh_oracle.c", "include/nsh_hip.h",
                                                "include/nsr_flowgraph.h"})
     # tools are listed by stem ('tools' / name + '.cpp')
     tools = {f"tools/{n}.cpp" for n in re.findall(r"'(\w+)'", re.search(

@@ -157,31 +157,14 @@ def test_mul_const_vcc_bitexact(torch_cuda, vlen, nitems):
 
 
 # "mfma" is the default matrix-core kernel (decim 1: per-chunk scaled fp16x2, k_fir_mfma12),
-# "mfma_x3" forces the bf16x3 six-product kernel (k_fir_mfma2), "mfma16" the 16-sample form.
-# (k_fir_mfma9 / 2 / 5 are legacy kernels: built only with make LEGACY=1, marker `legacy`)
-ALGOS = [("direct", nsh.FIR_DIRECT), ("mfma", nsh.FIR_MFMA),
-         pytest.param("mfma_v9", nsh.FIR_MFMA, marks=pytest.mark.legacy),
-         pytest.param("mfma_x3", nsh.FIR_MFMA_BF16X3, marks=pytest.mark.legacy),
-         pytest.param("mfma16", nsh.FIR_MFMA16, marks=pytest.mark.legacy), ("mfma_f32", nsh.FIR_MFMA_F32)]
-MAX_TAPS = {"direct": 4096, "mfma": 161, "mfma_v9": 161, "mfma_x3": 161, "mfma16": 145, "mfma_f32": 257}
-VARIANT = {"mfma_v9": "9"}  # name -> NSH_FIR_MFMA_VARIANT for tuning variants under test
+# "mfma_f32" the exact-fp32 matrix form (k_fir_f32mfma)
+ALGOS = [("direct", nsh.FIR_DIRECT), ("mfma", nsh.FIR_MFMA), ("mfma_f32", nsh.FIR_MFMA_F32)]
+MAX_TAPS = {"direct": 4096, "mfma": 161, "mfma_f32": 257}
 
 
 def make_plan(name, taps, decim, algo):
-    """FirPlan for an ALGOS entry (variants are chosen at plan creation by the env var)."""
-    v = VARIANT.get(name)
-    old = os.environ.get("NSH_FIR_MFMA_VARIANT")
-    if v:
-        os.environ["NSH_FIR_MFMA_VARIANT"] = v
-    try:
-        plan = nsh.FirPlan(taps, decim, algo)
-    finally:
-        if v:
-            if old is None:
-                del os.environ["NSH_FIR_MFMA_VARIANT"]
-            else:
-                os.environ["NSH_FIR_MFMA_VARIANT"] = old
-    return plan
+    """FirPlan for an ALGOS entry."""
+    return nsh.FirPlan(taps, decim, algo)
 
 
 def run_fir(torch, plan, x, n_out, hist=None):
@@ -221,7 +204,7 @@ def test_fir127_golden(torch_cuda, golden, name, algo):
     g = golden("fir127.npz")
     plan = make_plan(name, g["taps"], 1, algo)
     assert plan.algo == algo
-    if name == "mfma" and not os.environ.get("NSH_FIR_MFMA_VARIANT"):  # (unless a variant is forced: A/B runs)
+    if name == "mfma":
         assert plan.kernel == "k_fir_mfma12<5>", plan.kernel
     y, hist = run_fir(torch, plan, g["x"], g["x"].size)
     ok, err, scale = orc.tol_ok(y, g["y"])
@@ -266,15 +249,10 @@ def test_fir_decim_vs_oracle(torch_cuda, decim):
         np.testing.assert_array_equal(hout, h_ref)
 
 
-@pytest.fixture(params=["v11", pytest.param("v7", marks=pytest.mark.legacy)])
-def dec_form(request, monkeypatch):
-    """Both polyphase MFMA kernels: k_fir_mfma11 (default: fp16x2, per-chunk scale, exact
-    path) and k_fir_mfma7 (bf16x3 six products; NSH_FIR_MFMA_VARIANT=7)."""
-    if request.param == "v7":
-        monkeypatch.setenv("NSH_FIR_MFMA_VARIANT", "7")
-    else:
-        monkeypatch.delenv("NSH_FIR_MFMA_VARIANT", raising=False)
-    return request.param
+@pytest.fixture
+def dec_form():
+    """The polyphase MFMA kernel: k_fir_mfma11 (fp16x2, per-chunk scale, exact path)."""
+    return "v11"
 
 
 def _dec_plan(h, decim, form):
@@ -460,20 +438,15 @@ def _assert_nonfinite_pattern(y, ref):
     np.testing.assert_array_equal(np.sign(y.imag[inf]), np.sign(ref.imag[inf]))
 
 
-@pytest.fixture(params=["v12", pytest.param("v9", marks=pytest.mark.legacy)])
-def v8_form(request, monkeypatch):
-    """The fp16x2 kernels: k_fir_mfma12 (default: one chunk per workgroup) and k_fir_mfma9
-    (contiguous per-workgroup ranges, NSH_FIR_MFMA_VARIANT=9)."""
-    if request.param == "v9":
-        monkeypatch.setenv("NSH_FIR_MFMA_VARIANT", "9")
-    else:
-        monkeypatch.delenv("NSH_FIR_MFMA_VARIANT", raising=False)
-    return request.param
+@pytest.fixture
+def v8_form():
+    """The decim-1 fp16x2 kernel: k_fir_mfma12 (one chunk per workgroup)."""
+    return "v12"
 
 
 def _v8_plan(h, form):
     plan = nsh.FirPlan(h, 1, nsh.FIR_MFMA)
-    assert plan.kernel == ("k_fir_mfma12<5>" if form == "v12" else "k_fir_mfma9<5>"), plan.kernel
+    assert plan.kernel == "k_fir_mfma12<5>", plan.kernel
     return plan
 
 
@@ -520,9 +493,7 @@ def test_fir_mfma_exact_paths(torch_cuda, v8_form, ntaps, decim, kind):
     compute such chunks with the exact-fp32 matrix tile of k_fir_f32mfma (fp32 products and sums;
     the decimators filter the chunk undecimated and keep every D-th output): within tolerance of
     the oracle on each chunk's own scale, and at decim 1 bit-identical to the NSH_FIR_MFMA_F32
-    kernel when both use the same tap blocking (QF = 2Q - 1: 127 and 64 taps). The legacy
-    k_fir_mfma9 uses the fp32 direct form there (taps in order k = 0..L-1, one fused multiply-add
-    each, the order k_fir_direct accumulates in): bit-identical to k_fir_direct.
+    kernel when both use the same tap blocking (QF = 2Q - 1: 127 and 64 taps).
     'nan' (a NaN per chunk): every form computes such chunks with the fp32 direct form: the same
     NaN positions as k_fir_direct and every finite output bit-identical to it."""
     torch = torch_cuda
@@ -533,11 +504,9 @@ def test_fir_mfma_exact_paths(torch_cuda, v8_form, ntaps, decim, kind):
         x[100::2048] *= np.float32(2.0 ** 40)
     else:
         x[100::2048] = complex(np.nan, 0.5)
-    if decim > 1 and v8_form == "v9":
-        pytest.skip("decimators: one kernel form (k_fir_mfma11)")
     plan = nsh.FirPlan(h, decim, nsh.FIR_MFMA)
     if ntaps == 127:
-        assert plan.kernel.startswith({1: "k_fir_mfma12" if v8_form == "v12" else "k_fir_mfma9",
+        assert plan.kernel.startswith({1: "k_fir_mfma12",
                                        2: "k_fir_mfma11", 4: "k_fir_mfma11"}[decim]), plan.kernel
     y, hy = run_fir(torch, plan, x, n // decim)
     yd, hd = run_fir(torch, nsh.FirPlan(h, decim, nsh.FIR_DIRECT), x, n // decim)
@@ -547,14 +516,12 @@ def test_fir_mfma_exact_paths(torch_cuda, v8_form, ntaps, decim, kind):
         np.testing.assert_array_equal(np.isnan(y.real) | np.isnan(y.imag), nan)
         np.testing.assert_array_equal(y[~nan].view(np.uint32), yd[~nan].view(np.uint32))
         return
-    if decim == 1 and v8_form == "v12":
+    if decim == 1:
         pf = nsh.FirPlan(h, 1, nsh.FIR_MFMA_F32)
         q12 = int(plan.kernel.split("<")[1].rstrip(">"))
         if pf.kernel == "k_fir_f32mfma<%d>" % (2 * q12 - 1):
             yf, _ = run_fir(torch, pf, x, n)
             np.testing.assert_array_equal(y.view(np.uint32), yf.view(np.uint32))
-    elif decim == 1:  # legacy k_fir_mfma9: the fp32 direct form
-        np.testing.assert_array_equal(y.view(np.uint32), yd.view(np.uint32))
     ref = orc.fir_ccf(x[: n // decim * decim], h, decim)
     c = 2048 // decim
     for a in range(0, n // decim, c):   # each chunk on its own scale
@@ -654,21 +621,12 @@ def test_fir_plan_kernels():
         assert nsh.FirPlan(np.ones(L, np.float32), 1, nsh.FIR_MFMA).kernel == "k_fir_mfma12<%d>" % ((L + 30) // 32 + 1)
 
 
-@pytest.mark.legacy
-def test_fir_plan_kernels_legacy():
-    h = _firwin127()
-    assert nsh.FirPlan(h, 1, nsh.FIR_MFMA_BF16X3).kernel == "k_fir_mfma2<5,2>"
-    assert nsh.FirPlan(h, 1, nsh.FIR_MFMA16).kernel == "k_fir_mfma5<9,1>"
-
-
-def test_fir_legacy_algorithms_fail_loudly_when_not_built():
-    """Without make LEGACY=1 the superseded forms are refused at plan creation, never silently
+def test_fir_retired_algorithms_fail_loudly():
+    """The bf16x3 kernels retired in round 4 are refused at plan creation, never silently
     replaced by another kernel."""
-    if nsh.fir_legacy_available():
-        pytest.skip("legacy kernels built")
     h = _firwin127()
     for algo in (nsh.FIR_MFMA_BF16X3, nsh.FIR_MFMA16):
-        with pytest.raises(nsh.NshError, match="legacy"):
+        with pytest.raises(nsh.NshError, match="retired"):
             nsh.FirPlan(h, 1, algo)
 
 

@@ -6,7 +6,10 @@ whose reads of the sender's ring complete late on another thread: the edge's rel
 device rings (hip_buffer) on the GPU, where both ranks share the box's one GPU: the "p2p"
 transport (stream-ordered copies into IPC-mapped landing slots, auto's choice on one GPU) and
 the pinned-memory "socket" staging. RCCL needs two devices; auto selects it on a multi-GPU
-node (test_bench.py::test_bench_c5_rccl_two_gpus)."""
+node (test_bench.py::test_bench_c5_rccl_two_gpus). Until then the "rccl" transport's own code
+runs against the RCCL test double tests/cpp/fake_rccl.hip, which keeps RCCL's rendezvous: a
+send holds the sender's stream until the peer's stream has reached the matching receive (its
+negative control, a mis-ordered receive, deadlocks and is reported as a rendezvous timeout)."""
 import os
 import random
 import socket
@@ -40,12 +43,12 @@ def free_port_block(width=64):
     raise RuntimeError("no free port block")
 
 
-def run_pair(case, timeout=120, env_extra=None):
+def run_pair(case, timeout=120, env_extra=None, ranks=2):
     if not (os.path.exists(EXE) and os.path.exists(FAKE_RCCL)):
         subprocess.run(["make", "-s", "-C", ROOT, "tests"], check=True)
-    port = free_port_block(128)
+    port = free_port_block(192)
     procs = []
-    for r in (0, 1):
+    for r in range(ranks):
         env = dict(os.environ, QA_RANK=str(r), QA_PORT=str(port), **(env_extra or {}))
         procs.append(subprocess.Popen([EXE, case], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
     outs = []
@@ -87,6 +90,20 @@ def test_remote_edges_cpu_rccl_protocol(case):
     assert all("transport rccl" in o for o in outs)
 
 
+RCCL_FAKE = {"QA_TRANSPORT": "rccl", "NSH_RCCL_LIB": FAKE_RCCL, "NSH_REMOTE_TEST_RCCL": "1"}
+
+
+def test_rccl_rendezvous_negative_control_cpu():
+    """The test double's rendezvous is real: with the receiver posting READY only after its payload
+    (FAKE_RCCL_MISORDER=1), the sender never gets its READY and the receiver never gets its payload
+    -- a deadlock, bounded by the double's wait (FAKE_RCCL_TIMEOUT_S) and reported by fg->run() in
+    both processes as "rendezvous timed out". (The pre-round-4 double, which sent without waiting
+    for the receive, passed this mis-order.)"""
+    outs = run_pair("RemoteCpu.RendezvousMisorderTimesOut", timeout=90,
+                    env_extra=dict(RCCL_FAKE, FAKE_RCCL_MISORDER="1", FAKE_RCCL_TIMEOUT_S="4"))
+    assert all("rendezvous timed out" in o for o in outs)
+
+
 def test_rccl_on_host_rings_refused_without_the_test_double():
     """Without the test hook, "rccl" asked for host rings is refused by the receiver: an error of
     fg->run() in both processes (the real library would be handed host pointers)."""
@@ -111,7 +128,7 @@ def test_deferred_release_negative_control():
 
 
 GPU_CASES = ["RemoteGpu.DeviceChainRestart", "RemoteGpu.DecimatingPipelineC5", "RemoteGpu.DeviceTags",
-             "RemoteGpu.RestartDropsRemainder"]
+             "RemoteGpu.RestartDropsRemainder", "RemoteGpu.FullRingBackpressure"]
 
 
 @pytest.mark.gpu
@@ -143,3 +160,34 @@ def test_rccl_refused_on_one_gpu():
     of fg->run() in both processes (no abort, no hang)."""
     outs = run_pair("RemoteGpu.RcclRefusedOnOneGpu", timeout=120)
     assert "two different GPUs" in outs[1]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("transport", ["rccl", "p2p"])
+def test_four_stage_pipeline_gpu(transport):
+    """BASELINE C5 at G = 4 as four processes on the one GPU (one decimating stage each, three
+    crossings): the middle ranks each hold a receiving crossing on their adapter stream and a sending
+    one on their partition stream -- with rccl (the rendezvous test double), two communicators in
+    one process, both blocking their streams. Three runs, 1e-5 norm-wise vs the double-precision
+    chain at the last rank."""
+    env = dict(RCCL_FAKE, QA_EXPECT_TRANSPORT="rccl") if transport == "rccl" else \
+        {"QA_TRANSPORT": "p2p", "QA_EXPECT_TRANSPORT": "p2p"}
+    run_pair("RemoteGpu.FourStagePipeline", timeout=300, env_extra=env, ranks=4)
+
+
+@pytest.mark.gpu
+def test_rccl_backpressure_holds_sender_stream():
+    """A full receiving ring (slow host consumer) while the sender is inside ncclSend: bit-exact
+    over two runs, and the double reports that sends waited for their receives (> 1 ms)."""
+    outs = run_pair("RemoteGpu.FullRingBackpressure", timeout=300, env_extra=dict(RCCL_FAKE, QA_EXPECT_TRANSPORT="rccl"))
+    assert "waited > 200 us" in outs[0]
+
+
+@pytest.mark.gpu
+def test_rccl_rendezvous_negative_control_gpu():
+    """The negative control on device rings: the gate kernels hold both streams until the double's
+    bounded wait (4 s) gives up; fg->run() raises "rendezvous timed out" in both processes and every
+    stream drains (no kernel outlives its bound)."""
+    outs = run_pair("RemoteGpu.RendezvousMisorderTimesOut", timeout=120,
+                    env_extra=dict(RCCL_FAKE, FAKE_RCCL_MISORDER="1", FAKE_RCCL_TIMEOUT_S="4"))
+    assert all("rendezvous timed out" in o for o in outs)

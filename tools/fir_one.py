@@ -12,7 +12,7 @@ import torch
 from newsched_amd import nsh
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--algo", default="mfma", choices=["mfma", "mfma_x3", "direct", "f32", "casc"])
+ap.add_argument("--algo", default="mfma", choices=["mfma", "direct", "f32", "casc"])
 ap.add_argument("--log2n", type=int, default=25)
 ap.add_argument("--reps", type=int, default=10)
 ap.add_argument("--decim", type=int, default=1)
@@ -30,7 +30,7 @@ if a.algo == "casc":  # C5's fused chain (nsh_fir_cascade_ccf): 4 x fir(firwin(1
     for _ in range(a.reps):
         p(x, None, hc, y, n // 16)
 else:
-    p = nsh.FirPlan(h, a.decim, {"mfma": nsh.FIR_MFMA, "mfma_x3": nsh.FIR_MFMA_BF16X3, "direct": nsh.FIR_DIRECT,
+    p = nsh.FirPlan(h, a.decim, {"mfma": nsh.FIR_MFMA, "direct": nsh.FIR_DIRECT,
                                   "f32": nsh.FIR_MFMA_F32}[a.algo])
     for _ in range(a.reps):
         p(x, hin, hout, y, n // a.decim)
