@@ -2,11 +2,15 @@
 """Headline benchmark: MSamples/s through the 127-tap fir_filter_ccf flowgraph (BASELINE
 config C3: 2^28-sample complex-float stream, one MI355X per rank).
 
-A step = one flowgraph run over the rank's N-sample shard: nop_source -> nop_head(N) ->
-[HBM-resident hip_buffer ring, preloaded] -> gr::hip::fir_filter_ccf -> [hip_buffer] ->
-null_sink, all inside one scheduler_hip GPU domain (include/nsr_flowgraph.h). Inputs are
-resident in HBM before timing starts; the run ends only after the partition stream has
-drained. With --gpus N every rank (one process per GPU) streams its own contiguous time
+A step = one N-sample batch of the rank's shard through the flowgraph nop_source ->
+nop_head -> [HBM-resident hip_buffer ring, preloaded] -> gr::hip::fir_filter_ccf -> [hip_buffer]
+-> null_sink, all inside one scheduler_hip GPU domain (include/nsr_flowgraph.h). The timed
+region is ONE flowgraph run that streams K batches (nop_head passes K*N items; the resident ring
+holds x twice, so every batch reads x from HBM and the FIR's history carries over as in any
+continuous stream): K launches queued back to back on the partition stream, start and drain of
+the run inside the timed region. Inputs are resident in HBM before timing starts. The restart
+cost of a run (start, the executor pass, launch latency, drain detection) is reported next to it
+as `per_run_mode` (runs of one batch each, timed separately). With --gpus N every rank (one process per GPU) streams its own contiguous time
 shard x[rank*N, (rank+1)*N) with the 126-sample halo regenerated from the counter-based
 source: weak scaling, no data-path collective.
 
@@ -317,6 +321,9 @@ def main():
     ap.add_argument("--algo", default="auto", choices=["auto", "mfma", "mfma_f32", "direct"])
     ap.add_argument("--fp32-leg", choices=["on", "off"], default="on",
                     help="also time the exact-fp32 matrix form (NSH_FIR_MFMA_F32) on the same flowgraph")
+    ap.add_argument("--timing-stride", type=int, default=4,
+                    help="HIP-event timing on every k-th FIR launch of the timed run (each timed launch costs its "
+                         "event packets, ~7 us)")
     ap.add_argument("--out-buf-mib", type=int, default=2048, help="FIR output hip_buffer (default: one launch per 2^28-sample step)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-log2n", type=int, default=28, help="CPU baseline sample (default: the full stream)")
@@ -389,19 +396,22 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    # Warm-up: at least --warmup runs and at least --min-warmup-s seconds of them (the
-    # chip's clocks take ~20 back-to-back runs to settle), untimed.
+    # Warm-up: at least --warmup batches and at least --min-warmup-s seconds of them (the
+    # chip's clocks take ~20 back-to-back launches to settle), untimed.
     tw = time.perf_counter()
     warm = 0
+    fb.set_batches(max(1, a.warmup))
     while warm < a.warmup or time.perf_counter() - tw < a.min_warmup_s:
         fb.run()
-        warm += 1
+        warm += max(1, a.warmup)
     warm_s = time.perf_counter() - tw
+    fb.set_batches(a.steps)
+    fb.set_timing_stride(a.timing_stride)  # every stride-th launch carries its event pair
     barrier()
     st0 = fb.stats()  # cumulative HIP-event kernel time / samples of the FIR's timed launches
     launches0 = st0["launches"]
     t0 = time.perf_counter()
-    fb.run(a.steps)  # K complete flowgraph runs, looped in C (no Python between steps)
+    fb.run()  # one flowgraph run streaming K batches = K steps
     barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
@@ -414,8 +424,8 @@ def main():
     algo_used = {1: "direct", 2: "mfma", 5: "mfma_f32"}.get(st["algo"], str(st["algo"]))
     kernel = st["kernel"]
     timed_launches = st["launches"] - launches0
-    launches_per_run = timed_launches / a.steps
     per_launch_samples = samples / timed_launches
+    launches_per_run = n / per_launch_samples  # launches per step (batch); all of one size
     avg_launch_ms = kms / timed_launches
     achieved = BYTES_PER_SAMPLE * per_launch_samples / (avg_launch_ms * 1e-3) / 1e9  # GB/s
 
@@ -449,13 +459,14 @@ def main():
         "dtype": "f32",
         "data": "synthetic: counter-based splitmix64 complex-float stream (BASELINE.md §2), HBM-resident before timing",
         "config": {
-            "workload": "C3: 127-tap fir_filter_ccf (firwin(127,0.2) fp32 taps) over a 2^%d-sample complex-float stream per GPU, "
-                        "nop_source->nop_head->[resident hip_buffer]->hip::fir_filter_ccf->[hip_buffer]->null_sink in scheduler_hip"
-                        % a.log2n,
+            "workload": "C3: 127-tap fir_filter_ccf (firwin(127,0.2) fp32 taps) over 2^%d-sample complex-float batches per GPU, "
+                        "nop_source->nop_head->[resident hip_buffer]->hip::fir_filter_ccf->[hip_buffer]->null_sink in scheduler_hip; "
+                        "the K steps are one flowgraph run streaming K batches" % a.log2n,
             "samples_per_gpu": n,
             "ntaps": int(taps.size),
             "fir_algo": algo_used,
             "fir_launches_per_step": launches_per_run,
+            "timed_launches": timed_launches,
             "samples_per_launch": int(per_launch_samples),
             "parallelism": "time-sharded replicas x%d (126-sample halo regenerated, no collective)" % world,
         },
@@ -473,10 +484,31 @@ def main():
             "kernel_gflops": round(FLOP_PER_SAMPLE * per_launch_samples / (avg_launch_ms * 1e-3) / 1e9, 1),
             "flowgraph_achieved": round(BYTES_PER_SAMPLE * n / (step_us * 1e-6) / 1e9, 1),
             "flowgraph_frac": round(BYTES_PER_SAMPLE * n / (step_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
-            "overhead_us_per_step": round(step_us - avg_launch_ms * 1e3 * launches_per_run, 2),
+            "overhead_us_per_step": round(step_us - avg_launch_ms * 1e3 * launches_per_run, 2),  # incl. the run's start / drain
         },
         "parity": {"check": "last 4096 outputs of the last step vs oracle (double accumulation), every rank",
                    "max_abs_err": err, "scale": scale, "ok": bool(ok)},
+    }
+    # the restart cost: runs of ONE batch each (start, executor pass, launch, drain), timed apart
+    fb.set_batches(1)
+    fb.set_timing_stride(1)
+    pr_runs = max(5, a.steps // 2)
+    fb.run(3)
+    barrier()
+    p0 = fb.stats()
+    t0 = time.perf_counter()
+    fb.run(pr_runs)  # complete runs back to back, looped in C
+    barrier()
+    pr_el = time.perf_counter() - t0
+    p1 = fb.stats()
+    pr_kernel_us = (p1["kernel_ms"] - p0["kernel_ms"]) / max(1, p1["launches"] - p0["launches"]) * 1e3
+    out["per_run_mode"] = {
+        "runs": pr_runs, "ms_per_run": round(pr_el / pr_runs * 1e3, 4),
+        "value": round(world * n * pr_runs / pr_el / 1e6, 1), "unit": "MSamples/s",
+        "avg_launch_us": round(pr_kernel_us, 2),
+        "restart_overhead_us": round(pr_el / pr_runs * 1e6 - pr_kernel_us * launches_per_run, 2),
+        "flowgraph_frac": round(BYTES_PER_SAMPLE * n / (pr_el / pr_runs) / 1e9 / HBM_PEAK_GBS, 4),
+        "what": "one batch per flowgraph run: each run's start, executor pass, launch and drain detection in its time",
     }
     tr, src = load_pmc_traffic(kernel, per_launch_samples)
     if tr is not None:

@@ -66,6 +66,14 @@ int nsh_event_query(void* event);          /* 0 complete, 1 not ready, <0 error 
 int nsh_event_sync(void* event);
 int nsh_event_elapsed_ms(void* start, void* stop, float* ms);
 int nsh_stream_wait_event(void* stream, void* event);
+/* Times the NEXT kernel launched by this library on the calling thread (e.g. the FIR kernel of
+ * the next nsh_fir_ccf / nsh_fir_cascade_ccf): the launch records start_event when the kernel
+ * begins and stop_event when it ends, as part of its own dispatch (hipExtLaunchKernel), instead
+ * of two event records around the call -- two fewer stream packets per timed launch. Events from
+ * nsh_event_create. The setting is consumed by that one launch; (NULL, NULL) clears it. Replaces
+ * the per-work() cudaEventRecord pairs a CUDA block would use for kernel timing (the reference
+ * blocks do not time their kernels). */
+int nsh_time_next_launch(void* start_event, void* stop_event);
 
 /* ---- memory ----------------------------------------------------------------------- */
 enum nsh_copy_kind { NSH_H2D = 0, NSH_D2H = 1, NSH_D2D = 2, NSH_DEFAULT = 3 };

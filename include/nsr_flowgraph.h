@@ -33,10 +33,19 @@ int nsr_fir_bench_create(int dev, const float* taps, int ntaps, int algo, int64_
 int nsr_fir_bench_run(void* handle); /* one run (start + wait); rethrown work() errors -> rc */
 /* `count` runs back to back (each a complete fg->run(): start, every work(), drain), looped in C. */
 int nsr_fir_bench_runs(void* handle, int64_t count);
-/* Cumulative over every run since create (callers take differences around the runs they
- * time): summed FIR kernel time from HIP events around each launch on the partition stream,
- * FIR launches, samples, and the algorithm the plan resolved to. */
+/* Items per run = batches * n from the next run on (nop_head::set_length): one run then streams the
+ * resident n-sample input `batches` times through the FIR as one continuous stream (the ring holds
+ * x twice, so every batch reads x; the FIR's history carries across batches as in any stream) --
+ * one launch per batch, queued back to back on the partition stream. Default 1. */
+int nsr_fir_bench_set_batches(void* handle, int64_t batches);
+/* Cumulative over every timed launch since create (callers take differences around the runs
+ * they time): summed FIR kernel time from HIP events that each timed launch records as part of
+ * its dispatch on the partition stream (nsh_time_next_launch), the timed launches, their output
+ * samples, and the algorithm the plan resolved to. */
 int nsr_fir_bench_stats(void* handle, double* kernel_ms, uint64_t* launches, uint64_t* samples, int* algo);
+/* Time every stride-th FIR launch from now on (default 1: every launch). A timed launch costs
+ * its event pair's stream packets (~7 us per launch measured, tools/probe/stream_gap.py). */
+int nsr_fir_bench_set_timing_stride(void* handle, int stride);
 /* The FIR kernel the bench's block launches (after its first run), e.g. "k_fir_mfma12<5>". */
 const char* nsr_fir_bench_kernel(void* handle);
 /* The last `count` FIR outputs of the last run (interleaved re,im fp32) -> host. */

@@ -29,6 +29,9 @@ public:
         _ncopied_items = 0;
         return sync_block::start();
     }
+    // items passed per run from the next start() on (GNU Radio head::set_length)
+    void set_length(size_t nitems) { _nitems = nitems; }
+    size_t length() const { return _nitems; }
     work_return_code_t work(std::vector<block_work_input>& in, std::vector<block_work_output>& out) override
     {
         if (_ncopied_items >= _nitems) {

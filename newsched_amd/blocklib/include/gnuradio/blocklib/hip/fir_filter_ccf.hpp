@@ -38,8 +38,14 @@ public:
     // block's first input (a time shard's halo, regenerated or received by the caller).
     void set_initial_history(const std::vector<gr_complex>& h) { _init_hist = h; }
 
-    // Per-launch kernel timing with HIP events on the launch stream (bench/profiling).
-    void enable_timing(bool on) { _timing = on; }
+    // Per-launch kernel timing with HIP events on the launch stream (bench/profiling): every
+    // `stride`-th launch is timed (its own dispatch records the pair, nsh_time_next_launch).
+    void enable_timing(bool on, int stride = 1)
+    {
+        _timing = on;
+        _stride = stride > 0 ? stride : 1;
+    }
+    uint64_t timed_launches() const { return _timed_launches; }
     // Sum of kernel durations (ms) and output samples over every timed launch since the block
     // was made (cumulative across runs: a caller takes differences around the runs it times).
     // Reading it synchronises on the launches' events and folds them into the total; between
@@ -51,6 +57,8 @@ private:
     void release();
     std::vector<gr_complex> _init_hist;
     bool _timing = false;
+    int _stride = 1;
+    uint64_t _timed_launches = 0;
     std::vector<std::pair<void*, void*>> _ev;  // (start, stop) per launch, reused
     size_t _ev_used = 0;
     double _done_ms = 0; // kernel time of the launches folded so far

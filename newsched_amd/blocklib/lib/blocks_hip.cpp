@@ -173,12 +173,23 @@ bool fir_filter_ccf::start()
     return block::start();
 }
 
+// Kernel timing: the launch records its own start / stop events (nsh_time_next_launch) unless
+// NSH_FIR_TIMING=records asks for the two event records around the call (A/B of the two forms).
+static bool timing_by_records()
+{
+    static const bool r = [] {
+        const char* v = std::getenv("NSH_FIR_TIMING");
+        return v && std::string(v) == "records";
+    }();
+    return r;
+}
+
 work_return_code_t fir_filter_ccf::work(std::vector<block_work_input>& in, std::vector<block_work_output>& out)
 {
     const int n_out = out[0].n_items; // decim_block::do_work: in[0].n_items == D * n_out
     void* s = current_stream();
     std::pair<void*, void*>* ev = nullptr;
-    if (_timing) {
+    if (_timing && _launches % (uint64_t)_stride == 0) {
         if (_ev_used == _ev.size()) {
             std::pair<void*, void*> p{ nullptr, nullptr };
             check(nsh_event_create(&p.first), "hip::fir_filter_ccf timing");
@@ -186,7 +197,10 @@ work_return_code_t fir_filter_ccf::work(std::vector<block_work_input>& in, std::
             _ev.push_back(p);
         }
         ev = &_ev[_ev_used++];
-        check(nsh_event_record(ev->first, s), "hip::fir_filter_ccf timing");
+        if (timing_by_records())
+            check(nsh_event_record(ev->first, s), "hip::fir_filter_ccf timing");
+        else // the launch records both events itself (nsh_time_next_launch)
+            check(nsh_time_next_launch(ev->first, ev->second), "hip::fir_filter_ccf timing");
     }
     NSR_RT(4);
     check(nsh_fir_ccf(_plan, (const float*)in[0].buffer->read_ptr(), _zero_hist ? nullptr : (const float*)_hist[_cur],
@@ -194,8 +208,9 @@ work_return_code_t fir_filter_ccf::work(std::vector<block_work_input>& in, std::
           "hip::fir_filter_ccf");
     _zero_hist = false;
     if (ev) {
-        check(nsh_event_record(ev->second, s), "hip::fir_filter_ccf timing");
+        if (timing_by_records()) check(nsh_event_record(ev->second, s), "hip::fir_filter_ccf timing");
         _timed_samples += (uint64_t)n_out;
+        ++_timed_launches;
     }
     NSR_RT(5);
     _cur ^= 1;
@@ -309,7 +324,10 @@ work_return_code_t fir_filter_cascade_ccf::work(std::vector<block_work_input>& i
             _ev.push_back(p);
         }
         ev = &_ev[_ev_used++];
-        check(nsh_event_record(ev->first, s), "hip::fir_filter_cascade_ccf timing");
+        if (timing_by_records())
+            check(nsh_event_record(ev->first, s), "hip::fir_filter_cascade_ccf timing");
+        else // the launch records both events itself (nsh_time_next_launch)
+            check(nsh_time_next_launch(ev->first, ev->second), "hip::fir_filter_cascade_ccf timing");
     }
     check(nsh_fir_cascade_ccf(_plan, (const float*)in[0].buffer->read_ptr(),
                               _zero_hist ? nullptr : (const float*)_hist[_cur], (float*)_hist[_cur ^ 1],
@@ -317,7 +335,7 @@ work_return_code_t fir_filter_cascade_ccf::work(std::vector<block_work_input>& i
           "hip::fir_filter_cascade_ccf");
     _zero_hist = false;
     if (ev) {
-        check(nsh_event_record(ev->second, s), "hip::fir_filter_cascade_ccf timing");
+        if (timing_by_records()) check(nsh_event_record(ev->second, s), "hip::fir_filter_cascade_ccf timing");
         _timed_samples += (uint64_t)n_out;
     }
     _cur ^= 1;

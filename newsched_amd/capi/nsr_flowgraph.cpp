@@ -83,6 +83,9 @@ struct c5_pipeline {
 struct fir_bench {
     flowgraph::sptr fg;
     schedulers::scheduler_hip::sptr sched;
+    blocks::nop_head::sptr head;
+    int64_t n = 0;
+    bool timing = false;
     hip::fir_filter_ccf::sptr fir;
     std::shared_ptr<hip_buffer> out_ring;
     int dev = 0;
@@ -103,8 +106,11 @@ int nsr_fir_bench_create(int dev, const float* taps, int ntaps, int algo, int64_
         const size_t isz = sizeof(gr_complex);
         auto src = blocks::nop_source::make(isz);
         auto head = blocks::nop_head::make(isz, (size_t)n);
+        b->head = head;
+        b->n = n;
         b->fir = hip::fir_filter_ccf::make(std::vector<float>(taps, taps + ntaps), 1, algo);
-        b->fir->enable_timing(timing != 0);
+        b->timing = timing != 0;
+        b->fir->enable_timing(b->timing);
         if (first_index > 0) {
             std::vector<gr_complex> h((size_t)ntaps - 1);
             for (size_t j = 0; j < h.size(); ++j) h[j] = synth_at(first_index - h.size() + j, seed);
@@ -157,6 +163,15 @@ int nsr_fir_bench_run(void* handle)
     return guarded([&] { static_cast<fir_bench*>(handle)->fg->run(); });
 }
 
+int nsr_fir_bench_set_batches(void* handle, int64_t batches)
+{
+    return guarded([&] {
+        auto b = static_cast<fir_bench*>(handle);
+        if (batches < 1) throw std::invalid_argument("nsr_fir_bench_set_batches: batches must be >= 1");
+        b->head->set_length((size_t)(batches * b->n));
+    });
+}
+
 int nsr_fir_bench_runs(void* handle, int64_t count)
 {
     return guarded([&] {
@@ -165,12 +180,20 @@ int nsr_fir_bench_runs(void* handle, int64_t count)
     });
 }
 
+int nsr_fir_bench_set_timing_stride(void* handle, int stride)
+{
+    return guarded([&] {
+        auto b = static_cast<fir_bench*>(handle);
+        b->fir->enable_timing(b->timing, stride);
+    });
+}
+
 int nsr_fir_bench_stats(void* handle, double* kernel_ms, uint64_t* launches, uint64_t* samples, int* algo)
 {
     return guarded([&] {
         auto b = static_cast<fir_bench*>(handle);
         if (kernel_ms) *kernel_ms = b->fir->kernel_ms();
-        if (launches) *launches = b->fir->launches();
+        if (launches) *launches = b->fir->timed_launches();
         if (samples) *samples = b->fir->timed_samples();
         if (algo) *algo = b->fir->algo();
     });

@@ -1,6 +1,7 @@
 // Shared helpers for the libnsh_hip.so translation units (gfx950 only).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <cstdint>
 #include <cstdio>
 #include <string>
@@ -25,6 +26,31 @@ inline int fail_msg(const char* what)
 }
 
 inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Timing of the next kernel launch on this thread (nsh_time_next_launch): a start / stop event
+// pair that the launch itself records, as part of the kernel's dispatch (hipExtLaunchKernelGGL),
+// instead of two separate event packets around it on the stream. Taken (and cleared) by the first
+// launch() after it was set.
+struct launch_events {
+    hipEvent_t start = nullptr, stop = nullptr;
+};
+inline launch_events& next_launch_events()
+{
+    static thread_local launch_events e;
+    return e;
+}
+template <typename K, typename... A>
+inline void launch(K kernel, dim3 grid, dim3 block, uint32_t lds, hipStream_t s, A... args)
+{
+    launch_events& e = next_launch_events();
+    if (e.start || e.stop) {
+        const launch_events t = e;
+        e = launch_events();
+        hipExtLaunchKernelGGL(kernel, grid, block, lds, s, t.start, t.stop, 0u, args...);
+    } else {
+        hipLaunchKernelGGL(kernel, grid, block, lds, s, args...);
+    }
+}
 
 // Grid for a grid-stride streaming kernel: enough workgroups to fill 256 CUs several
 // times over, capped so each thread still walks several 16-byte vectors.

@@ -127,7 +127,7 @@ int launch_direct(const nsh_fir_plan* p, const float2* in, const float2* hin, fl
     const size_t lds = (size_t)(count + count / (R * D) + 1) * sizeof(float2);
     const int64_t grid = (n_out + T - 1) / T;
     if (grid > 0x7fffffff) return nsh::fail_msg("nsh_fir_ccf: too many outputs for one call");
-    hipLaunchKernelGGL((k_fir_direct<D, R>), dim3((unsigned)grid), dim3(kThreads), lds, s,
+    nsh::launch((k_fir_direct<D, R>), dim3((unsigned)grid), dim3(kThreads), lds, s,
                        in, hin, hout, out, p->taps_dev, p->L, p->Lp, n_out);
     NSH_CK_LAUNCH("nsh_fir_ccf(direct)");
     return 0;

@@ -190,7 +190,7 @@ int launch_f32(const nsh_fir_plan* p, const float2* in, const float2* hin, float
     const int64_t per_x = (nchunks + 7) / 8;
     const int64_t grid = per_x * 8;
     if (grid > 0x7fffffff) return nsh::fail_msg("nsh_fir_ccf(mfma f32): stream too long for one launch");
-    hipLaunchKernelGGL((k_fir_f32mfma<QF>), dim3((unsigned)grid), dim3(G::NT), G::LDS, s, in, hin, hout, out,
+    nsh::launch((k_fir_f32mfma<QF>), dim3((unsigned)grid), dim3(G::NT), G::LDS, s, in, hin, hout, out,
                        (const float4*)p->tf32_dev, (const float*)p->taps_dev, p->L, n_out, per_x);
     NSH_CK_LAUNCH("nsh_fir_ccf(mfma f32)");
     return 0;

@@ -741,7 +741,7 @@ int launch_v11(const nsh_fir_plan* p, const float2* in, const float2* hin, float
     const int n_cu = plan_cus(p);
     const int64_t max_grid = (int64_t)n_cu * 2; // launch_v9's longer grids measured 4-7 % slower here
     const unsigned grid = (unsigned)(nchunks < max_grid ? nchunks : max_grid);
-    hipLaunchKernelGGL((k_fir_mfma11<D, QH>), dim3(grid), dim3(G::NT), G::LDS, s, in, hin, hout, out,
+    nsh::launch((k_fir_mfma11<D, QH>), dim3(grid), dim3(G::NT), G::LDS, s, in, hin, hout, out,
                        (const _Float16*)p->fragd8_dev, (const float4*)p->tf32q_dev, (const float*)p->taps_dev, p->L, p->sh8,
                        n_out);
     NSH_CK_LAUNCH("nsh_fir_ccf(mfma decim fp16x2)");
@@ -772,7 +772,7 @@ int launch_v12(const nsh_fir_plan* p, const float2* in, const float2* hin, float
     const int64_t per_x = (nchunks + 7) / 8; // workgroups (= chunks) per XCD
     const int64_t grid = per_x * 8;
     if (grid > 0x7fffffff) return nsh::fail_msg("nsh_fir_ccf(mfma v12): stream too long for one launch");
-    hipLaunchKernelGGL((k_fir_mfma12<Q>), dim3((unsigned)grid), dim3(G::NT), G::LDS, s, in, hin, hout, out,
+    nsh::launch((k_fir_mfma12<Q>), dim3((unsigned)grid), dim3(G::NT), G::LDS, s, in, hin, hout, out,
                        (const uint4*)p->frag12_dev, (const float4*)p->tf32q_dev, (const float*)p->taps_dev, p->L, p->sh8,
                        n_out, per_x);
     NSH_CK_LAUNCH("nsh_fir_ccf(mfma fp16x2 v12)");

@@ -106,6 +106,13 @@ int nsh_event_record(void* event, void* stream)
     NSH_CK(hipEventRecord(reinterpret_cast<hipEvent_t>(event), S(stream)));
     return 0;
 }
+int nsh_time_next_launch(void* start_event, void* stop_event)
+{
+    auto& e = next_launch_events();
+    e.start = reinterpret_cast<hipEvent_t>(start_event);
+    e.stop = reinterpret_cast<hipEvent_t>(stop_event);
+    return 0;
+}
 int nsh_event_query(void* event)
 {
     hipError_t e = hipEventQuery(reinterpret_cast<hipEvent_t>(event));

@@ -43,6 +43,7 @@ SIGNATURES = {
     "nsh_event_sync": (_i, [_vp]),
     "nsh_event_elapsed_ms": (_i, [_vp, _vp, C.POINTER(_f)]),
     "nsh_stream_wait_event": (_i, [_vp, _vp]),
+    "nsh_time_next_launch": (_i, [_vp, _vp]),
     "nsh_malloc": (_i, [_i, _sz, C.POINTER(_vp)]),
     "nsh_free": (_i, [_vp]),
     "nsh_host_alloc": (_i, [_sz, C.POINTER(_vp)]),

@@ -20,6 +20,8 @@ SIGNATURES = {
     "nsr_fir_bench_create": (_i, [_i, C.POINTER(C.c_float), _i, _i, _i64, _u64, _u64, _sz, _i, C.POINTER(_vp)]),
     "nsr_fir_bench_run": (_i, [_vp]),
     "nsr_fir_bench_runs": (_i, [_vp, _i64]),
+    "nsr_fir_bench_set_batches": (_i, [_vp, _i64]),
+    "nsr_fir_bench_set_timing_stride": (_i, [_vp, _i]),
     "nsr_fir_bench_stats": (_i, [_vp, C.POINTER(_d), C.POINTER(_u64), C.POINTER(_u64), C.POINTER(_i)]),
     "nsr_fir_bench_kernel": (C.c_char_p, [_vp]),
     "nsr_fir_bench_tail": (_i, [_vp, _i64, C.POINTER(C.c_float)]),
@@ -71,6 +73,14 @@ class FirBench:
         check(lib().nsr_fir_bench_create(device, _f32p(t), self.ntaps, algo, self.n, first_index, seed,
                                          out_buf_bytes, 1 if timing else 0, C.byref(h)), "nsr_fir_bench_create")
         self._h = h
+
+    def set_timing_stride(self, stride: int):
+        """Time every stride-th FIR launch (HIP events recorded by the launch itself)."""
+        check(lib().nsr_fir_bench_set_timing_stride(self._h, int(stride)), "nsr_fir_bench_set_timing_stride")
+
+    def set_batches(self, batches: int):
+        """n-sample batches per run (one continuous stream of batches * n samples per run)."""
+        check(lib().nsr_fir_bench_set_batches(self._h, int(batches)), "nsr_fir_bench_set_batches")
 
     def run(self, count: int = 1):
         """count back-to-back flowgraph runs (fg->run() each; a loop in C for count > 1: no

@@ -758,3 +758,35 @@ def test_fir_headline_full_size(torch_cuda):
     lin = (0.5 * y + y2 - y3).abs().max().item()
     scale = y3.abs().max().item()
     assert lin <= 2e-6 * scale, (lin, scale)
+
+
+def test_time_next_launch_events(torch_cuda):
+    """nsh_time_next_launch: the next FIR launch records the event pair itself (hipExtLaunchKernel);
+    the elapsed time is positive and the setting is consumed by that one launch."""
+    import ctypes as C
+    torch = torch_cuda
+    L = nsh.lib()
+    h = _firwin127()
+    plan = nsh.FirPlan(h, 1, nsh.FIR_MFMA)
+    n = 1 << 22
+    x = orc.synth(n, 3)
+    dx, dy = dev(torch, x), torch.empty(n, dtype=torch.complex64, device="cuda")
+    hout = torch.empty(126, dtype=torch.complex64, device="cuda")
+    ev = [C.c_void_p(), C.c_void_p()]
+    for e in ev:
+        assert L.nsh_event_create(C.byref(e)) == 0
+    assert L.nsh_time_next_launch(ev[0], ev[1]) == 0
+    plan(dx, 0, hout, dy, n)
+    torch.cuda.synchronize()
+    ms = C.c_float()
+    assert L.nsh_event_sync(ev[1]) == 0
+    assert L.nsh_event_elapsed_ms(ev[0], ev[1], C.byref(ms)) == 0
+    assert 0.0 < ms.value < 50.0, ms.value
+    ok, err, _ = orc.tol_ok(host(dy)[:4096], orc.fir_ccf(x[:4096], h))
+    assert ok, err
+    plan(dx, 0, hout, dy, n)  # not timed: the events keep the first launch's times
+    torch.cuda.synchronize()
+    ms2 = C.c_float()
+    assert L.nsh_event_elapsed_ms(ev[0], ev[1], C.byref(ms2)) == 0 and ms2.value == ms.value
+    for e in ev:
+        L.nsh_event_destroy(e)
