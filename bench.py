@@ -8,9 +8,9 @@ nop_head -> [HBM-resident hip_buffer ring, preloaded] -> gr::hip::fir_filter_ccf
 region is ONE flowgraph run that streams K batches (nop_head passes K*N items; the resident ring
 holds x twice, so every batch reads x from HBM and the FIR's history carries over as in any
 continuous stream): K launches queued back to back on the partition stream, start and drain of
-the run inside the timed region. Inputs are resident in HBM before timing starts. The restart
-cost of a run (start, the executor pass, launch latency, drain detection) is reported next to it
-as `per_run_mode` (runs of one batch each, timed separately). With --gpus N every rank (one process per GPU) streams its own contiguous time
+the run inside the timed region. Inputs are resident in HBM before timing starts. (The restart
+cost of a run -- start, the executor pass, launch latency, drain detection, ~20-35 us -- is
+measured by tools/probe/stream_gap.py at K = 1) With --gpus N every rank (one process per GPU) streams its own contiguous time
 shard x[rank*N, (rank+1)*N) with the 126-sample halo regenerated from the counter-based
 source: weak scaling, no data-path collective.
 
@@ -321,7 +321,7 @@ def main():
     ap.add_argument("--algo", default="auto", choices=["auto", "mfma", "mfma_f32", "direct"])
     ap.add_argument("--fp32-leg", choices=["on", "off"], default="on",
                     help="also time the exact-fp32 matrix form (NSH_FIR_MFMA_F32) on the same flowgraph")
-    ap.add_argument("--timing-stride", type=int, default=4,
+    ap.add_argument("--timing-stride", type=int, default=2,
                     help="HIP-event timing on every k-th FIR launch of the timed run (each timed launch costs its "
                          "event packets, ~7 us)")
     ap.add_argument("--out-buf-mib", type=int, default=2048, help="FIR output hip_buffer (default: one launch per 2^28-sample step)")
@@ -488,27 +488,6 @@ def main():
         },
         "parity": {"check": "last 4096 outputs of the last step vs oracle (double accumulation), every rank",
                    "max_abs_err": err, "scale": scale, "ok": bool(ok)},
-    }
-    # the restart cost: runs of ONE batch each (start, executor pass, launch, drain), timed apart
-    fb.set_batches(1)
-    fb.set_timing_stride(1)
-    pr_runs = max(5, a.steps // 2)
-    fb.run(3)
-    barrier()
-    p0 = fb.stats()
-    t0 = time.perf_counter()
-    fb.run(pr_runs)  # complete runs back to back, looped in C
-    barrier()
-    pr_el = time.perf_counter() - t0
-    p1 = fb.stats()
-    pr_kernel_us = (p1["kernel_ms"] - p0["kernel_ms"]) / max(1, p1["launches"] - p0["launches"]) * 1e3
-    out["per_run_mode"] = {
-        "runs": pr_runs, "ms_per_run": round(pr_el / pr_runs * 1e3, 4),
-        "value": round(world * n * pr_runs / pr_el / 1e6, 1), "unit": "MSamples/s",
-        "avg_launch_us": round(pr_kernel_us, 2),
-        "restart_overhead_us": round(pr_el / pr_runs * 1e6 - pr_kernel_us * launches_per_run, 2),
-        "flowgraph_frac": round(BYTES_PER_SAMPLE * n / (pr_el / pr_runs) / 1e9 / HBM_PEAK_GBS, 4),
-        "what": "one batch per flowgraph run: each run's start, executor pass, launch and drain detection in its time",
     }
     tr, src = load_pmc_traffic(kernel, per_launch_samples)
     if tr is not None:
