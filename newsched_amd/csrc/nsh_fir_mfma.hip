@@ -81,6 +81,9 @@ namespace {
 #ifndef NSH_V12_F32T
 #define NSH_V12_F32T 1 // probe builds: 0 = finite wide-range chunks on the fp32 direct form
 #endif
+#ifndef NSH_V12_NO_EXACT
+#define NSH_V12_NO_EXACT 0 // timing probes only: no exact-path code in k_fir_mfma12 (wrong on such chunks)
+#endif
 #ifndef NSH_V12_LDS_PAD
 #define NSH_V12_LDS_PAD 0 // probe builds: extra LDS per workgroup (fewer resident workgroups per CU)
 #endif
@@ -265,7 +268,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
         const unsigned m = __builtin_amdgcn_readfirstlane(max(max(slot_max[0], slot_max[1]), max(slot_max[2], slot_max[3])));
         const unsigned z = __builtin_amdgcn_readfirstlane(min(min(slot_mnz[0], slot_mnz[1]), min(slot_mnz[2], slot_mnz[3])));
         const int s = scale_of(m);
-        const bool exact = chunk_needs_exact(m, z, s);
+        const bool exact = !NSH_V12_NO_EXACT && chunk_needs_exact(m, z, s);
         const bool f32t = NSH_V12_F32T && exact && m < 0x7f800000u; // finite: the exact-fp32 tile
         using GF = geom12f<Q>;
         static_assert(GF::H == G::H && GF::BYTES <= G::SLOTS, "the fp32 tile's image fits the planes + tap image");

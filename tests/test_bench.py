@@ -202,3 +202,24 @@ def test_bench_c5_rccl_two_gpus(torch_cuda):
     c5 = _json_line(out.stdout)["c5_pipeline"]
     assert c5["ok"] and c5["parity"]["ok"], c5
     assert all("rccl" in t for t in c5["transports"].values()), c5
+
+
+@pytest.mark.gpu
+def test_bench_c5_leg_g8_rccl_transport_with_test_double(torch_cuda):
+    """The driver's 8-GPU C5 layout (two time shards x G = 4, eight ranks: shard s's stage g on rank
+    4 s + g, three crossings per shard) on the rendezvous test double, 8 ranks on the one GPU: both
+    shards' tails parity-green, every rank on rccl."""
+    fake = os.path.join(ROOT, "build", "tests", "libfake_rccl.so")
+    env = dict(os.environ, NSH_BENCH_BACKEND="gloo", NSH_RCCL_LIB=fake, NSH_REMOTE_TEST_RCCL="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    out = subprocess.run([sys.executable, "bench.py", "--gpus", "8", "--c5-log2n", "20", "--c5-transport", "rccl",
+                          "--fp32-leg", "off", "--c5-fused", "off"] + ARGS,
+                         cwd=ROOT, capture_output=True, text=True, timeout=600, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    d = _json_line(out.stdout)
+    assert d["n_gpus"] == 8 and d["parity"]["ok"], d
+    c5 = d["c5_pipeline"]
+    assert c5["layout"] == "G=4 stage groups x 2 time shards", c5
+    assert c5["ok"] and c5["parity"]["ok"], c5
+    assert len(c5["transports"]) == 8 and all(":rccl" in t for t in c5["transports"].values()), c5
