@@ -143,7 +143,12 @@ int nsh_synth_cf32(float* out, int64_t n, uint64_t first_index, uint64_t seed, v
  * (k_fir_mfma11). In both, a 2048-input chunk whose samples (with its halo) are finite but span
  * more than the split holds takes the exact-fp32 matrix tile of NSH_FIR_MFMA_F32 (fp32 products
  * and sums; the decimators filter it undecimated and keep every decim-th output), and one
- * holding inf/NaN the fp32 direct form (exact IEEE semantics), inside the same launch;
+ * holding inf/NaN the fp32 direct form (exact IEEE semantics) -- at decim 1 in a second kernel
+ * the call enqueues right after the first on the same stream (k_fir_exact12 filters the chunks
+ * k_fir_mfma12 queued; it returns at once when none were), at decim 2 and 4 inside the same
+ * launch. A plan may be used on several streams (each has its own queue of such chunks); its
+ * first call on a stream, or a call with more chunks than any before on that stream, allocates
+ * that queue (the latter after synchronizing the stream);
  * NSH_FIR_MFMA16 (3) and NSH_FIR_MFMA_BF16X3 (4) name bf16x3 kernels retired in round 4: plan
  * creation refuses them; NSH_FIR_MFMA_F32 is the exact-fp32 Toeplitz form on the fp32-input matrix instructions
  * (decim 1, ntaps <= 257, finite taps; no operand split: fp32 products and sums, chunks with

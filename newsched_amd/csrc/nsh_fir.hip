@@ -255,6 +255,7 @@ int nsh_fir_plan_destroy(void* plan)
     if (p->tf32q_dev) (void)hipFree(p->tf32q_dev);
     if (p->fragd8_dev) (void)hipFree(p->fragd8_dev);
     if (p->casc) nsh_fir_cascade_plan_destroy(p->casc);
+    for (auto& q : p->xq) (void)hipFree(q.d);
     delete p;
     return 0;
 }

@@ -1,6 +1,7 @@
 // Internal FIR plan shared by nsh_fir.hip (direct form, dispatch) and nsh_fir_mfma.hip.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -29,6 +30,16 @@ struct nsh_fir_plan {
     void* tf32_dev = nullptr;
     void* tf32q_dev = nullptr; // the exact-fp32 tile taps of k_fir_mfma12 / k_fir_mfma11, same layout
     int QFT = 0;               // their tap blocks: 2Q - 1 (k_fir_mfma12), D (QHD - 1) + 1 (k_fir_mfma11)
+    // k_fir_mfma12's exact queue, one per stream the plan runs on (the chunks it hands to
+    // k_fir_exact12: device words [count, done, entries...], nsh_fir_mfma.hip); launches on one
+    // stream are ordered, so each stream's queue is empty again when its next launch starts
+    struct xqueue {
+        hipStream_t s;
+        unsigned* d;
+        int64_t cap;
+    };
+    mutable std::mutex xq_mu;
+    mutable std::vector<xqueue> xq;
     void* casc = nullptr; // NSH_FIR_PFFT: a one-stage nsh_fir_cascade plan (k_fir_pfft)
     int n_cu = 0;         // the device's CU count, queried once (0 = not yet)
     std::string kernel;   // the kernel nsh_fir_ccf launches (rocprof name without namespace)

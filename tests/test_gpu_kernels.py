@@ -529,6 +529,64 @@ def test_fir_mfma_exact_paths(torch_cuda, v8_form, ntaps, decim, kind):
         assert ok, (a, err, scale)
 
 
+def test_fir_mfma12_exact_queue_streams(torch_cuda):
+    """k_fir_mfma12 hands the chunks the split cannot carry to k_fir_exact12 through a queue per plan
+    and stream. One plan on two streams, calls with and without such chunks interleaved, the second
+    stream's queue grown by a longer call (1 chunk, then 2500): every call with exact chunks meets the
+    tolerance per chunk, and every call without them is bit-identical to a fresh plan's output -- a
+    queue left non-empty would have re-filtered stale chunks into it."""
+    torch = torch_cuda
+    h = _firwin127()
+    plan = _v8_plan(h, "v12")
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+
+    def call(x, stream):
+        dx = dev(torch, x)
+        hin = torch.zeros(126, dtype=torch.complex64, device="cuda")
+        hout = torch.zeros_like(hin)
+        dy = torch.full((x.size,), complex(7.0, 7.0), dtype=torch.complex64, device="cuda")
+        torch.cuda.current_stream().synchronize()
+        plan(dx, hin, hout, dy, x.size, stream=stream)
+        stream.synchronize()
+        return host(dy)
+
+    def fresh(x):
+        p = nsh.FirPlan(h, 1, nsh.FIR_MFMA)
+        y, _ = run_fir(torch, p, x, x.size)
+        p.close()
+        return y
+
+    def check_exact(y, x):
+        ref = orc.fir_ccf(x, h)
+        for a in range(0, x.size, 2048):
+            ok, err, scale = orc.tol_ok(y[a:a + 2048], ref[a:a + 2048])
+            assert ok, (a, err, scale)
+
+    xe = orc.synth(40 * 2048 + 5, 61)
+    xe[300::4096] *= np.float32(2.0 ** 40)           # every other chunk on the exact-fp32 tile
+    xe[7 * 2048 + 9] = complex(np.nan, 1.0)          # one chunk on the direct form
+    xp = orc.synth(40 * 2048 + 5, 62)                # no exact chunk
+    small = orc.synth(2048, 63)
+    small[10] *= np.float32(2.0 ** 40)
+    check_exact(call(small, s2), small)              # s2's queue: 1024 entries
+    for stream in (s1, s2, s1):
+        y = call(xe, stream)
+        nan = np.isnan(y.real) | np.isnan(y.imag)
+        ref = orc.fir_ccf(xe, h)
+        np.testing.assert_array_equal(nan, np.isnan(ref.real) | np.isnan(ref.imag))
+        ok_rows = ~(np.isnan(ref.real) | np.isnan(ref.imag))
+        for a in range(0, xe.size, 2048):
+            m = ok_rows[a:a + 2048]
+            ok, err, scale = orc.tol_ok(y[a:a + 2048][m], ref[a:a + 2048][m])
+            assert ok, (a, err, scale)
+        np.testing.assert_array_equal(call(xp, stream).view(np.uint32), fresh(xp).view(np.uint32))
+    big = orc.synth(2500 * 2048, 64)                 # grows s2's queue (2500 > 1024 entries)
+    big[500::2048] *= np.float32(2.0 ** 40)
+    check_exact(call(big, s2), big)
+    np.testing.assert_array_equal(call(xp, s2).view(np.uint32), fresh(xp).view(np.uint32))
+    plan.close()
+
+
 @pytest.mark.parametrize("decim", [1, 2, 4])
 @pytest.mark.parametrize("ntaps", [127, 61])
 def test_fir_mfma_exact_tile_mixed_stream(torch_cuda, ntaps, decim):
