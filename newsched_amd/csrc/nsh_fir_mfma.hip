@@ -81,9 +81,6 @@ namespace {
 #ifndef NSH_V12_F32T
 #define NSH_V12_F32T 1 // probe builds: 0 = finite wide-range chunks on the fp32 direct form
 #endif
-#ifndef NSH_V11_NO_EXACT
-#define NSH_V11_NO_EXACT 0 // timing probes only: k_fir_mfma11 with its exact forms compiled out (wrong on such chunks)
-#endif
 #ifndef NSH_V12_LDS_PAD
 #define NSH_V12_LDS_PAD 0 // probe builds: extra LDS per workgroup (fewer resident workgroups per CU)
 #endif
@@ -163,14 +160,22 @@ __device__ __forceinline__ void store_pair12(const float4& v, unsigned char* buf
 // hist_in), so the second kernel sees the inputs the first one saw. With the two exact forms
 // compiled into it, k_fir_mfma12 ran 3 % slower on streams that never take them (735 vs 711 us
 // per 2^28, profiles/r04i_v12_no_exact_ab.log): their code shaped the main path's registers and
-// schedule. The queue (per plan and stream, device memory): [0] queued chunks, [1] workgroups of
-// k_fir_exact12 done, [XQ_HEAD + i] entry i = (chunk << 1) | non-finite. k_fir_exact12 returns at
-// once on an empty queue; otherwise its last workgroup to finish empties it for the next launch.
+// schedule. The queue (per plan and stream, device memory, u32 words) is split into XQ_N sub-queues
+// so that a stream whose every chunk is exact does not serialise 2^17 atomics on one address
+// (one counter: k_fir_mfma12 took 1.53 ms instead of ~0.4 on such a stream, profiles/r04m_*):
+// workgroup b appends to sub-queue b mod XQ_N -- counter at word XQ_LINE (b mod XQ_N), entries
+// from word XQ_E + (b mod XQ_N) subcap, entry = (chunk << 1) | non-finite -- and word XQ_DONE counts
+// k_fir_exact12's finished workgroups. k_fir_exact12 returns at once when every counter is 0;
+// otherwise its last workgroup to finish zeroes them for the next launch on this stream.
 template <int Q>
 using geom12f = nsh_f32t::geom<2 * Q - 2, 2 * Q - 1>;
-constexpr int XQ_HEAD = 2;
+constexpr int XQ_N = 64;                   // sub-queues (one counter each)
+constexpr int XQ_LINE = 64;                // words between counters (256 B)
+constexpr int XQ_DONE = XQ_N * XQ_LINE;    // finished k_fir_exact12 workgroups
+constexpr int XQ_E = XQ_DONE + XQ_LINE;    // first entry word
+__host__ __device__ constexpr int64_t xq_subcap(int64_t grid) { return (grid + XQ_N - 1) / XQ_N; }
 #ifndef NSH_X12_PER_CU
-#define NSH_X12_PER_CU 4 // k_fir_exact12 workgroups per CU (a persistent walk over the queue)
+#define NSH_X12_PER_CU 5 // k_fir_exact12 workgroups per CU (a persistent walk over the queue) = its waves per SIMD
 #endif
 
 // chunk ch -> registers (nontemporal) and its halo (default policy: the previous chunk's tail was
@@ -201,6 +206,59 @@ __device__ __forceinline__ void load12(const float2* __restrict__ in, const floa
         const nsh::buf_f2 a = __builtin_bit_cast(nsh::buf_f2, __builtin_amdgcn_raw_buffer_load_b64(hr, off0, 0, 0));
         const nsh::buf_f2 b = __builtin_bit_cast(nsh::buf_f2, __builtin_amdgcn_raw_buffer_load_b64(hr, off1, 0, 0));
         hv = make_float4(a.x, a.y, b.x, b.y);
+    }
+}
+
+// One chunk on an exact form, from its samples in registers: finite -> the exact-fp32 tile, else the
+// fp32 direct form. Stages the chunk in LDS (after a barrier: the caller may have used LDS), then
+// filters and stores it.
+template <int Q>
+__device__ __forceinline__ void exact_chunk12(unsigned char* lds, float2* __restrict__ out, const float4* __restrict__ timg32,
+                                              const float* __restrict__ taps, int L, int64_t n_out, int64_t ch,
+                                              const float4 (&v)[4], const float4& hv, bool f32t)
+{
+    using G = geom12<Q>;
+    using GF = geom12f<Q>;
+    static_assert(GF::H == G::H && GF::BYTES <= G::SLOTS, "the fp32 tile's image fits the planes + tap image");
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int h = lane >> 5;
+    const int phase = lane & 31;
+    nsh::lds_barrier(); // every wave is done with what LDS held before
+    if (f32t) {
+        float4 t32[2];
+        nsh_f32t::load_taps<GF>(timg32, t32, tid, G::NT);
+        if (tid < G::HP) nsh_f32t::put<GF>(lds, hv, 2 * tid);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) nsh_f32t::put<GF>(lds, v[u], G::H + 2 * (tid + G::NT * u));
+        nsh_f32t::put_taps<GF>(lds, t32, tid, G::NT);
+    } else { // inf / NaN in range: the fp32 direct form (exact IEEE semantics)
+        float4* r = reinterpret_cast<float4*>(lds);
+        if (tid < G::HP) r[tid] = hv;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) r[G::HP + tid + G::NT * u] = v[u];
+    }
+    nsh::lds_barrier();
+    nf2 o[8];
+    if (f32t) {
+        nsh_f32t::f32x4 acc[4];
+        nsh_f32t::tile<GF, 2 * Q - 1>(lds, wave, lane, acc);
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int u = 0; u < 2; ++u) o[2 * t + u] = nf2{ acc[t][2 * u], acc[t][2 * u + 1] };
+    } else {
+        direct_tile9<Q>(lds, taps, L, wave, h, phase, o);
+    }
+    // direct: output wave TILE + phase + 32 ((reg & 3) + 8 (reg >> 2) + 4 h);
+    // exact-fp32 tile: output 16 (32 wave + 8 t + 2 g + u) + i of o[2 t + u] (nsh_f32t::tile)
+    const __amdgpu_buffer_rsrc_t r = chunk_rsrc<2048>(out, ch, n_out);
+    const int lb = f32t ? (16 * (32 * wave + 2 * (lane >> 4)) + (lane & 15)) * 8 : (wave * TILE + phase + 128 * h) * 8;
+#pragma unroll
+    for (int reg = 0; reg < 8; ++reg) {
+        const int c = f32t ? 128 * (4 * reg - 3 * (reg & 1)) : 256 * ((reg & 3) + 8 * (reg >> 2));
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(nsh::u32x2, o[reg]), r, lb, c, nsh::AUX_ST);
     }
 }
 
@@ -285,9 +343,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
     if (__builtin_expect(chunk_needs_exact(m, z, s), 0)) {
         // k_fir_exact12 filters it (a vector atomic and a vector store from one lane)
         if (tid == 0) {
-            const unsigned i = __hip_atomic_fetch_add(xq, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(xq + XQ_HEAD + i, (unsigned)(ch << 1) | (m >= 0x7f800000u ? 1u : 0u), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned k = blockIdx.x % XQ_N;
+            const unsigned i = __hip_atomic_fetch_add(xq + XQ_LINE * k, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(xq + XQ_E + k * xq_subcap(gridDim.x) + i, (unsigned)(ch << 1) | (m >= 0x7f800000u ? 1u : 0u),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     } else {
         if (tid < G::HP) store_pair12<Q>(hv, lds, 2 * tid, s);
@@ -361,89 +420,61 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
 // CU), one chunk per workgroup step, staged in the same LDS geometry (the fp32 tile's image fits
 // the planes + tap image; a raw fp32 chunk + halo fits the planes).
 template <int Q>
-__global__ __launch_bounds__(256) void k_fir_exact12(const float2* __restrict__ in,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NSH_X12_PER_CU))) void k_fir_exact12(const float2* __restrict__ in,
                                                     const float2* __restrict__ hist_in,
                                                     float2* __restrict__ out,
                                                     const float4* __restrict__ timg32, // exact-fp32 tile taps [4][TWF]
                                                     const float* __restrict__ taps,
                                                     unsigned* __restrict__ xq,
+                                                    int64_t subcap,
                                                     int L,
                                                     int64_t n_out)
 {
-    using G = geom12<Q>;
-    using GF = geom12f<Q>;
-    static_assert(GF::H == G::H && GF::BYTES <= G::SLOTS, "the fp32 tile's image fits the planes + tap image");
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    const unsigned cnt = __hip_atomic_load(xq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (cnt == 0) return; // nothing queued (the common case): nothing to empty either
+    static_assert(XQ_N == 64, "one sub-queue counter per lane");
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    const int wave = tid >> 6;
-    const int h = lane >> 5;
-    const int phase = lane & 31;
+    // every wave: the XQ_N counters (one per lane) and their inclusive prefix sum
+    unsigned incl = __hip_atomic_load(xq + XQ_LINE * lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const unsigned t = __shfl_up(incl, d);
+        if (lane >= d) incl += t;
+    }
+    const unsigned cnt = __builtin_amdgcn_readlane(incl, 63);
+    if (cnt == 0) return; // nothing queued (the common case): nothing to empty either
+    auto entry = [&](unsigned i) {
+        const int k = __popcll(__ballot(incl <= i)); // sub-queue holding queued chunk i (prefix sums ascend)
+        const unsigned start = k ? __shfl(incl, k - 1) : 0u;
+        return __hip_atomic_load(xq + XQ_E + k * subcap + (i - start), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
     for (unsigned i = blockIdx.x; i < cnt; i += gridDim.x) {
-        const unsigned e = __hip_atomic_load(xq + XQ_HEAD + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int64_t ch = e >> 1;
-        const bool f32t = NSH_V12_F32T && !(e & 1u); // finite: the exact-fp32 tile
+        const unsigned e = entry(i);
         float4 v[4], hv;
-        load12<Q>(in, hist_in, L, n_out, ch, v, hv);
-        nsh::lds_barrier(); // every wave is done with the previous chunk's LDS
-        if (f32t) {
-            float4 t32[2];
-            nsh_f32t::load_taps<GF>(timg32, t32, tid, G::NT);
-            if (tid < G::HP) nsh_f32t::put<GF>(lds, hv, 2 * tid);
-#pragma unroll
-            for (int u = 0; u < 4; ++u) nsh_f32t::put<GF>(lds, v[u], G::H + 2 * (tid + G::NT * u));
-            nsh_f32t::put_taps<GF>(lds, t32, tid, G::NT);
-        } else { // inf / NaN in range: the fp32 direct form (exact IEEE semantics)
-            float4* r = reinterpret_cast<float4*>(lds);
-            if (tid < G::HP) r[tid] = hv;
-#pragma unroll
-            for (int u = 0; u < 4; ++u) r[G::HP + tid + G::NT * u] = v[u];
-        }
-        nsh::lds_barrier();
-        nf2 o[8];
-        if (f32t) {
-            nsh_f32t::f32x4 acc[4];
-            nsh_f32t::tile<GF, 2 * Q - 1>(lds, wave, lane, acc);
-#pragma unroll
-            for (int t = 0; t < 4; ++t)
-#pragma unroll
-                for (int u = 0; u < 2; ++u) o[2 * t + u] = nf2{ acc[t][2 * u], acc[t][2 * u + 1] };
-        } else {
-            direct_tile9<Q>(lds, taps, L, wave, h, phase, o);
-        }
-        // direct: output wave TILE + phase + 32 ((reg & 3) + 8 (reg >> 2) + 4 h);
-        // exact-fp32 tile: output 16 (32 wave + 8 t + 2 g + u) + i of o[2 t + u] (nsh_f32t::tile)
-        const __amdgpu_buffer_rsrc_t r = chunk_rsrc<2048>(out, ch, n_out);
-        const int lb = f32t ? (16 * (32 * wave + 2 * (lane >> 4)) + (lane & 15)) * 8 : (wave * TILE + phase + 128 * h) * 8;
-#pragma unroll
-        for (int reg = 0; reg < 8; ++reg) {
-            const int c = f32t ? 128 * (4 * reg - 3 * (reg & 1)) : 256 * ((reg & 3) + 8 * (reg >> 2));
-            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(nsh::u32x2, o[reg]), r, lb, c, nsh::AUX_ST);
-        }
+        load12<Q>(in, hist_in, L, n_out, e >> 1, v, hv);
+        exact_chunk12<Q>(lds, out, timg32, taps, L, n_out, e >> 1, v, hv, NSH_V12_F32T && !(e & 1u));
     }
     // the last workgroup to get here empties the queue for the next launch on this stream (every
     // workgroup read the count above before counting itself done)
+    __shared__ unsigned last;
     __syncthreads();
-    if (tid == 0) {
-        const unsigned d = __hip_atomic_fetch_add(xq + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-        if (d == gridDim.x - 1) {
-            __hip_atomic_store(xq, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(xq + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+    if (tid == 0)
+        last = __hip_atomic_fetch_add(xq + XQ_DONE, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    __syncthreads();
+    if (last && tid < 64) { // wave 0: every counter, one lane each (vector stores), and the done count
+        __hip_atomic_store(xq + XQ_LINE * tid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (tid == 0) __hip_atomic_store(xq + XQ_DONE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
-// k_fir_mfma11's exact chunks (round 4, as k_fir_mfma12's): a chunk the split cannot carry is
-// queued by k_fir_mfma11 and filtered by k_fir_exact11 right after it on the same stream -- a finite
-// chunk whose range the split cannot hold as if undecimated by k_fir_f32mfma's tile
-// (nsh_fir_f32_tile.hpp, QF = HR + 1 tap blocks of 16 over the chunk's D H-sample halo) with every
-// D-th output kept (the same fp32 matrix work per input sample as at decim 1, no polyphase form), one
-// holding inf/NaN by the fp32 direct form. Each plane buffer holds the tile's two fp32 planes (at
-// <2,5> and <4,3> they fit the split's buffer; other forms may grow it); the tile's taps (one copy,
-// loaded once per workgroup) and a per-wave output scratch (the tile's lane map -> the split path's,
-// for the common store) follow the stash.
+// k_fir_mfma11's LDS with the exact-fp32 tile: a finite chunk whose range the split cannot hold is
+// filtered as if undecimated by k_fir_f32mfma's tile (nsh_fir_f32_tile.hpp, QF = HR + 1 tap blocks
+// of 16 over the chunk's D H-sample halo) and every D-th output kept -- the same fp32 matrix work per
+// input sample as at decim 1, no polyphase form. Each plane buffer holds the tile's two fp32 planes
+// (at <2,5> and <4,3> they fit the split's buffer; other forms may grow it); the tile's taps (one
+// copy, loaded once per workgroup) and a per-wave output scratch (the tile's lane map -> the split
+// path's, for the common store) follow the stash. LDS stays within 2 resident workgroups per CU
+// (the kernel's occupancy).
 template <int D, int QH>
 struct geom11x : geom11<D, QH> {
     using B = geom11<D, QH>;
@@ -451,11 +482,13 @@ struct geom11x : geom11<D, QH> {
     static constexpr int QF = HRF + 1;
     using GF = nsh_f32t::geom<HRF, QF>;
     static constexpr int BUF = (B::BUF > 2 * GF::PLANE ? B::BUF : 2 * GF::PLANE);
-    static constexpr int TAPF = BUF;                               // tile taps
+    static constexpr int STASH_AT = 2 * BUF;
+    static constexpr int TAPF = STASH_AT + 2 * B::STASH;          // tile taps
     static constexpr int SCR = TAPF + (GF::TAPS + 255) / 256 * 256; // [4 waves][WAVE_OUT] float2
-    static constexpr int LDS = SCR + 4 * B::WAVE_OUT * 8;
+    static constexpr int SLOTS = SCR + 4 * B::WAVE_OUT * 8;
+    static constexpr int LDS = SLOTS + 64;
     static_assert(GF::H == D * B::H && BUF % 256 == 0, "tile halo = the chunk's halo");
-    static_assert((B::HP + 1024) * 16 <= BUF, "a raw fp32 chunk + halo fits the buffer");
+    static_assert(2 * LDS <= 160 * 1024, "2 workgroups per CU");
 };
 
 template <int D, int QH>
@@ -464,16 +497,18 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma11(const float2* __restrict_
                                                       float2* __restrict__ hist_out,
                                                       float2* __restrict__ out,
                                                       const _Float16* __restrict__ frag, // per phase: [2][KS][64] x8, [2][64] x4
-                                                      unsigned* __restrict__ xq,         // exact queue (k_fir_mfma12)
+                                                      const float4* __restrict__ timg32, // tile taps [4][TWF]
+                                                      const float* __restrict__ taps,
                                                       int L,
                                                       int sh,
                                                       int64_t n_out)
 {
-    using G = geom11<D, QH>;
+    using G = geom11x<D, QH>;
+    using GF = typename G::GF;
     constexpr int KS = G::KS;
     typedef float f32x4 __attribute__((ext_vector_type(4)));
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    float4* stash = reinterpret_cast<float4*>(lds + 2 * G::BUF); // [2][HP] raw halo sources
+    float4* stash = reinterpret_cast<float4*>(lds + G::STASH_AT); // [2][HP] raw halo sources
     unsigned* slot_max = reinterpret_cast<unsigned*>(lds + G::SLOTS);
     unsigned* slot_mnz = slot_max + 8;
 
@@ -481,6 +516,11 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma11(const float2* __restrict_
     const int lane = tid & 63;
     const int wave = tid >> 6;
     const int64_t n_in = n_out * D;
+    {   // the tile's taps, once per workgroup (read after the prologue's barriers)
+        float4 t32[2];
+        nsh_f32t::load_taps<GF>(timg32, t32, tid, G::NT);
+        nsh_f32t::put_taps_at<GF>(lds + G::TAPF, t32, tid, G::NT);
+    }
 
     if (blockIdx.x == 0) {
         for (int j = tid; j < L - 1; j += G::NT) hist_out[j] = virt(in, hist_in, n_in - (L - 1) + j, n_in, L);
@@ -534,9 +574,25 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma11(const float2* __restrict_
             for (int f = 0; f < D; ++f) st[(tid - (G::NT - G::H / 2)) * D + f] = v[(G::UNITS - 1) * D + f];
         }
     };
-    // chunk -> the split phase planes of buf (an exact chunk is not staged: k_fir_exact11 filters it)
-    auto put_chunk = [&](unsigned char* buf, const float4* hsrc, const float4 (&v)[4], bool exact, int sc) {
-        if (__builtin_expect(exact, 0)) return;
+    // chunk -> buffer: raw fp32 (halo float4 [0, HP), chunk float4 HP + j) or split phase planes
+    auto put_chunk = [&](unsigned char* buf, const float4* hsrc, const float4 (&v)[4], bool raw, bool f32t, int sc) {
+        if (__builtin_expect(f32t, 0)) { // the tile's fp32 planes (16-sample rows), halo first
+            if (tid < G::HP) nsh_f32t::put<GF>(buf, hsrc[tid], 2 * tid);
+#pragma unroll
+            for (int u = 0; u < G::UNITS; ++u)
+#pragma unroll
+                for (int f = 0; f < D; ++f) nsh_f32t::put<GF>(buf, v[u * D + f], GF::H + 2 * ((tid + G::NT * u) * D + f));
+            return;
+        }
+        if (raw) {
+            float4* rb = reinterpret_cast<float4*>(buf);
+            if (tid < G::HP) rb[tid] = hsrc[tid];
+#pragma unroll
+            for (int u = 0; u < G::UNITS; ++u)
+#pragma unroll
+                for (int f = 0; f < D; ++f) rb[G::HP + (tid + G::NT * u) * D + f] = v[u * D + f];
+            return;
+        }
         if (tid < D * (G::H / 2)) { // halo: phase r, pair pi from the raw halo samples
             const int r = tid / (G::H / 2), pi = tid % (G::H / 2);
             const int sr = r == 0 ? 0 : D - r;
@@ -621,6 +677,61 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma11(const float2* __restrict_
                                     (nf2{ lo[t][2 * half], lo[t][2 * half + 1] } + nf2{ lo_t[t][2 * half], lo_t[t][2 * half + 1] });
         unscale_tile(sum, unscale, o);
     };
+    // exact path: y[m] = sum_k h[k] x[D m - k] from the raw chunk (float2 index D H + D m - k)
+    // exact path. D = 4: outputs 0 and 1 are 64 input samples apart and share their inputs
+    // (direct_group; decim_qh gives L - 1 <= D H and every k <= D (H - 16) below L): dense-exact
+    // floor 74.7 -> 97.6 GS/s input. D = 2 keeps one output at a time: its two unrolled groups
+    // cost the main path a third of its speed (594 -> 890 us per 2^28, profiles/r02o_*).
+    auto direct_tile = [&](const unsigned char* cur, nf2 (&o)[2 * G::TILES]) {
+        if constexpr (D == 4 || NSH_DECIM2_SHARED) {
+#pragma unroll 1
+            for (int t = 0; t < G::TILES; ++t) {
+                nf2 acc[2];
+                direct_group<2, 16 * D, D * G::H, D * (G::H - 16)>(
+                    reinterpret_cast<const nf2*>(cur), D * G::H + D * (wave * G::WAVE_OUT + (8 * t + 2 * g) * 16 + phase), taps, L, acc);
+                if (t == 0) {
+                    o[0] = acc[0];
+                    o[1] = acc[1];
+                } else {
+                    o[2 * G::TILES - 2] = acc[0];
+                    o[2 * G::TILES - 1] = acc[1];
+                }
+            }
+        } else {
+            const float2* raw = reinterpret_cast<const float2*>(cur);
+            for (int oi = 0; oi < 2 * G::TILES; ++oi) {
+                const int blk = (oi >> 1) * 8 + 2 * g + (oi & 1);
+                const int j = D * G::H + D * (wave * G::WAVE_OUT + blk * 16 + phase);
+                float re = 0.f, im = 0.f;
+                for (int k = 0; k < L; ++k) {
+                    const float2 x = raw[j - k];
+                    re = fmaf(taps[k], x.x, re);
+                    im = fmaf(taps[k], x.y, im);
+                }
+                o[oi] = nf2{ re, im };
+            }
+        }
+    };
+    // the tile's outputs n = 16 (32 wave + 8 t + 2 g + u) + i (undecimated), the lanes with
+    // i mod D = 0 keeping theirs (m = n / D), through the wave's LDS scratch into the split
+    // path's lane map (the wave's own outputs: a wave barrier, no workgroup barrier)
+    auto f32_tile = [&](const unsigned char* cur, nf2 (&o)[2 * G::TILES]) {
+        f32x4 acc[4];
+        nsh_f32t::tile_at<GF, G::QF>(cur, lds + G::TAPF, wave, lane, acc);
+        nf2* scr = reinterpret_cast<nf2*>(lds + G::SCR) + wave * G::WAVE_OUT;
+        const int i = lane & 15;
+        if (i % D == 0) {
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+#pragma unroll
+                for (int u = 0; u < 2; ++u) scr[(16 * (8 * t + 2 * g + u) + i) / D] = nf2{ acc[t][2 * u], acc[t][2 * u + 1] };
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int oi = 0; oi < 2 * G::TILES; ++oi) o[oi] = scr[((oi >> 1) * 8 + 2 * g + (oi & 1)) * 16 + phase];
+    };
     auto store_tile = [&](int64_t ch, const nf2 (&o)[2 * G::TILES]) {
         const __amdgpu_buffer_rsrc_t r = chunk_rsrc<G::CHUNK>(out, ch, n_out);
 #pragma unroll
@@ -653,9 +764,9 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma11(const float2* __restrict_
     unsigned m_prev = max(max(slot_max[0], slot_max[1]), max(slot_max[2], slot_max[3]));
     unsigned z_prev = min(min(slot_mnz[0], slot_mnz[1]), min(slot_mnz[2], slot_mnz[3]));
     int s_cur = scale_of(m_prev);
-    bool ex_cur = !NSH_V11_NO_EXACT && chunk_needs_exact(m_prev, z_prev, s_cur);
-    bool nf_cur = m_prev >= 0x7f800000u; // inf / NaN in range (the direct form)
-    put_chunk(lds, stash + G::HP, va, ex_cur, s_cur);
+    bool ex_cur = chunk_needs_exact(m_prev, z_prev, s_cur);
+    bool f32_cur = ex_cur && m_prev < 0x7f800000u; // finite: the exact-fp32 tile
+    put_chunk(lds, stash + G::HP, va, ex_cur, f32_cur, s_cur);
     stash_tail(stash, va);
     load(va, clamp(c_begin + 1));
     load(vb, clamp(c_begin + 2));
@@ -679,22 +790,21 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma11(const float2* __restrict_
         const unsigned z_nxt = min(min(slot_mnz[4 * pn], slot_mnz[4 * pn + 1]), min(slot_mnz[4 * pn + 2], slot_mnz[4 * pn + 3]));
         const unsigned m2 = max(m_prev, m_nxt);
         const int s_nxt = scale_of(m2);
-        const bool ex_nxt = !NSH_V11_NO_EXACT && chunk_needs_exact(m2, min(z_prev, z_nxt), s_nxt);
+        const bool ex_nxt = chunk_needs_exact(m2, min(z_prev, z_nxt), s_nxt);
+        const bool f32_nxt = ex_nxt && m2 < 0x7f800000u;
         load(ld, clamp(ch + 3));
-        put_chunk(nbuf, stash + pi * G::HP, nxt, ex_nxt, s_nxt);
+        put_chunk(nbuf, stash + pi * G::HP, nxt, ex_nxt, f32_nxt, s_nxt);
         stash_tail(stash + pn * G::HP, nxt);
+        nf2 o[2 * G::TILES];
         if (__builtin_expect(ex_cur, 0)) {
-            // k_fir_exact11 filters it (a vector atomic and a vector store from one lane)
-            if (tid == 0) {
-                const unsigned q = __hip_atomic_fetch_add(xq, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(xq + XQ_HEAD + q, (unsigned)(ch << 1) | (nf_cur ? 1u : 0u), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            }
+            if (f32_cur)
+                f32_tile(cur, o);
+            else
+                direct_tile(cur, o);
         } else {
-            nf2 o[2 * G::TILES];
             mfma_tile(cur, -(s_cur + sh), o);
-            store_tile(ch, o);
         }
+        store_tile(ch, o);
         unsigned m, z;
         reduce(nn, m, z);
         if (lane == 0) {
@@ -704,7 +814,7 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma11(const float2* __restrict_
         m_prev = m_nxt;
         z_prev = z_nxt;
         ex_cur = ex_nxt;
-        nf_cur = m2 >= 0x7f800000u;
+        f32_cur = f32_nxt;
         s_cur = s_nxt;
         nsh::lds_barrier();
     };
@@ -718,144 +828,19 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma11(const float2* __restrict_
     if (ch <= c_last) step(vb, vc, va, ch);
 }
 
-// The chunks k_fir_mfma11 queued: a persistent walk over the queue (NSH_X12_PER_CU workgroups per
-// CU). The chunk's D H-sample halo is read from the input (or the history) again.
-template <int D, int QH>
-__global__ __launch_bounds__(256) void k_fir_exact11(const float2* __restrict__ in,
-                                                    const float2* __restrict__ hist_in,
-                                                    float2* __restrict__ out,
-                                                    const float4* __restrict__ timg32, // tile taps [4][TWF]
-                                                    const float* __restrict__ taps,
-                                                    unsigned* __restrict__ xq,
-                                                    int L,
-                                                    int64_t n_out)
-{
-    using G = geom11x<D, QH>;
-    using GF = typename G::GF;
-    typedef float f32x4 __attribute__((ext_vector_type(4)));
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    const unsigned cnt = __hip_atomic_load(xq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (cnt == 0) return; // nothing queued (the common case): nothing to empty either
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = tid >> 6;
-    const int g = lane >> 4;
-    const int phase = lane & 15;
-    const int64_t n_in = n_out * D;
-    {   // the tile's taps, once per workgroup (read after the loop's first barrier)
-        float4 t32[2];
-        nsh_f32t::load_taps<GF>(timg32, t32, tid, G::NT);
-        nsh_f32t::put_taps_at<GF>(lds + G::TAPF, t32, tid, G::NT);
-    }
-    for (unsigned i = blockIdx.x; i < cnt; i += gridDim.x) {
-        const unsigned e = __hip_atomic_load(xq + XQ_HEAD + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int64_t ch = e >> 1;
-        const bool f32t = !(e & 1u); // finite: the exact-fp32 tile
-        float4 v[4];
-        {
-            const __amdgpu_buffer_rsrc_t r = chunk_rsrc<G::CHUNK_IN>(in, ch, n_in);
-#pragma unroll
-            for (int u = 0; u < G::UNITS; ++u)
-#pragma unroll
-                for (int f = 0; f < D; ++f) v[u * D + f] = buf_load_f4(r, ((tid + G::NT * u) * D + f) * 16);
-        }
-        float4 hv = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (tid < G::HP) {
-            const int64_t gg = ch * G::CHUNK_IN - 2 * G::HP + 2 * tid;
-            const float2 x0 = virt(in, hist_in, gg, n_in, L), x1 = virt(in, hist_in, gg + 1, n_in, L);
-            hv = make_float4(x0.x, x0.y, x1.x, x1.y);
-        }
-        nsh::lds_barrier(); // every wave is done with the previous chunk's LDS
-        if (f32t) { // the tile's fp32 planes (16-sample rows), halo first
-            if (tid < G::HP) nsh_f32t::put<GF>(lds, hv, 2 * tid);
-#pragma unroll
-            for (int u = 0; u < G::UNITS; ++u)
-#pragma unroll
-                for (int f = 0; f < D; ++f) nsh_f32t::put<GF>(lds, v[u * D + f], GF::H + 2 * ((tid + G::NT * u) * D + f));
-        } else {    // raw fp32: halo float4 [0, HP), chunk float4 HP + j
-            float4* rb = reinterpret_cast<float4*>(lds);
-            if (tid < G::HP) rb[tid] = hv;
-#pragma unroll
-            for (int u = 0; u < G::UNITS; ++u)
-#pragma unroll
-                for (int f = 0; f < D; ++f) rb[G::HP + (tid + G::NT * u) * D + f] = v[u * D + f];
-        }
-        nsh::lds_barrier();
-        nf2 o[2 * G::TILES];
-        if (f32t) {
-            // the tile's outputs n = 16 (32 wave + 8 t + 2 g + u) + i (undecimated), the lanes with
-            // i mod D = 0 keeping theirs (m = n / D), through the wave's LDS scratch into the split
-            // path's lane map (the wave's own outputs: a wave barrier, no workgroup barrier)
-            f32x4 acc[4];
-            nsh_f32t::tile_at<GF, G::QF>(lds, lds + G::TAPF, wave, lane, acc);
-            nf2* scr = reinterpret_cast<nf2*>(lds + G::SCR) + wave * G::WAVE_OUT;
-            const int ii = lane & 15;
-            if (ii % D == 0) {
-#pragma unroll
-                for (int t = 0; t < 4; ++t)
-#pragma unroll
-                    for (int u = 0; u < 2; ++u) scr[(16 * (8 * t + 2 * g + u) + ii) / D] = nf2{ acc[t][2 * u], acc[t][2 * u + 1] };
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-            for (int oi = 0; oi < 2 * G::TILES; ++oi) o[oi] = scr[((oi >> 1) * 8 + 2 * g + (oi & 1)) * 16 + phase];
-        } else if constexpr (D == 4 || NSH_DECIM2_SHARED) {
-            // y[m] = sum_k h[k] x[D m - k] from the raw chunk (float2 index D H + D m - k). D = 4:
-            // outputs 0 and 1 are 64 input samples apart and share their inputs (direct_group;
-            // decim_qh gives L - 1 <= D H and every k <= D (H - 16) below L)
-#pragma unroll 1
-            for (int t = 0; t < G::TILES; ++t) {
-                nf2 acc[2];
-                direct_group<2, 16 * D, D * G::H, D * (G::H - 16)>(
-                    reinterpret_cast<const nf2*>(lds), D * G::H + D * (wave * G::WAVE_OUT + (8 * t + 2 * g) * 16 + phase), taps, L, acc);
-                o[2 * t] = acc[0];
-                o[2 * t + 1] = acc[1];
-            }
-        } else { // D = 2: one output at a time
-            const float2* raw = reinterpret_cast<const float2*>(lds);
-            for (int oi = 0; oi < 2 * G::TILES; ++oi) {
-                const int blk = (oi >> 1) * 8 + 2 * g + (oi & 1);
-                const int j = D * G::H + D * (wave * G::WAVE_OUT + blk * 16 + phase);
-                float re = 0.f, im = 0.f;
-                for (int k = 0; k < L; ++k) {
-                    const float2 x = raw[j - k];
-                    re = fmaf(taps[k], x.x, re);
-                    im = fmaf(taps[k], x.y, im);
-                }
-                o[oi] = nf2{ re, im };
-            }
-        }
-        const __amdgpu_buffer_rsrc_t r = chunk_rsrc<G::CHUNK>(out, ch, n_out);
-#pragma unroll
-        for (int oi = 0; oi < 2 * G::TILES; ++oi)
-            buf_store_f2(r, (wave * G::WAVE_OUT + ((oi >> 1) * 8 + 2 * g + (oi & 1)) * 16 + phase) * 8, o[oi]);
-    }
-    // the last workgroup to get here empties the queue for the next launch on this stream
-    __syncthreads();
-    if (tid == 0) {
-        const unsigned d = __hip_atomic_fetch_add(xq + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-        if (d == gridDim.x - 1) {
-            __hip_atomic_store(xq, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(xq + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-}
-
-// The plan's exact queue for stream s, with room for nchunks entries. Grown (rare: the first call
+// The plan's exact queue for stream s, at least `words` u32 long. Grown (rare: the first call
 // with more chunks than any before on this stream) after the stream has drained, so no launch
 // still uses the old one; a new queue starts empty in stream order.
-unsigned* exact_queue(const nsh_fir_plan* p, hipStream_t s, int64_t nchunks, hipError_t& e)
+unsigned* exact_queue(const nsh_fir_plan* p, hipStream_t s, int64_t words, hipError_t& e)
 {
     e = hipSuccess;
     std::lock_guard<std::mutex> g(p->xq_mu);
     nsh_fir_plan::xqueue* q = nullptr;
     for (auto& x : p->xq)
         if (x.s == s) q = &x;
-    if (q && q->cap >= nchunks) return q->d;
-    int64_t cap = 1024;
-    while (cap < nchunks) cap *= 2;
+    if (q && q->cap >= words) return q->d;
+    int64_t cap = XQ_E + 1024;
+    while (cap < words) cap *= 2;
     if (q) {
         if ((e = hipStreamSynchronize(s)) != hipSuccess) return nullptr;
         (void)hipFree(q->d);
@@ -866,8 +851,8 @@ unsigned* exact_queue(const nsh_fir_plan* p, hipStream_t s, int64_t nchunks, hip
         q = &p->xq.back();
     }
     unsigned* d = nullptr;
-    if ((e = hipMalloc(&d, (size_t)(XQ_HEAD + cap) * sizeof(unsigned))) != hipSuccess) return nullptr;
-    if ((e = hipMemsetAsync(d, 0, XQ_HEAD * sizeof(unsigned), s)) != hipSuccess) {
+    if ((e = hipMalloc(&d, (size_t)cap * sizeof(unsigned))) != hipSuccess) return nullptr;
+    if ((e = hipMemsetAsync(d, 0, XQ_E * sizeof(unsigned), s)) != hipSuccess) {
         (void)hipFree(d);
         return nullptr;
     }
@@ -880,25 +865,17 @@ template <int D, int QH>
 int launch_v11(const nsh_fir_plan* p, const float2* in, const float2* hin, float2* hout, float2* out, int64_t n_out,
                hipStream_t s)
 {
-    using G = geom11<D, QH>;
-    using GX = geom11x<D, QH>;
-    if (p->QFT != GX::QF) return nsh::fail_msg("nsh_fir_ccf(mfma decim): tile tap image does not match the kernel");
+    using G = geom11x<D, QH>;
+    if (p->QFT != G::QF) return nsh::fail_msg("nsh_fir_ccf(mfma decim): tile tap image does not match the kernel");
     NSH_CK(set_lds_attr((const void*)k_fir_mfma11<D, QH>, G::LDS, p->dev));
-    NSH_CK(set_lds_attr((const void*)k_fir_exact11<D, QH>, GX::LDS, p->dev));
     const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
     const int n_cu = plan_cus(p);
     const int64_t max_grid = (int64_t)n_cu * 2; // launch_v9's longer grids measured 4-7 % slower here
     const unsigned grid = (unsigned)(nchunks < max_grid ? nchunks : max_grid);
-    hipError_t e;
-    unsigned* xq = exact_queue(p, s, nchunks, e);
-    if (!xq) return nsh::fail(e, "nsh_fir_ccf(mfma decim): exact queue");
     nsh::launch((k_fir_mfma11<D, QH>), dim3(grid), dim3(G::NT), G::LDS, s, in, hin, hout, out,
-                (const _Float16*)p->fragd8_dev, xq, p->L, p->sh8, n_out);
+                       (const _Float16*)p->fragd8_dev, (const float4*)p->tf32q_dev, (const float*)p->taps_dev, p->L, p->sh8,
+                       n_out);
     NSH_CK_LAUNCH("nsh_fir_ccf(mfma decim fp16x2)");
-    const int64_t xcap = (int64_t)n_cu * NSH_X12_PER_CU;
-    hipLaunchKernelGGL((k_fir_exact11<D, QH>), dim3((unsigned)(nchunks < xcap ? nchunks : xcap)), dim3(G::NT), GX::LDS, s,
-                       in, hin, out, (const float4*)p->tf32q_dev, (const float*)p->taps_dev, xq, p->L, n_out);
-    NSH_CK_LAUNCH("nsh_fir_ccf(mfma decim exact chunks)");
     return 0;
 }
 
@@ -928,14 +905,15 @@ int launch_v12(const nsh_fir_plan* p, const float2* in, const float2* hin, float
     const int64_t grid = per_x * 8;
     if (grid > 0x7fffffff) return nsh::fail_msg("nsh_fir_ccf(mfma v12): stream too long for one launch");
     hipError_t e;
-    unsigned* xq = exact_queue(p, s, nchunks, e);
+    const int64_t subcap = xq_subcap(grid);
+    unsigned* xq = exact_queue(p, s, XQ_E + XQ_N * subcap, e);
     if (!xq) return nsh::fail(e, "nsh_fir_ccf(mfma v12): exact queue");
     nsh::launch((k_fir_mfma12<Q>), dim3((unsigned)grid), dim3(G::NT), G::LDS, s, in, hin, hout, out,
                 (const uint4*)p->frag12_dev, xq, p->L, p->sh8, n_out, per_x);
     NSH_CK_LAUNCH("nsh_fir_ccf(mfma fp16x2 v12)");
     const int64_t xcap = (int64_t)plan_cus(p) * NSH_X12_PER_CU;
     hipLaunchKernelGGL((k_fir_exact12<Q>), dim3((unsigned)(nchunks < xcap ? nchunks : xcap)), dim3(G::NT), G::LDS, s, in,
-                       hin, out, (const float4*)p->tf32q_dev, (const float*)p->taps_dev, xq, p->L, n_out);
+                       hin, out, (const float4*)p->tf32q_dev, (const float*)p->taps_dev, xq, subcap, p->L, n_out);
     NSH_CK_LAUNCH("nsh_fir_ccf(mfma v12 exact chunks)");
     return 0;
 }

@@ -16,5 +16,9 @@ DECIM=4 timeout -k 10 150 python tools/probe/lib_abn.py $B $E $F > $O/ab_d4_1.lo
 DECIM=4 timeout -k 10 150 python tools/probe/lib_abn.py $F $E $B > $O/ab_d4_2.log 2>&1 &&
 DECIM=2 INPUT=spike4 timeout -k 10 150 python tools/probe/lib_abn.py $B $E > $O/ab_d2_spike4.log 2>&1 &&
 DECIM=4 INPUT=spike4 timeout -k 10 150 python tools/probe/lib_abn.py $B $E > $O/ab_d4_spike4.log 2>&1 &&
+P=build/abl/nsh_fir_mfma_p64.so; X=build/abl/nsh_fir_mfma_x2.so
+timeout -k 10 150 python tools/probe/lib_abn.py $E $P > $O/ab_p64_1.log 2>&1 &&
+timeout -k 10 150 python tools/probe/lib_abn.py $P $E > $O/ab_p64_2.log 2>&1 &&
+INPUT=spike1 ROUNDS=4 timeout -k 10 150 python tools/probe/lib_abn.py $E $X > $O/ab_x2_spike1.log 2>&1 &&
 timeout -k 10 300 python -u tools/probe/cliff.py --reps 5 > $O/cliff.log 2>&1 &&
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1
