@@ -254,6 +254,33 @@ def run_fp32_leg(a, n, taps, first, device, barrier, dist, tdev, torch, orc, nsr
             "parity": {"max_abs_err": err, "ok": bool(ok)}}
 
 
+def run_copy_leg(n, barrier, torch, nsh):
+    """The measured STREAM-copy ceiling beside the spec peak: nsh_copy (k_copy_v4) of
+    the headline's 2^log2n complex samples, i.e. the same 16 B per sample the FIR moves, timed with
+    HIP events on its stream after a short warm-up."""
+    x = torch.empty(n, dtype=torch.complex64, device="cuda")
+    y = torch.empty_like(x)
+    nsh.synth(x, n, 0)
+    s = torch.cuda.Stream()
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < 0.3:
+        nsh.copy(x, y, 8 * n, stream=s)
+        s.synchronize()
+    reps = 10
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    barrier()
+    e0.record(s)
+    for _ in range(reps):
+        nsh.copy(x, y, 8 * n, stream=s)
+    e1.record(s)
+    s.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    del x, y
+    gbs = BYTES_PER_SAMPLE * n / (ms * 1e-3) / 1e9
+    return {"kernel": "k_copy_v4", "avg_launch_us": round(ms * 1e3, 2), "GBs": round(gbs, 1),
+            "frac_of_peak": round(gbs / HBM_PEAK_GBS, 4)}
+
+
 def run_c5_fused_leg(a, first, device, barrier, dist, tdev, torch, orc, nsh):
     """BASELINE config C5's chain 4 x fir_filter_ccf(firwin(127, 0.45), 2) as the fused kernel
     scheduler_hip puts in its place (hip::fir_filter_cascade_ccf -> nsh_fir_cascade_ccf,
@@ -489,6 +516,9 @@ def main():
         "parity": {"check": "last 4096 outputs of the last step vs oracle (double accumulation), every rank",
                    "max_abs_err": err, "scale": scale, "ok": bool(ok)},
     }
+    cp = run_copy_leg(n, barrier, torch, nsh)
+    out["roofline"]["copy_measured"] = cp
+    out["roofline"]["frac_of_copy"] = round(achieved / cp["GBs"], 4)
     tr, src = load_pmc_traffic(kernel, per_launch_samples)
     if tr is not None:
         out["roofline"]["traffic"] = int(tr)

@@ -79,6 +79,8 @@ def test_bench_one_gpu(torch_cuda):
     assert d["n_gpus"] == 1 and d["steps"] == 3 and d["scaling"] == "weak"
     assert d["parity"]["ok"], d["parity"]
     assert d["value"] > 0 and d["roofline"]["achieved"] > 0 and 0 < d["roofline"]["frac"] < 1
+    cp = d["roofline"]["copy_measured"]  # the measured copy ceiling beside the spec peak
+    assert cp["kernel"] == "k_copy_v4" and 0 < cp["frac_of_peak"] < 1 and d["roofline"]["frac_of_copy"] > 0
     assert d["config"]["workload"].startswith("C3")
 
 
