@@ -587,6 +587,35 @@ def test_fir_mfma12_exact_queue_streams(torch_cuda):
     plan.close()
 
 
+@pytest.mark.parametrize("kind", ["nan", "spike"])
+def test_fir_mfma12_exact_chunk_zero_from_history(torch_cuda, kind):
+    """A history sample that sends chunk 0 to an exact form (inf/NaN: the direct form; a 2^40
+    spike: the exact-fp32 tile): k_fir_exact12 re-reads chunk 0's halo from hist_in (the first kernel
+    has already written hist_out by then, so the two must differ -- they may not alias). The
+    non-finite pattern equals the direct form's and the oracle's; finite outputs meet the tolerance
+    per chunk; hist_out is the last 126 inputs either way."""
+    torch = torch_cuda
+    h = _firwin127()
+    n = 3 * 2048 + 17
+    x = orc.synth(n, 71)
+    hist = orc.synth(126, 72)
+    if kind == "nan":
+        hist[100] = complex(np.nan, 0.0)
+    else:
+        hist[100] *= np.float32(2.0 ** 40)
+    y, hy = run_fir(torch, _v8_plan(h, "v12"), x, n, hist=hist)
+    yd, hd = run_fir(torch, nsh.FirPlan(h, 1, nsh.FIR_DIRECT), x, n, hist=hist)
+    np.testing.assert_array_equal(hy.view(np.uint32), x[-126:].view(np.uint32))
+    ref = orc.fir_ccf(x, h, hist=hist)
+    bad = ~(np.isfinite(ref.real) & np.isfinite(ref.imag))
+    np.testing.assert_array_equal(~(np.isfinite(y.real) & np.isfinite(y.imag)), bad)
+    np.testing.assert_array_equal(~(np.isfinite(yd.real) & np.isfinite(yd.imag)), bad)
+    for a in range(0, n, 2048):
+        m = ~bad[a:a + 2048]
+        ok, err, scale = orc.tol_ok(y[a:a + 2048][m], ref[a:a + 2048][m])
+        assert ok, (a, err, scale)
+
+
 @pytest.mark.parametrize("decim", [1, 2, 4])
 @pytest.mark.parametrize("ntaps", [127, 61])
 def test_fir_mfma_exact_tile_mixed_stream(torch_cuda, ntaps, decim):
