@@ -164,15 +164,16 @@ __device__ __forceinline__ void store_pair12(const float4& v, unsigned char* buf
 // so that a stream whose every chunk is exact does not serialise 2^17 atomics on one address
 // (one counter: k_fir_mfma12 took 1.53 ms instead of ~0.4 on such a stream, profiles/r04m_*):
 // workgroup b appends to sub-queue b mod XQ_N -- counter at word XQ_LINE (b mod XQ_N), entries
-// from word XQ_E + (b mod XQ_N) subcap, entry = (chunk << 1) | non-finite -- and word XQ_DONE counts
-// k_fir_exact12's finished workgroups. k_fir_exact12 returns at once when every counter is 0;
-// otherwise its last workgroup to finish zeroes them for the next launch on this stream.
+// from word XQ_E + (b mod XQ_N) subcap, entry = (chunk << 1) | non-finite. A queue holds two such
+// sets; launch k on a stream uses set k & 1, and its k_fir_exact12 zeroes the other set's
+// counters (set k - 1's, consumed by the previous k_fir_exact12 on this stream; the next
+// k_fir_mfma12 appends to it) -- no count of finished workgroups: 1280 agent-scope atomics on one
+// word serialised into ~40 us whenever a launch queued anything (profiles/r04t_*).
 template <int Q>
 using geom12f = nsh_f32t::geom<2 * Q - 2, 2 * Q - 1>;
 constexpr int XQ_N = 64;                   // sub-queues (one counter each)
 constexpr int XQ_LINE = 64;                // words between counters (256 B)
-constexpr int XQ_DONE = XQ_N * XQ_LINE;    // finished k_fir_exact12 workgroups
-constexpr int XQ_E = XQ_DONE + XQ_LINE;    // first entry word
+constexpr int XQ_E = XQ_N * XQ_LINE;       // first entry word
 __host__ __device__ constexpr int64_t xq_subcap(int64_t grid) { return (grid + XQ_N - 1) / XQ_N; }
 #ifndef NSH_X12_PER_CU
 #define NSH_X12_PER_CU 5 // k_fir_exact12 workgroups per CU (a persistent walk over the queue) = its waves per SIMD
@@ -425,7 +426,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NSH_X12_PER
                                                     float2* __restrict__ out,
                                                     const float4* __restrict__ timg32, // exact-fp32 tile taps [4][TWF]
                                                     const float* __restrict__ taps,
-                                                    unsigned* __restrict__ xq,
+                                                    const unsigned* __restrict__ xq, // this launch's set
+                                                    unsigned* __restrict__ xq_next,  // the next launch's set
                                                     int64_t subcap,
                                                     int L,
                                                     int64_t n_out)
@@ -434,6 +436,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NSH_X12_PER
     static_assert(XQ_N == 64, "one sub-queue counter per lane");
     const int tid = threadIdx.x;
     const int lane = tid & 63;
+    if (blockIdx.x == 0 && tid < 64) // the next launch's counters (vector stores, one lane each)
+        __hip_atomic_store(xq_next + XQ_LINE * tid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // every wave: the XQ_N counters (one per lane) and their inclusive prefix sum
     unsigned incl = __hip_atomic_load(xq + XQ_LINE * lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
@@ -442,7 +446,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NSH_X12_PER
         if (lane >= d) incl += t;
     }
     const unsigned cnt = __builtin_amdgcn_readlane(incl, 63);
-    if (cnt == 0) return; // nothing queued (the common case): nothing to empty either
+    if (cnt == 0) return; // nothing queued (the common case)
     auto entry = [&](unsigned i) {
         const int k = __popcll(__ballot(incl <= i)); // sub-queue holding queued chunk i (prefix sums ascend)
         const unsigned start = k ? __shfl(incl, k - 1) : 0u;
@@ -453,17 +457,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NSH_X12_PER
         float4 v[4], hv;
         load12<Q>(in, hist_in, L, n_out, e >> 1, v, hv);
         exact_chunk12<Q>(lds, out, timg32, taps, L, n_out, e >> 1, v, hv, NSH_V12_F32T && !(e & 1u));
-    }
-    // the last workgroup to get here empties the queue for the next launch on this stream (every
-    // workgroup read the count above before counting itself done)
-    __shared__ unsigned last;
-    __syncthreads();
-    if (tid == 0)
-        last = __hip_atomic_fetch_add(xq + XQ_DONE, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
-    __syncthreads();
-    if (last && tid < 64) { // wave 0: every counter, one lane each (vector stores), and the done count
-        __hip_atomic_store(xq + XQ_LINE * tid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (tid == 0) __hip_atomic_store(xq + XQ_DONE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -828,37 +821,43 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma11(const float2* __restrict_
     if (ch <= c_last) step(vb, vc, va, ch);
 }
 
-// The plan's exact queue for stream s, at least `words` u32 long. Grown (rare: the first call
-// with more chunks than any before on this stream) after the stream has drained, so no launch
-// still uses the old one; a new queue starts empty in stream order.
-unsigned* exact_queue(const nsh_fir_plan* p, hipStream_t s, int64_t words, hipError_t& e)
+// The plan's exact queue for stream s: two sets of at least `words` u32 each (stride returned), and
+// the set this launch uses (the stream's launch count & 1). Grown (rare: the first call with more
+// chunks than any before on this stream) after the stream has drained, so no launch still uses the
+// old one; a new queue starts with both sets' counters zero, in stream order.
+unsigned* exact_queue(const nsh_fir_plan* p, hipStream_t s, int64_t words, int64_t& stride, int& set, hipError_t& e)
 {
     e = hipSuccess;
     std::lock_guard<std::mutex> g(p->xq_mu);
     nsh_fir_plan::xqueue* q = nullptr;
     for (auto& x : p->xq)
         if (x.s == s) q = &x;
-    if (q && q->cap >= words) return q->d;
-    int64_t cap = XQ_E + 1024;
-    while (cap < words) cap *= 2;
-    if (q) {
-        if ((e = hipStreamSynchronize(s)) != hipSuccess) return nullptr;
-        (void)hipFree(q->d);
-        q->d = nullptr;
-        q->cap = 0;
-    } else {
-        p->xq.push_back({ s, nullptr, 0 });
-        q = &p->xq.back();
+    if (!q || q->stride < words) {
+        int64_t st = XQ_E + 1024;
+        while (st < words) st *= 2;
+        if (q) {
+            if ((e = hipStreamSynchronize(s)) != hipSuccess) return nullptr;
+            (void)hipFree(q->d);
+            q->d = nullptr;
+            q->stride = 0;
+        } else {
+            p->xq.push_back({ s, nullptr, 0, 0 });
+            q = &p->xq.back();
+        }
+        unsigned* d = nullptr;
+        if ((e = hipMalloc(&d, (size_t)(2 * st) * sizeof(unsigned))) != hipSuccess) return nullptr;
+        if ((e = hipMemsetAsync(d, 0, XQ_E * sizeof(unsigned), s)) == hipSuccess)
+            e = hipMemsetAsync(d + st, 0, XQ_E * sizeof(unsigned), s);
+        if (e != hipSuccess) {
+            (void)hipFree(d);
+            return nullptr;
+        }
+        q->d = d;
+        q->stride = st;
     }
-    unsigned* d = nullptr;
-    if ((e = hipMalloc(&d, (size_t)cap * sizeof(unsigned))) != hipSuccess) return nullptr;
-    if ((e = hipMemsetAsync(d, 0, XQ_E * sizeof(unsigned), s)) != hipSuccess) {
-        (void)hipFree(d);
-        return nullptr;
-    }
-    q->d = d;
-    q->cap = cap;
-    return d;
+    stride = q->stride;
+    set = (int)(q->launches++ & 1);
+    return q->d;
 }
 
 template <int D, int QH>
@@ -906,14 +905,19 @@ int launch_v12(const nsh_fir_plan* p, const float2* in, const float2* hin, float
     if (grid > 0x7fffffff) return nsh::fail_msg("nsh_fir_ccf(mfma v12): stream too long for one launch");
     hipError_t e;
     const int64_t subcap = xq_subcap(grid);
-    unsigned* xq = exact_queue(p, s, XQ_E + XQ_N * subcap, e);
+    int64_t stride = 0;
+    int set = 0;
+    unsigned* xq = exact_queue(p, s, XQ_E + XQ_N * subcap, stride, set, e);
     if (!xq) return nsh::fail(e, "nsh_fir_ccf(mfma v12): exact queue");
+    unsigned* cur = xq + set * stride;
+    unsigned* nxt = xq + (set ^ 1) * stride;
     nsh::launch((k_fir_mfma12<Q>), dim3((unsigned)grid), dim3(G::NT), G::LDS, s, in, hin, hout, out,
-                (const uint4*)p->frag12_dev, xq, p->L, p->sh8, n_out, per_x);
+                (const uint4*)p->frag12_dev, cur, p->L, p->sh8, n_out, per_x);
     NSH_CK_LAUNCH("nsh_fir_ccf(mfma fp16x2 v12)");
     const int64_t xcap = (int64_t)plan_cus(p) * NSH_X12_PER_CU;
     hipLaunchKernelGGL((k_fir_exact12<Q>), dim3((unsigned)(nchunks < xcap ? nchunks : xcap)), dim3(G::NT), G::LDS, s, in,
-                       hin, out, (const float4*)p->tf32q_dev, (const float*)p->taps_dev, xq, subcap, p->L, n_out);
+                       hin, out, (const float4*)p->tf32q_dev, (const float*)p->taps_dev, (const unsigned*)cur, nxt, subcap,
+                       p->L, n_out);
     NSH_CK_LAUNCH("nsh_fir_ccf(mfma v12 exact chunks)");
     return 0;
 }

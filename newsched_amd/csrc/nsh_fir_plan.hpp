@@ -35,8 +35,9 @@ struct nsh_fir_plan {
     // stream are ordered, so each stream's queue is empty again when its next launch starts
     struct xqueue {
         hipStream_t s;
-        unsigned* d;
-        int64_t cap;
+        unsigned* d;      // two sets of `stride` words: launch k on this stream uses set k & 1
+        int64_t stride;
+        uint64_t launches;
     };
     mutable std::mutex xq_mu;
     mutable std::vector<xqueue> xq;
