@@ -320,6 +320,9 @@ struct pshape {
     static constexpr int RSTEP = 128 / PW; // ring rows between a thread's consecutive slots
 };
 
+#ifndef NSH_PFFT_RINGORDER
+#define NSH_PFFT_RINGORDER 1 // the window transformed in ring order (rotated), the rotation undone at the output
+#endif
 #ifndef NSH_PFFT_SPLIT_READS
 #define NSH_PFFT_SPLIT_READS 1
 #endif
@@ -466,9 +469,23 @@ __global__ __launch_bounds__(64 * P / PW, 1) void k_fir_pfft(pfft_args a)
         const float usc = __uint_as_float((unsigned)(127 - ks) << 23);
         const int64_t rowf = f * V;
         if (!bad) {
+            cf v[PW][8];
+#if NSH_PFFT_RINGORDER
+            // The window in ring order: slot t = (rowf + q) mod M holds window row q, i.e. the
+            // sequence read is the window rotated by s = rowf mod M. Its transform is the window's
+            // times W^{s k} for every phase alike, so the inverse yields c rotated by s, which the
+            // output stores undo (q = (t - s) mod M). Slots j + 64 r share one swizzle, so the eight
+            // reads are one per-lane base plus immediate offsets -- no per-frame address arithmetic
+            // (the rotation-free form spent ~30 VALU per wave and frame on it).
+#pragma unroll
+            for (int i = 0; i < PW; ++i) {
+                const cf* rb = ring + ring_at<P>(j, w * PW + i);
+#pragma unroll
+                for (int r = 0; r < 8; ++r) v[i][r] = (NSH_PFFT_ABLATE & 16) ? cf{ sc, (float)r } : rb[64 * P * r];
+            }
+#else
             // rows rowf + j + 64 r share one swizzle (64 r moves s / (32 / P) by a multiple of P)
             const int sr = (int)((rowf + j) & (M - 1));
-            cf v[PW][8];
 #pragma unroll
             for (int i = 0; i < PW; ++i) {
                 const int e0 = ring_at<P>(sr, w * PW + i);
@@ -476,6 +493,7 @@ __global__ __launch_bounds__(64 * P / PW, 1) void k_fir_pfft(pfft_args a)
                 for (int r = 0; r < 8; ++r)
                     v[i][r] = (NSH_PFFT_ABLATE & 16) ? cf{ sc, (float)r } : ring[(e0 + 64 * P * r) & (M * P - 1)];
             }
+#endif
             if (scale) { // wave-uniform branch
 #pragma unroll
                 for (int i = 0; i < PW; ++i)
@@ -577,11 +595,22 @@ __global__ __launch_bounds__(64 * P / PW, 1) void k_fir_pfft(pfft_args a)
             fft512_multi<1>(v, ib, t2, t3);
             const __amdgpu_buffer_rsrc_t ro = span_rsrc(a.out + rowf, a.n_out - rowf, V);
             const cf us = cf{ usc, -usc }; // 2^-k and the output conjugation
+#if NSH_PFFT_RINGORDER
+            // slot t = j + 64 r holds output row q = (t - s) mod M (the window was read in ring order)
+            int t0 = j - (int)(rowf & (M - 1));
+            asm volatile("" : "+v"(t0)); // computed here, not hoisted
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                const int q = (t0 + 64 * r) & (M - 1);
+                if (q >= Q) nsh::buf_store_f2(ro, (q - Q) * 8, v[0][r] * us);
+            }
+#else
             int ob = (j - Q) * 8;
             asm volatile("" : "+v"(ob)); // computed here, not hoisted (8 offsets would spill)
 #pragma unroll
             for (int r = 0; r < 8; ++r)
                 if (j + 64 * r >= Q) nsh::buf_store_f2(ro, ob + 512 * r, v[0][r] * us);
+#endif
             PFFT_T(5);
         }
     }
