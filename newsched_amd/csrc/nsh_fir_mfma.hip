@@ -452,8 +452,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NSH_X12_PER
         const unsigned start = k ? __shfl(incl, k - 1) : 0u;
         return __hip_atomic_load(xq + XQ_E + k * subcap + (i - start), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
+    const int64_t nchunks = (n_out + geom12<Q>::CHUNK - 1) / geom12<Q>::CHUNK;
     for (unsigned i = blockIdx.x; i < cnt; i += gridDim.x) {
         const unsigned e = entry(i);
+        if ((int64_t)(e >> 1) >= nchunks) continue; // never for a queue this launch filled (defensive)
         float4 v[4], hv;
         load12<Q>(in, hist_in, L, n_out, e >> 1, v, hv);
         exact_chunk12<Q>(lds, out, timg32, taps, L, n_out, e >> 1, v, hv, NSH_V12_F32T && !(e & 1u));
