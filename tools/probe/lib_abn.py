@@ -72,10 +72,15 @@ for r in run:
 s.synchronize()
 t = [[] for _ in libs]
 st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-for _ in range(3):  # clocks settle
+# clocks and power settle: every build in turn for at least WARM_S seconds (default 2; with 3 rounds
+# only, the first two builds of a round ran ~1.5 % slower than the last two, profiles/r04r_*)
+import time
+
+t_w = time.perf_counter()
+while time.perf_counter() - t_w < float(os.environ.get("WARM_S", "2")):
     for r in run:
         r()
-s.synchronize()
+    s.synchronize()
 for _ in range(rounds):
     for i, r in enumerate(run):
         st.record(s)
