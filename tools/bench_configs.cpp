@@ -2,8 +2,11 @@
 // measured through the same runtime as the headline: flowgraphs in one scheduler_hip domain
 // with an HBM-resident input ring (nop_source -> nop_head(n) -> [2n-item hip_buffer,
 // preloaded with the counter-based stream] -> blocks -> null_sink), wall time of whole
-// fg->run() calls (median of K after one warm-up), tail parity against an in-tool CPU
-// reference, and the CPU scheduler_mt path of the same config where the CPU blocks exist.
+// fg->run() calls (median of K after one warm-up) and, as bench.py times the headline since round 4,
+// one run streaming K batches through the same flowgraph (nop_head passes K n items over the
+// resident ring: every batch is read from HBM; the run's start and drain paid once), tail parity
+// against an in-tool CPU reference, and the CPU scheduler_mt path of the same config where the
+// CPU blocks exist.
 //   build/tools/bench_configs [log2n=28] [steps=5]     -> one JSON line per config
 #include <algorithm>
 #include <chrono>
@@ -107,6 +110,7 @@ static double median(std::vector<double> v)
 struct gpu_fg {
     flowgraph::sptr fg;
     schedulers::scheduler_hip::sptr sched;
+    std::shared_ptr<blocks::nop_head> head;
     block_sptr snk;
     int64_t n_items;
     size_t isz;
@@ -117,7 +121,7 @@ struct gpu_fg {
         : n_items(n_items_), isz(isz_)
     {
         auto src = blocks::nop_source::make(isz);
-        auto head = blocks::nop_head::make(isz, (size_t)n_items);
+        head = blocks::nop_head::make(isz, (size_t)n_items);
         snk = blocks::null_sink::make(isz);
         fg = flowgraph::make();
         fg->connect(src, 0, head, 0)->set_custom_buffer(VMCIRC_BUFFER_ARGS);
@@ -161,6 +165,16 @@ struct gpu_fg {
         }
         return median(t);
     }
+    // one run streaming `batches` batches (after run()'s warm-up): seconds per batch
+    double run_streamed(int batches)
+    {
+        head->set_length((size_t)(batches * n_items));
+        const auto t0 = clk::now();
+        fg->run();
+        const double s = std::chrono::duration<double>(clk::now() - t0).count() / batches;
+        head->set_length((size_t)n_items);
+        return s;
+    }
     // last `count` samples written into the sink's input ring
     std::vector<gr_complex> tail(int64_t count)
     {
@@ -199,7 +213,15 @@ static double cpu_run(std::vector<block_sptr> chain, int64_t n, size_t fixed = 3
 }
 
 static void emit(const std::string& s) { std::printf("%s\n", s.c_str()), std::fflush(stdout); }
-static std::string num(double v, int prec = 1)
+static std::string num(double v, int prec = 1);
+// the streamed figure (K batches in one run) beside the per-run one
+static std::string streamed(double n_per_batch, double s, int batches, double bytes_per_sample, double hbm)
+{
+    const double gbs = bytes_per_sample * n_per_batch / s / 1e9;
+    return ", \"streamed\": {\"batches_per_run\": " + std::to_string(batches) + ", \"value\": " + num(n_per_batch / s / 1e6, 1) +
+           ", \"ms_per_batch\": " + num(s * 1e3, 3) + ", \"achieved_GBs\": " + num(gbs, 1) + ", \"hbm_frac\": " + num(gbs / hbm, 4) + "}";
+}
+static std::string num(double v, int prec)
 {
     char b[64];
     std::snprintf(b, sizeof b, "%.*f", prec, v);
@@ -251,6 +273,7 @@ int main(int argc, char** argv)
         gpu_fg g(chain, n, sizeof(gr_complex), (size_t)n * sizeof(gr_complex), variant != 2);
         const bool one_pass = variant != 2;
         const double s = g.run(steps);
+        const double ss = g.run_streamed(steps);
         auto y = g.tail(4096);
         auto x = synth(4096, n - 4096);
         for (auto& v : x)
@@ -263,7 +286,8 @@ int main(int argc, char** argv)
         std::string line = "{\"config\": \"C2\", \"variant\": \"" + std::string(name[variant]) +
                            "\", \"value\": " + num(n / s / 1e6) + ", \"unit\": \"MSamples/s\", \"ms_per_run\": " + num(s * 1e3, 3) +
                            ", \"hbm_bytes_per_sample\": " + (one_pass ? "16" : "64") + ", \"achieved_GBs\": " + num(gbs) +
-                           ", \"hbm_frac\": " + num(gbs / hbm, 4) + ", \"parity_tail_bitexact\": " + (exact ? "true" : "false");
+                           ", \"hbm_frac\": " + num(gbs / hbm, 4) + streamed((double)n, ss, steps, one_pass ? 16.0 : 64.0, hbm) +
+                           ", \"parity_tail_bitexact\": " + (exact ? "true" : "false");
         if (variant == 1) {
             const int64_t nc = 1 << 25;
             std::vector<block_sptr> cc;
@@ -305,13 +329,14 @@ int main(int argc, char** argv)
                 chain = { hip::fft_vcc::make(1024, true), hip::multiply_const_vcc::make(w), hip::fft_vcc::make(1024, false) };
             gpu_fg g(chain, frames, 1024 * sizeof(gr_complex), (size_t)n * sizeof(gr_complex), variant != 2);
             const double s = g.run(steps);
+            const double ss = g.run_streamed(steps);
             auto y = g.tail(1024);
             const int bytes = variant == 2 ? 48 : 16;
             const double gbs = (double)bytes * n / s / 1e9;
             emit(std::string("{\"config\": \"C4\", \"variant\": \"") + names[variant] + "\", \"value\": " + num(n / s / 1e6) +
                  ", \"unit\": \"MSamples/s\", \"ms_per_run\": " + num(s * 1e3, 3) + ", \"hbm_bytes_per_sample\": " +
                  std::to_string(bytes) + ", \"achieved_GBs\": " + num(gbs) + ", \"hbm_frac\": " + num(gbs / hbm, 4) +
-                 ", \"parity_last_frame_rel_err\": " + num(rel_err(y, r), 9) + "}");
+                 streamed((double)n, ss, steps, bytes, hbm) + ", \"parity_last_frame_rel_err\": " + num(rel_err(y, r), 9) + "}");
         }
     }
 
@@ -332,13 +357,14 @@ int main(int argc, char** argv)
             for (int i = 0; i < 4; ++i) chain.push_back(hip::fir_filter_ccf::make(h, 2));
             gpu_fg g(chain, n, sizeof(gr_complex), (size_t)n * sizeof(gr_complex), true, fused == 1);
             const double s = g.run(steps);
-            auto y = g.tail(m);
-            const double gbs = 8.5 * n / s / 1e9;
             std::string launches;
             for (auto& b : g.sched->fusion_plan().fused)
                 if (auto c = std::dynamic_pointer_cast<hip::fir_filter_cascade_ccf>(b))
                     launches = ", \"cascade_launches_per_run\": " + num((double)c->launches() / (steps + 20), 2) +
                                ", \"cascade_kernel\": \"" + c->kernel() + "\"";
+            const double ss = g.run_streamed(steps);
+            auto y = g.tail(m);
+            const double gbs = 8.5 * n / s / 1e9;
             const char* var = fused ? "G=1: 4 x fir_filter_ccf(127 taps, decim 2), fused by scheduler_hip into one "
                                       "fir_filter_cascade_ccf (k_fir_pfft<16>, default)"
                                     : "G=1: 4 x fir_filter_ccf(127 taps, decim 2), FIR fusion off (4 launches, every "
@@ -346,7 +372,8 @@ int main(int argc, char** argv)
             emit(std::string("{\"config\": \"C5\", \"variant\": \"") + var + "\", \"value\": " + num(n / s / 1e6) +
                  ", \"unit\": \"MSamples/s (input)\", \"ms_per_run\": " + num(s * 1e3, 3) +
                  ", \"hbm_bytes_per_input_sample\": 8.5, \"achieved_GBs\": " + num(gbs) + ", \"hbm_frac\": " +
-                 num(gbs / hbm, 4) + ", \"parity_tail_rel_err\": " + num(rel_err(y, r), 9) + launches +
+                 num(gbs / hbm, 4) + streamed((double)n, ss, steps, 8.5, hbm) + ", \"parity_tail_rel_err\": " +
+                 num(rel_err(y, r), 9) + launches +
                  (fused ? ", \"cpu_baseline\": {\"value\": " + num(nc / cs / 1e6, 2) +
                               ", \"unit\": \"MSamples/s (input)\", \"sample\": \"2^24 samples, vector_source->head->4x "
                               "blocks::fir_filter_ccf(decim 2)->null_sink, scheduler_mt thread per block\"}}"
