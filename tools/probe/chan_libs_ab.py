@@ -38,7 +38,7 @@ s.synchronize()
 import time
 
 t0 = time.time()
-while time.time() - t0 < 1.0:  # clocks settle
+while time.time() - t0 < float(os.environ.get("WARM_S", "2")):  # clocks settle (2 s: see lib_abn.py)
     for r in run:
         r()
     s.synchronize()
