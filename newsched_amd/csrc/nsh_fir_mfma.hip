@@ -1,6 +1,7 @@
 // libnsh_hip.so: fir_filter_ccf on the matrix cores -- the product kernels.
 //
 //   k_fir_mfma12<Q>      decim 1 (the C3 bench kernel)
+//   k_fir_exact12<Q>     decim 1: the chunks k_fir_mfma12 queued for an exact form (same call, same stream)
 //   k_fir_mfma11<D, QH>  decim 2 and 4 (polyphase; the staged C5 chain's stages)
 //
 // Blocked Toeplitz form. Split the output stream into 32-sample blocks; output n = 32*beta + i:
@@ -13,8 +14,9 @@
 // Precision: fp32 from fp16x2 -- both operands split into two fp16 terms at a power-of-two
 // scale (taps once on the host, samples per 2048-sample chunk), three products
 // x0h0 + x0h1 + x1h0 accumulated in fp32 (see the fp16x2 notes in nsh_fir_mfma_shared.hpp and
-// below); chunks holding non-finite or fp16-subnormal-range samples take the fp32 direct form
-// inside the same launch (exact IEEE semantics).
+// below); chunks whose range the split cannot hold take the exact-fp32 matrix tile, chunks holding
+// inf/NaN the fp32 direct form (exact IEEE semantics) -- at decim 1 in k_fir_exact12, at decim 2
+// and 4 inside the same launch.
 //
 // The forms this file superseded -- k_fir_mfma2 (bf16x3, six products), k_fir_mfma5 (16-sample
 // blocks), k_fir_mfma7 (bf16x3 decimator), k_fir_mfma9 (v12's predecessor) and k_fir_casc2 (two
