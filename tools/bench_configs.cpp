@@ -214,6 +214,40 @@ static double cpu_run(std::vector<block_sptr> chain, int64_t n, size_t fixed = 3
 
 static void emit(const std::string& s) { std::printf("%s\n", s.c_str()), std::fflush(stdout); }
 static std::string num(double v, int prec = 1);
+// the measured device copy (nsh_copy = k_copy_v4, 16 B per sample), GB/s: the second peak
+// BASELINE.md asks every config to be quoted against -- measured last, on a warm chip, best of 3
+static double measure_copy(int64_t n)
+{
+    void *x = nullptr, *y = nullptr, *s = nullptr, *e0 = nullptr, *e1 = nullptr;
+    hip::check(nsh_malloc(0, (size_t)n * 8, &x), "copy");
+    hip::check(nsh_malloc(0, (size_t)n * 8, &y), "copy");
+    hip::check(nsh_stream_create(0, &s), "copy");
+    hip::check(nsh_event_create(&e0), "copy");
+    hip::check(nsh_event_create(&e1), "copy");
+    hip::check(nsh_synth_cf32((float*)x, n, 0, 0x6E736368, s), "copy");
+    const auto t0 = clk::now();
+    while (std::chrono::duration<double>(clk::now() - t0).count() < 1.5) { // clocks settle (first GPU work of the run)
+        hip::check(nsh_copy(x, y, (size_t)n * 8, s), "copy");
+        hip::check(nsh_stream_sync(s), "copy");
+    }
+    const int reps = 10;
+    float ms = 0;
+    for (int k = 0; k < 3; ++k) {
+        hip::check(nsh_event_record(e0, s), "copy");
+        for (int i = 0; i < reps; ++i) hip::check(nsh_copy(x, y, (size_t)n * 8, s), "copy");
+        hip::check(nsh_event_record(e1, s), "copy");
+        hip::check(nsh_event_sync(e1), "copy");
+        float m = 0;
+        hip::check(nsh_event_elapsed_ms(e0, e1, &m), "copy");
+        ms = k == 0 ? m : std::min(ms, m);
+    }
+    nsh_event_destroy(e0);
+    nsh_event_destroy(e1);
+    nsh_stream_destroy(s);
+    nsh_free(x);
+    nsh_free(y);
+    return 16.0 * n / (ms / reps * 1e-3) / 1e9;
+}
 // the streamed figure (K batches in one run) beside the per-run one
 static std::string streamed(double n_per_batch, double s, int batches, double bytes_per_sample, double hbm)
 {
@@ -379,6 +413,13 @@ int main(int argc, char** argv)
                               "blocks::fir_filter_ccf(decim 2)->null_sink, scheduler_mt thread per block\"}}"
                         : std::string("}")));
         }
+    }
+    // ---- the measured copy ceiling (after the GPU configs: the chip is warm) -------------------
+    {
+        const double gbs = measure_copy(n);
+        emit("{\"config\": \"copy\", \"variant\": \"nsh_copy (k_copy_v4) of 2^" + std::to_string(log2n) +
+             " complex samples on fresh buffers, 16 B per sample, best of 3 x 10 launches (HIP events)\", \"achieved_GBs\": " +
+             num(gbs) + ", \"hbm_frac\": " + num(gbs / hbm, 4) + "}");
     }
     // ---- C3 with host endpoints: the PCIe-inclusive rate (not the metric: bench.py's input is
     // resident). vector_source(repeat) -> head -[H2D]-> hip::fir_filter_ccf -[D2H]-> null_sink,
