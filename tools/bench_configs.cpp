@@ -140,6 +140,9 @@ struct gpu_fg {
         sched->set_fir_fusion(fir_fusion);
         fg->set_scheduler(sched);
         fg->set_wait_spin_us(5000); // a run is ~1 ms: poll for its end instead of sleeping (as bench.py's flowgraph)
+        // and the partition stream's drain, likewise (as bench.py's flowgraph): without it each
+        // streamed batch waited ~22 us in a blocking stream sync between launches (r04zp trace)
+        sched->set_flush_spin_us(5000);
         fg->validate();
         // the head's output edge (its consumer may be a fused block replacing chain[0])
         auto ring = std::dynamic_pointer_cast<hip_buffer>(sched->buffers()->get_output_buffers(head->output_stream_ports()[0])[0]);
@@ -154,9 +157,12 @@ struct gpu_fg {
     }
     double run(int steps)
     {
-        // warm-up to the sustained clock: the chip's power management settles after ~20
-        // back-to-back runs (tools/probe/run_series.py), as in bench.py's default warmup
-        for (int i = 0; i < 20; ++i) fg->run();
+        // warm-up to the sustained clock: at least 20 back-to-back runs (tools/probe/run_series.py)
+        // and at least 1 s of them, as bench.py's warm-up -- 20 runs of a ~0.7 ms config last
+        // ~15 ms, and the first GPU config then measured 4-6 % below its own streamed rate on a
+        // cold chip (C2's hand-fused block in r04zc / r04zm)
+        const auto tw = clk::now();
+        for (int i = 0; i < 20 || std::chrono::duration<double>(clk::now() - tw).count() < 1.0; ++i) fg->run();
         std::vector<double> t;
         for (int i = 0; i < steps; ++i) {
             const auto t0 = clk::now();
