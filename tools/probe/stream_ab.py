@@ -34,9 +34,14 @@ ops = {
 st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 for name, (bps, fn) in ops.items():
     ys = [torch.zeros(n, dtype=torch.complex64, device="cuda") for _ in libs]
-    for _ in range(10):
+    # clocks settle: every build in turn for WARM_S seconds (default 2, as lib_abn.py); with 10
+    # passes only, the builds' in-round position moved the copy by up to 10 % (profiles/r04zs_*)
+    import time
+    t_w = time.perf_counter()
+    while time.perf_counter() - t_w < float(os.environ.get("WARM_S", "2")):
         for L, y in zip(libs, ys):
             assert fn(L, y) == 0
+        s.synchronize()
     t = [[] for _ in libs]
     for _ in range(rounds):
         for i, (L, y) in enumerate(zip(libs, ys)):
