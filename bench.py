@@ -71,7 +71,24 @@ def cpu_model():
 
 
 def free_port():
-    with socket.socket() as s:
+    """A free TCP port below the kernel's ephemeral range (ip_local_port_range): a port inside it
+    can be handed to a client's connect() as its source port while the server is not listening
+    yet, and such a client then connects to itself (GPUTEST_r04)."""
+    import random
+    try:
+        with open("/proc/sys/net/ipv4/ip_local_port_range") as f:
+            lo = int(f.read().split()[0])
+    except (OSError, ValueError, IndexError):
+        lo = 32768
+    for _ in range(500):
+        p = random.randrange(10000, max(lo, 10001))
+        with socket.socket() as s:
+            try:
+                s.bind(("127.0.0.1", p))
+            except OSError:
+                continue
+            return p
+    with socket.socket() as s:  # nothing free below the range: let the kernel choose
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
 
@@ -133,11 +150,19 @@ def run_c5(a, dist, backend, rank, world, device, torch, orc, nsr):
     taps = firwin(127, 0.45)
     first = max(0, shard * n - C5_HALO)  # shards > 0 start with the chain's halo (discarded)
     n_in = shard * n + n - first
-    port = torch.tensor([free_port() if rank == 0 else 0], dtype=torch.int64,
-                        device="cuda" if backend == "nccl" else "cpu")
+    # Rendezvous: rank 0 makes a fresh directory (one node) and a job nonce; the receiving end of
+    # each crossing listens on a port the kernel picks and publishes it in <dir>/shard<s>/, the
+    # sending end waits for that entry (no derived port numbers: GPUTEST_r04).
+    rdv = [None, None]
+    if rank == 0 and world > 1:
+        import random
+        import tempfile
+        rdv = [tempfile.mkdtemp(prefix="nsh_c5_"), random.getrandbits(63)]
+        for s_ in range(shards):
+            os.makedirs(os.path.join(rdv[0], "shard%d" % s_))
     if dist is not None:
-        dist.broadcast(port, 0)
-    base_port = int(port.item()) + 1 + 8 * shard
+        dist.broadcast_object_list(rdv, src=0)
+    rdv_dir = os.path.join(rdv[0], "shard%d" % shard) if rdv[0] else ""
     own_gpus = torch.cuda.device_count() >= world
     transport = a.c5_transport if a.c5_transport != "default" else ("rccl" if own_gpus and world > 1 else "auto")
     res = {"layout": "G=%d stage groups x %d time shards" % (G, shards), "stages": "4 x fir_filter_ccf(firwin(127,0.45), D=2)",
@@ -151,7 +176,7 @@ def run_c5(a, dist, backend, rank, world, device, torch, orc, nsr):
     def leg():
         try:
             pipe = box["pipe"] = nsr.C5Pipeline(taps, n_in, group=group, n_groups=G, device=device, first_index=first,
-                                                base_port=base_port, transport=transport,
+                                                rendezvous_dir=rdv_dir, nonce=rdv[1] or 0, transport=transport,
                                                 buf_bytes=a.c5_buf_mib << 20)
             for _ in range(a.c5_warmup):
                 pipe.run()
@@ -206,6 +231,12 @@ def run_c5(a, dist, backend, rank, world, device, torch, orc, nsr):
         res["transports"] = {"0": tr}
     if pipe is not None:
         pipe.close()
+    if rdv[0] and status != 2.0:  # (status is the max over ranks: the same decision everywhere)
+        if dist is not None:
+            dist.barrier()  # every rank's pipeline is closed
+        if rank == 0:
+            import shutil
+            shutil.rmtree(rdv[0], ignore_errors=True)
     res["ok"] = status == 0.0
     res["_abandoned_any"] = status == 2.0  # some rank's leg is still running: exit hard after the line
     if status == 0.0:

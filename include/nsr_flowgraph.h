@@ -57,14 +57,19 @@ int nsr_fir_bench_destroy(void* handle);
  * (n_groups in {1, 2, 4}; group g runs stages [4g/G, 4(g+1)/G) in a scheduler_hip domain on
  * `dev`, plus the source (g = 0) / the sink (g = G-1); the other groups' domains are
  * remote_domain placeholders). Every process of one pipeline calls this with the same
- * arguments except `group` and `dev`. Crossing i listens on 127.0.0.1:base_port+i.
+ * arguments except `group` and `dev`. Rendezvous: every process of the pipeline passes the
+ * same `rendezvous_dir` (a directory on this node, empty before the job; needed for
+ * n_groups > 1) and the same `nonce` (job id): the receiving end of crossing i listens on a
+ * kernel-chosen port on 127.0.0.1 and publishes it there as crossing<i>, the sending end waits
+ * for that entry; handshakes with the wrong role or nonce, and sockets connected to
+ * themselves, are refused (domain_adapter_remote.hpp).
  * transport: "auto" (RCCL when both rings are device memory on GPUs with different PCI bus
  * ids, else the TCP socket, staged through pinned memory) | "rccl" (fail otherwise) |
  * "socket". buf_bytes: scheduler_hip fixed_buf_size. n must be a multiple of decim^4.
  * Reference: graph_utils.cpp:11-205 (partition), domain_adapter_direct.hpp:236-257. */
 int nsr_c5_create(int group, int n_groups, int dev, const float* taps, int ntaps, int decim, int64_t n,
-                  uint64_t first_index, uint64_t seed, int base_port, const char* transport, size_t buf_bytes,
-                  void** handle);
+                  uint64_t first_index, uint64_t seed, const char* rendezvous_dir, uint64_t nonce,
+                  const char* transport, size_t buf_bytes, void** handle);
 int nsr_c5_run(void* handle);
 /* The transports this process's crossings negotiated, e.g. "send1:rccl,recv0:rccl". */
 int nsr_c5_transport(void* handle, char* buf, int len);

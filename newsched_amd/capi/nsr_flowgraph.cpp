@@ -221,8 +221,8 @@ int nsr_fir_bench_destroy(void* handle)
 }
 
 int nsr_c5_create(int group, int n_groups, int dev, const float* taps, int ntaps, int decim, int64_t n,
-                  uint64_t first_index, uint64_t seed, int base_port, const char* transport, size_t buf_bytes,
-                  void** handle)
+                  uint64_t first_index, uint64_t seed, const char* rendezvous_dir, uint64_t nonce,
+                  const char* transport, size_t buf_bytes, void** handle)
 {
     return guarded([&] {
         const int n_stages = 4;
@@ -249,7 +249,10 @@ int nsr_c5_create(int group, int n_groups, int dev, const float* taps, int ntaps
         std::vector<scheduler_sptr> scheds;
         domain_conf_vec dc;
         remote_edge_options o;
-        o.base_port = base_port;
+        if (n_groups > 1 && (!rendezvous_dir || !*rendezvous_dir))
+            throw std::invalid_argument("nsr_c5_create: n_groups > 1 needs a rendezvous directory");
+        o.rendezvous_dir = rendezvous_dir ? rendezvous_dir : "";
+        o.nonce = nonce;
         o.transport = transport && *transport ? transport : "auto";
         o.device = dev;
         o.timeout_s = 120;

@@ -16,6 +16,9 @@ void clear_error();
 
 inline int fail(hipError_t e, const char* what)
 {
+    // reported here, by return code: clear HIP's per-thread last error too, or the next entry
+    // point's launch check (NSH_CK_LAUNCH: hipGetLastError) would blame its own launch for it
+    (void)hipGetLastError();
     set_error(std::string(what) + ": " + hipGetErrorString(e));
     return (int)e ? (int)e : -1;
 }
@@ -51,6 +54,30 @@ inline void launch(K kernel, dim3 grid, dim3 block, uint32_t lds, hipStream_t s,
         hipLaunchKernelGGL(kernel, grid, block, lds, s, args...);
     }
 }
+
+// The pending pair, taken (and cleared) by an entry point that times several launches as one:
+// start recorded by the first kernel's dispatch, stop by the last one's (launch_timed).
+inline launch_events take_launch_events()
+{
+    const launch_events t = next_launch_events();
+    next_launch_events() = launch_events();
+    return t;
+}
+template <typename K, typename... A>
+inline void launch_timed(K kernel, dim3 grid, dim3 block, uint32_t lds, hipStream_t s, hipEvent_t start, hipEvent_t stop,
+                         A... args)
+{
+    if (start || stop)
+        hipExtLaunchKernelGGL(kernel, grid, block, lds, s, start, stop, 0u, args...);
+    else
+        hipLaunchKernelGGL(kernel, grid, block, lds, s, args...);
+}
+// Clears the pending pair when an entry point returns, whatever the path (early returns, errors,
+// kernels that do not consume it): an armed pair must never be recorded around a later, unrelated
+// launch on this thread.
+struct launch_events_guard {
+    ~launch_events_guard() { next_launch_events() = launch_events(); }
+};
 
 // Grid for a grid-stride streaming kernel: enough workgroups to fill 256 CUs several
 // times over, capped so each thread still walks several 16-byte vectors.

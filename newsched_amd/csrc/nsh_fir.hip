@@ -265,6 +265,7 @@ const char* nsh_fir_plan_kernel(void* plan) { return plan ? static_cast<nsh_fir_
 
 int nsh_fir_ccf(void* plan, const float* in, const float* hist_in, float* hist_out, float* out, int64_t n_out, void* stream)
 {
+    nsh::launch_events_guard timing_guard; // the armed event pair never outlives this call
     auto* p = static_cast<nsh_fir_plan*>(plan);
     if (!p) return nsh::fail_msg("nsh_fir_ccf: null plan");
     if (n_out <= 0) return 0;

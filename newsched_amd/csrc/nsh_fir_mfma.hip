@@ -348,8 +348,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
         if (tid == 0) {
             const unsigned k = blockIdx.x % XQ_N;
             const unsigned i = __hip_atomic_fetch_add(xq + XQ_LINE * k, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(xq + XQ_E + k * xq_subcap(gridDim.x) + i, (unsigned)(ch << 1) | (m >= 0x7f800000u ? 1u : 0u),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // i < subcap always, on a queue whose counters were zeroed (xq_reset after a failed
+            // call): the bound keeps a stale counter from writing into the next sub-queue
+            if (i < (unsigned)xq_subcap(gridDim.x))
+                __hip_atomic_store(xq + XQ_E + k * xq_subcap(gridDim.x) + i, (unsigned)(ch << 1) | (m >= 0x7f800000u ? 1u : 0u),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     } else {
         if (tid < G::HP) store_pair12<Q>(hv, lds, 2 * tid, s);
@@ -442,6 +445,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NSH_X12_PER
         __hip_atomic_store(xq_next + XQ_LINE * tid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // every wave: the XQ_N counters (one per lane) and their inclusive prefix sum
     unsigned incl = __hip_atomic_load(xq + XQ_LINE * lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    incl = min(incl, (unsigned)subcap); // entries past a sub-queue's capacity were never written
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
         const unsigned t = __shfl_up(incl, d);
@@ -864,6 +868,21 @@ unsigned* exact_queue(const nsh_fir_plan* p, hipStream_t s, int64_t words, int64
     return q->d;
 }
 
+// After a failed launch in the k_fir_mfma12 / k_fir_exact12 pair the queue's parity no longer
+// matches what ran (the set k_fir_exact12 should have zeroed still holds counts): zero both sets'
+// counters in stream order (behind anything the failed call did enqueue) and restart the parity,
+// so the next call appends to a clean set.
+void xq_reset(const nsh_fir_plan* p, hipStream_t s)
+{
+    std::lock_guard<std::mutex> g(p->xq_mu);
+    for (auto& q : p->xq)
+        if (q.s == s && q.d) {
+            (void)hipMemsetAsync(q.d, 0, XQ_E * sizeof(unsigned), s);
+            (void)hipMemsetAsync(q.d + q.stride, 0, XQ_E * sizeof(unsigned), s);
+            q.launches = 0;
+        }
+}
+
 template <int D, int QH>
 int launch_v11(const nsh_fir_plan* p, const float2* in, const float2* hin, float2* hout, float2* out, int64_t n_out,
                hipStream_t s)
@@ -915,14 +934,23 @@ int launch_v12(const nsh_fir_plan* p, const float2* in, const float2* hin, float
     if (!xq) return nsh::fail(e, "nsh_fir_ccf(mfma v12): exact queue");
     unsigned* cur = xq + set * stride;
     unsigned* nxt = xq + (set ^ 1) * stride;
-    nsh::launch((k_fir_mfma12<Q>), dim3((unsigned)grid), dim3(G::NT), G::LDS, s, in, hin, hout, out,
-                (const uint4*)p->frag12_dev, cur, p->L, p->sh8, n_out, per_x);
-    NSH_CK_LAUNCH("nsh_fir_ccf(mfma fp16x2 v12)");
+    // a timed call is timed as one: start with k_fir_mfma12's dispatch, stop with k_fir_exact12's
+    // (the follow-up launch and every exact chunk are inside the pair)
+    const nsh::launch_events t = nsh::take_launch_events();
+    nsh::launch_timed((k_fir_mfma12<Q>), dim3((unsigned)grid), dim3(G::NT), G::LDS, s, t.start, (hipEvent_t) nullptr, in,
+                      hin, hout, out, (const uint4*)p->frag12_dev, cur, p->L, p->sh8, n_out, per_x);
+    if ((e = hipGetLastError()) != hipSuccess) {
+        xq_reset(p, s);
+        return nsh::fail(e, "nsh_fir_ccf(mfma fp16x2 v12)");
+    }
     const int64_t xcap = (int64_t)plan_cus(p) * NSH_X12_PER_CU;
-    hipLaunchKernelGGL((k_fir_exact12<Q>), dim3((unsigned)(nchunks < xcap ? nchunks : xcap)), dim3(G::NT), G::LDS, s, in,
-                       hin, out, (const float4*)p->tf32q_dev, (const float*)p->taps_dev, (const unsigned*)cur, nxt, subcap,
-                       p->L, n_out);
-    NSH_CK_LAUNCH("nsh_fir_ccf(mfma v12 exact chunks)");
+    nsh::launch_timed((k_fir_exact12<Q>), dim3((unsigned)(nchunks < xcap ? nchunks : xcap)), dim3(G::NT), G::LDS, s,
+                      (hipEvent_t) nullptr, t.stop, in, hin, out, (const float4*)p->tf32q_dev, (const float*)p->taps_dev,
+                      (const unsigned*)cur, nxt, subcap, p->L, n_out);
+    if ((e = hipGetLastError()) != hipSuccess) {
+        xq_reset(p, s);
+        return nsh::fail(e, "nsh_fir_ccf(mfma v12 exact chunks)");
+    }
     return 0;
 }
 

@@ -797,6 +797,7 @@ const char* nsh_fir_cascade_kernel(void* plan) { return plan ? static_cast<nsh_f
 int nsh_fir_cascade_ccf(void* plan, const float* in, const float* hist_in, float* hist_out, float* out, int64_t n_out,
                         void* stream)
 {
+    nsh::launch_events_guard timing_guard; // the armed event pair never outlives this call
     auto* p = static_cast<nsh_fir_casc_plan*>(plan);
     if (!p) return nsh::fail_msg("nsh_fir_cascade_ccf: null plan");
     if (n_out <= 0) return 0;
@@ -838,11 +839,11 @@ int nsh_fir_cascade_ccf(void* plan, const float* in, const float* hist_in, float
 #endif
     wg = (a.nf + a.fpw - 1) / a.fpw;
     if (p->D == 16)
-        hipLaunchKernelGGL((k_fir_pfft<16, PW16>), dim3((unsigned)wg), dim3(pshape<16, PW16>::NT), lds_bytes<16>(),
-                           nsh::S(stream), a);
+        nsh::launch((k_fir_pfft<16, PW16>), dim3((unsigned)wg), dim3(pshape<16, PW16>::NT), lds_bytes<16>(),
+                    nsh::S(stream), a);
     else
-        hipLaunchKernelGGL((k_fir_pfft<8, PW8>), dim3((unsigned)wg), dim3(pshape<8, PW8>::NT), lds_bytes<8>(),
-                           nsh::S(stream), a);
+        nsh::launch((k_fir_pfft<8, PW8>), dim3((unsigned)wg), dim3(pshape<8, PW8>::NT), lds_bytes<8>(),
+                    nsh::S(stream), a);
     NSH_CK_LAUNCH("nsh_fir_cascade_ccf");
     return 0;
 }

@@ -26,8 +26,8 @@ SIGNATURES = {
     "nsr_fir_bench_kernel": (C.c_char_p, [_vp]),
     "nsr_fir_bench_tail": (_i, [_vp, _i64, C.POINTER(C.c_float)]),
     "nsr_fir_bench_destroy": (_i, [_vp]),
-    "nsr_c5_create": (_i, [_i, _i, _i, C.POINTER(C.c_float), _i, _i, _i64, _u64, _u64, _i, C.c_char_p, _sz,
-                           C.POINTER(_vp)]),
+    "nsr_c5_create": (_i, [_i, _i, _i, C.POINTER(C.c_float), _i, _i, _i64, _u64, _u64, C.c_char_p, _u64,
+                           C.c_char_p, _sz, C.POINTER(_vp)]),
     "nsr_c5_run": (_i, [_vp]),
     "nsr_c5_transport": (_i, [_vp, C.c_char_p, _i]),
     "nsr_c5_tail": (_i, [_vp, _i64, C.POINTER(C.c_float)]),
@@ -115,14 +115,16 @@ class FirBench:
 
 
 class C5Pipeline:
-    """One process's share of the C5 decimating pipeline (see nsr_c5_create)."""
+    """One process's share of the C5 decimating pipeline (see nsr_c5_create). Every process of
+    one pipeline passes the same rendezvous_dir (a fresh directory on this node) and nonce."""
 
     def __init__(self, taps, n, group=0, n_groups=1, device=0, decim=2, first_index=0, seed=0x6E736368,
-                 base_port=29700, transport="auto", buf_bytes=64 << 20):
+                 rendezvous_dir="", nonce=0, transport="auto", buf_bytes=64 << 20):
         t = np.ascontiguousarray(np.asarray(taps, np.float32))
         h = C.c_void_p()
         check(lib().nsr_c5_create(group, n_groups, device, _f32p(t), int(t.size), decim, int(n), first_index, seed,
-                                  base_port, transport.encode(), buf_bytes, C.byref(h)), "nsr_c5_create")
+                                  rendezvous_dir.encode(), int(nonce), transport.encode(), buf_bytes, C.byref(h)),
+              "nsr_c5_create")
         self._h = h
         self.last = group == n_groups - 1
 

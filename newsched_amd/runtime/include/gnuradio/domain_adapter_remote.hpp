@@ -20,7 +20,18 @@
 //                                            socket the TCP socket (host rings; device rings
 //                                                   staged through pinned memory)
 //
-// Crossing i uses TCP port base_port + i on `host` (the receiving process listens).
+// Rendezvous (how a sender finds its receiver). With `rendezvous_dir` set (the normal case):
+// the receiver binds an ephemeral port chosen by the kernel when its adapter is made
+// (partition time), then publishes "<port> <nonce>" in <rendezvous_dir>/crossing<i>
+// (write + rename, atomic); the sender waits for that file and only then connects, so it
+// never connects to a port nobody listens on. Without it, crossing i uses the fixed port
+// base_port + i (pick one outside ip_local_port_range). Either way the connection is
+// checked before use: a socket connected to itself (TCP simultaneous open when the sender's
+// source port equals the destination port and no listener exists yet) is rejected and the
+// connect retried; the hellos carry the role (SEND / RECV), the job's nonce and the pid, and a
+// peer with the wrong role or nonce (an echo, another job's listener, a stray client) is
+// dropped and the rendezvous retried until timeout_s. (GPUTEST_r04: an 8-rank C5 run on
+// derived ephemeral ports paired a sender with itself)
 // Sender: every post_write of the upstream block is forwarded immediately (chunks of at
 // most the receiver's free ring space). The span is released by one rule for every
 // transport (remote::transport in the .cpp): at once when the transport's read of it is
@@ -50,6 +61,10 @@ class transport; // data path: "rccl" | "p2p" | "socket" | "deferred_test"
 // deferred_test transport: messages whose ring span changed between send() and the transport's
 // delayed read of it (the ring was overwritten before the transfer read it); process-wide
 uint64_t deferred_test_violations();
+// connections rejected because they were connected to themselves (process-wide)
+uint64_t self_connects_rejected();
+// hello exchanges refused because the peer had the wrong role / nonce (process-wide)
+uint64_t peers_refused();
 } // namespace remote
 
 // Placeholder scheduler for a domain that another process runs. Never initialised or
@@ -75,12 +90,19 @@ enum class remote_role { SEND, RECV };
 
 struct remote_edge_options {
     std::string host = "127.0.0.1"; // address of the receiving process
-    int base_port = 29650;          // crossing i listens on base_port + i
+    // a directory every process of the job can see (one node): receivers publish the port they
+    // were given there; "" = the fixed ports below
+    std::string rendezvous_dir;
+    int base_port = 29650;          // without rendezvous_dir: crossing i listens on base_port + i
+    uint64_t nonce = 0;             // job id, the same in every process of one flowgraph
     // "auto" (rccl across GPUs, p2p for two processes on one GPU, socket for host rings) |
     // "rccl" | "p2p" | "socket" | "deferred_test" (host rings; CPU tests of the release rule)
     std::string transport = "auto";
     int device = -1;                // GPU of this process (-1: the current thread's device)
     double timeout_s = 120.0;       // connect / accept / handshake limit
+    // p2p: how long a sender waits for a free landing slot while the receiver is alive but
+    // backpressured (its downstream slow or paused); 0 = as long as the channel is healthy
+    double stall_timeout_s = 0;
 };
 
 class domain_adapter_remote : public domain_adapter
@@ -157,6 +179,8 @@ private:
     std::mutex _rev_m;       // SEND: reverse-message reads
     std::mutex _ring_m;      // RECV: ring writes vs. reset_flags' discard
     uint64_t _inflight = 0;  // SEND: items handed to the transport, not yet released
+    int _lfd = -1;           // RECV: listening socket (bound at make)
+    int _port = 0;           // RECV: its port
     void* _stream = nullptr; // RECV thread's stream (device rings)
     void* _scratch = nullptr; // RECV: discard area after the reader finished
     size_t _scratch_bytes = 0;

@@ -14,6 +14,7 @@
 #include <sys/socket.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -29,7 +30,8 @@ namespace remote {
 
 namespace {
 enum msg_type : uint32_t {
-    M_HELLO = 0x4e534831u,
+    M_HELLO = 0x4e534832u, // "NSH2": hellos carry role, pid and nonce
+
     M_DATA = 2,
     M_DONE = 3,
     M_READER_DONE = 4,
@@ -54,7 +56,11 @@ struct hello {
     int64_t max_chunk;  // receiver's answer: items per message
     char pci[32];       // PCI bus id of `device` ("" for host rings): ordinals differ per
                         // process under per-rank HIP_VISIBLE_DEVICES, bus ids do not
+    int32_t role;       // R_SEND | R_RECV: a sender must hear a receiver, and vice versa
+    int32_t pid;        // the writer's process (diagnostics: an echo carries our own pid)
+    uint64_t nonce;     // remote_edge_options::nonce: both ends belong to one job
 };
+enum role_code : int32_t { R_SEND = 0x53454e44, R_RECV = 0x52454356 };
 // p2p: the receiver's landing slots, sent after its hello; the sender answers with a u32
 // status (0 = mapped)
 struct p2p_offer {
@@ -230,6 +236,12 @@ public:
         return ::poll(&pfd, 1, timeout_ms) > 0 && (pfd.revents & (POLLIN | POLLHUP));
     }
     void shutdown_both() { ::shutdown(_fd, SHUT_RDWR); }
+    // close with a reset instead of FIN (no TIME_WAIT): for refused peers
+    void reset_on_close()
+    {
+        linger l{ 1, 0 };
+        setsockopt(_fd, SOL_SOCKET, SO_LINGER, &l, sizeof(l));
+    }
     void shutdown_write() { ::shutdown(_fd, SHUT_WR); }
     // read and drop until the peer closes (or the timeout): closing a socket with unread
     // bytes resets the connection and can destroy data the peer has not read yet
@@ -266,49 +278,186 @@ sockaddr_in resolve(const std::string& host, int port)
     return a;
 }
 
-int listen_on(const std::string& host, int port)
+std::atomic<uint64_t> g_self_connects{ 0 };
+std::atomic<uint64_t> g_peers_refused{ 0 };
+
+// port 0: the kernel picks a free one; *bound receives the port actually bound
+int listen_on(const std::string& host, int port, int* bound)
 {
     const int fd = ::socket(AF_INET, SOCK_STREAM, 0);
     if (fd < 0) throw std::runtime_error("remote edge: socket");
     int one = 1;
     setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
     sockaddr_in a = resolve(host, port);
-    if (::bind(fd, reinterpret_cast<sockaddr*>(&a), sizeof(a)) != 0 || ::listen(fd, 4) != 0) {
+    if (::bind(fd, reinterpret_cast<sockaddr*>(&a), sizeof(a)) != 0 || ::listen(fd, 8) != 0) {
         const int e = errno;
         ::close(fd);
         throw std::runtime_error("remote edge: cannot listen on " + host + ":" + std::to_string(port) + ": " +
                                  std::strerror(e));
     }
+    sockaddr_in got{};
+    socklen_t len = sizeof(got);
+    if (::getsockname(fd, reinterpret_cast<sockaddr*>(&got), &len) != 0) {
+        ::close(fd);
+        throw std::runtime_error("remote edge: getsockname");
+    }
+    *bound = ntohs(got.sin_port);
     return fd;
 }
 
-std::shared_ptr<channel> accept_one(int lfd, double timeout_s)
+std::shared_ptr<channel> accept_one(int lfd, double timeout_s, const std::atomic<bool>& cancel)
 {
-    pollfd pfd{ lfd, POLLIN, 0 };
-    const int r = ::poll(&pfd, 1, (int)(timeout_s * 1000));
-    if (r <= 0) throw std::runtime_error("remote edge: no peer connected within the timeout");
+    const auto t0 = clk::now();
+    for (;;) {
+        pollfd pfd{ lfd, POLLIN, 0 };
+        if (::poll(&pfd, 1, 100) > 0) break;
+        if (cancel.load()) throw std::runtime_error("remote edge: cancelled");
+        if (since(t0) > timeout_s) throw std::runtime_error("remote edge: no peer connected within the timeout");
+    }
     const int fd = ::accept(lfd, nullptr, nullptr);
     if (fd < 0) throw std::runtime_error(std::string("remote edge: accept: ") + std::strerror(errno));
     return std::make_shared<channel>(fd);
 }
 
+// one hello from `ch` within timeout_s; false if none came (closed, timed out, truncated)
+bool recv_hello(channel& ch, hello& h, double timeout_s, const std::atomic<bool>& cancel)
+{
+    const auto t0 = clk::now();
+    while (!ch.readable(100)) {
+        if (cancel.load() || since(t0) > timeout_s) return false;
+    }
+    try {
+        return ch.recv_bytes(&h, sizeof(h));
+    } catch (const std::exception&) {
+        return false;
+    }
+}
+
+// A socket whose local and peer addresses are equal is connected to itself: connect() to a
+// port nobody listens on, from an ephemeral source port that happens to equal it, completes by
+// TCP simultaneous open (GPUTEST_r04, rank 4 of the 8-rank C5 rehearsal).
+bool connected_to_itself(int fd)
+{
+    sockaddr_in a{}, b{};
+    socklen_t la = sizeof(a), lb = sizeof(b);
+    if (::getsockname(fd, reinterpret_cast<sockaddr*>(&a), &la) != 0 ||
+        ::getpeername(fd, reinterpret_cast<sockaddr*>(&b), &lb) != 0)
+        return false;
+    return a.sin_addr.s_addr == b.sin_addr.s_addr && a.sin_port == b.sin_port;
+}
+
+// close without TIME_WAIT (RST): the port is free again at once for its rightful listener
+void close_reset(int fd)
+{
+    linger l{ 1, 0 };
+    setsockopt(fd, SOL_SOCKET, SO_LINGER, &l, sizeof(l));
+    ::close(fd);
+}
+
+// Test hook NSH_REMOTE_TEST_SELF_CONNECT: "1" = the first connect attempt binds its source to
+// the destination address, which with nobody listening there yields a socket connected to
+// itself (what an ephemeral source port equal to the destination does by chance); "hello" =
+// the same, and the socket-level check below is skipped, so the hello's role check has to
+// refuse the echo. Returns 0 (off), 1 or 2.
+int self_connect_hook()
+{
+    const char* f = std::getenv("NSH_REMOTE_TEST_SELF_CONNECT");
+    if (!f || !*f || *f == '0') return 0;
+    test_hook_notice("NSH_REMOTE_TEST_SELF_CONNECT", f);
+    return std::strcmp(f, "hello") == 0 ? 2 : 1;
+}
+
 std::shared_ptr<channel> connect_retry(const std::string& host, int port, double timeout_s,
-                                       const std::atomic<bool>& cancel)
+                                       const std::atomic<bool>& cancel, int& force_self)
 {
     const auto t0 = clk::now();
     const sockaddr_in a = resolve(host, port);
     for (;;) {
         const int fd = ::socket(AF_INET, SOCK_STREAM, 0);
         if (fd < 0) throw std::runtime_error("remote edge: socket");
-        if (::connect(fd, reinterpret_cast<const sockaddr*>(&a), sizeof(a)) == 0) return std::make_shared<channel>(fd);
-        ::close(fd);
+        const int hook = force_self;
+        if (hook) { // a bind failure means someone listens there: connect normally
+            force_self = 0;
+            int one = 1;
+            setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+            (void)::bind(fd, reinterpret_cast<const sockaddr*>(&a), sizeof(a));
+        }
+        if (::connect(fd, reinterpret_cast<const sockaddr*>(&a), sizeof(a)) == 0) {
+            if (hook == 2 || !connected_to_itself(fd)) return std::make_shared<channel>(fd);
+            g_self_connects.fetch_add(1);
+            std::fprintf(stderr, "newsched remote edge: rejected a socket connected to itself (%s:%d); retrying\n",
+                         host.c_str(), port);
+            close_reset(fd);
+        } else {
+            ::close(fd);
+        }
         if (cancel.load()) throw std::runtime_error("remote edge: cancelled");
         if (since(t0) > timeout_s)
             throw std::runtime_error("remote edge: cannot connect to " + host + ":" + std::to_string(port));
         std::this_thread::sleep_for(std::chrono::milliseconds(20));
     }
 }
+
+// ---- rendezvous files: <dir>/crossing<i> = "<port> <nonce>" ----------------------------
+std::string rdv_path(const std::string& dir, int crossing) { return dir + "/crossing" + std::to_string(crossing); }
+
+void rdv_publish(const std::string& dir, int crossing, int port, uint64_t nonce)
+{
+    const std::string p = rdv_path(dir, crossing);
+    const std::string tmp = p + ".tmp." + std::to_string((long)::getpid());
+    FILE* f = std::fopen(tmp.c_str(), "w");
+    if (!f) throw std::runtime_error("remote edge: cannot write " + tmp + ": " + std::strerror(errno));
+    std::fprintf(f, "%d %llu\n", port, (unsigned long long)nonce);
+    const bool ok = std::fclose(f) == 0 && std::rename(tmp.c_str(), p.c_str()) == 0; // atomic publish
+    if (!ok) throw std::runtime_error("remote edge: cannot publish " + p + ": " + std::strerror(errno));
+}
+
+// the port the receiver of `crossing` published for this job (waits for it; a file left by
+// another job -- another nonce -- is waited past, it is replaced when this job's receiver
+// publishes)
+int rdv_lookup(const std::string& dir, int crossing, uint64_t nonce, double timeout_s, const std::atomic<bool>& cancel)
+{
+    const std::string p = rdv_path(dir, crossing);
+    const auto t0 = clk::now();
+    std::string seen;
+    for (;;) {
+        if (FILE* f = std::fopen(p.c_str(), "r")) {
+            int port = 0;
+            unsigned long long n = 0;
+            const int k = std::fscanf(f, "%d %llu", &port, &n);
+            std::fclose(f);
+            if (k == 2 && port > 0 && port < 65536) {
+                if ((uint64_t)n == nonce) return port;
+                seen = " (" + p + " holds nonce " + std::to_string(n) + ", this job's is " + std::to_string(nonce) + ")";
+            }
+        }
+        if (cancel.load()) throw std::runtime_error("remote edge: cancelled");
+        if (since(t0) > timeout_s)
+            throw std::runtime_error("remote edge: no receiver published crossing " + std::to_string(crossing) + " in " +
+                                     dir + " within the timeout" + seen);
+        std::this_thread::sleep_for(std::chrono::milliseconds(10));
+    }
+}
+
+// "" if `peer` is the other end this side needs (role `want`, this job's nonce), else why not
+std::string refuse_reason(const hello& peer, int32_t want, uint64_t nonce)
+{
+    if (peer.magic != M_HELLO) return "not a newsched remote-edge hello (magic)";
+    if (peer.role != want) {
+        if (peer.role == (want == R_SEND ? R_RECV : R_SEND) && peer.pid == (int32_t)::getpid() && want == R_RECV)
+            return "the peer is this process's own sender (a socket connected to itself echoed our hello)";
+        return std::string("the peer is a ") + (peer.role == R_SEND ? "sender" : peer.role == R_RECV ? "receiver" : "stranger") +
+               " (pid " + std::to_string(peer.pid) + "), expected a " + (want == R_SEND ? "sender" : "receiver");
+    }
+    if (peer.nonce != nonce)
+        return "the peer (pid " + std::to_string(peer.pid) + ") belongs to another job (nonce " + std::to_string(peer.nonce) +
+               ", this job's is " + std::to_string(nonce) + ")";
+    return "";
+}
 } // namespace
+
+uint64_t self_connects_rejected() { return g_self_connects.load(); }
+uint64_t peers_refused() { return g_peers_refused.load(); }
 
 // ---- data transports -------------------------------------------------------------------
 //
@@ -557,7 +706,8 @@ uint64_t deferred_test_violations() { return deferred_test_transport::g_violatio
 // M_SLOT_FREE(slot) once that copy is done. A sender with no free slot reads reverse messages
 // until one comes back -- and fails instead of waiting forever when the outbox has failed (its
 // DATA headers are then skipped, so no slot would ever be freed), the adapter is closing, or
-// no slot came back within the edge's timeout.
+// the receiver closed the channel (read_reverse throws); a merely backpressured receiver is
+// waited for, unless remote_edge_options::stall_timeout_s sets a limit.
 class p2p_transport : public transport
 {
 public:
@@ -627,7 +777,10 @@ public:
             }
             _box->rethrow(); // a failed DATA job: the receiver will never free a slot
             if (_closing && _closing->load()) throw std::runtime_error("remote edge: p2p send while closing");
-            if (since(t0) > _timeout_s) throw std::runtime_error("remote edge: p2p: no landing slot freed within the timeout");
+            // a backpressured receiver (slow downstream) frees slots late, not never: only an
+            // explicit stall limit ends the wait (remote_edge_options::stall_timeout_s)
+            if (_timeout_s > 0 && since(t0) > _timeout_s)
+                throw std::runtime_error("remote edge: p2p: no landing slot freed within stall_timeout_s");
             _read_reverse(); // blocks briefly for a reverse message (M_SLOT_FREE)
         }
         void* s = hip::current_stream();
@@ -676,7 +829,7 @@ private:
     size_t _slot_bytes;
     std::function<bool()> _read_reverse;
     const std::atomic<bool>* _closing = nullptr;
-    double _timeout_s = 120.0;
+    double _timeout_s = 0; // stall limit, 0 = none
     int _fail_after = -1; // test hook: DATA jobs from this one on fail
     int _sent = 0;
     void* _local = nullptr;  // receiver: the slots
@@ -839,12 +992,6 @@ struct adapter_port_intf : neighbor_interface {
         cv->notify_all();
     }
 };
-std::mutex g_listen_m;
-std::map<std::pair<int, int>, int>& listen_fds() // (port, crossing) -> listening fd
-{
-    static std::map<std::pair<int, int>, int> m;
-    return m;
-}
 } // namespace
 
 domain_adapter_remote::domain_adapter_remote(remote_role role, int crossing, const remote_edge_options& opt)
@@ -869,11 +1016,12 @@ domain_adapter_remote::sptr domain_adapter_remote::make(remote_role role, port_s
     p->_isz = other_port->itemsize();
     if (role == remote_role::RECV) {
         // listen now (partition time), accept later: the peer can connect whenever it
-        // reaches this crossing, whatever order either process initialises its edges in
-        const int port = opt.base_port + crossing;
-        std::lock_guard<std::mutex> g(g_listen_m);
-        auto key = std::make_pair(port, crossing);
-        if (!listen_fds().count(key)) listen_fds()[key] = remote::listen_on(opt.host, port);
+        // reaches this crossing, whatever order either process initialises its edges in.
+        // With a rendezvous directory the kernel picks the port (bound before anyone can
+        // connect to it) and the sender learns it from the published file.
+        const bool rdv = !opt.rendezvous_dir.empty();
+        p->_lfd = remote::listen_on(opt.host, rdv ? 0 : opt.base_port + crossing, &p->_port);
+        if (rdv) remote::rdv_publish(opt.rendezvous_dir, crossing, p->_port, opt.nonce);
     }
     return p;
 }
@@ -919,13 +1067,15 @@ domain_adapter_remote::~domain_adapter_remote()
         nsh_stream_sync(_stream);
         nsh_stream_destroy(_stream);
     }
-    if (_role == remote_role::RECV) {
-        std::lock_guard<std::mutex> g(g_listen_m);
-        auto key = std::make_pair(_opt.base_port + _crossing, _crossing);
-        auto it = listen_fds().find(key);
-        if (it != listen_fds().end()) {
-            ::close(it->second);
-            listen_fds().erase(it);
+    if (_lfd >= 0) ::close(_lfd);
+    if (_role == remote_role::RECV && !_opt.rendezvous_dir.empty()) {
+        // withdraw this receiver's entry, unless another receiver has replaced it since
+        const std::string p = remote::rdv_path(_opt.rendezvous_dir, _crossing);
+        if (FILE* f = std::fopen(p.c_str(), "r")) {
+            int port = 0;
+            const bool mine = std::fscanf(f, "%d", &port) == 1 && port == _port;
+            std::fclose(f);
+            if (mine) ::unlink(p.c_str());
         }
     }
 }
@@ -966,14 +1116,53 @@ void domain_adapter_remote::buffer_ready()
         mine.is_device = dev_side ? 1 : 0;
         mine.device = _device;
         mine.want = transport_code(_opt.transport);
+        mine.role = _role == remote_role::SEND ? R_SEND : R_RECV;
+        mine.pid = (int32_t)::getpid();
+        mine.nonce = _opt.nonce;
         if (dev_side && _device >= 0) hip::check(nsh_device_pci_id(_device, mine.pci, (int)sizeof(mine.pci)), "remote edge: pci id");
+        const std::string where = "remote edge: crossing " + std::to_string(_crossing);
         hello peer{};
+        const auto t0 = clk::now();
+        std::string last_refusal;
+        // a peer that is not this crossing's other end: counted, said on stderr, dropped
+        auto refused = [&](const std::string& why) {
+            g_peers_refused.fetch_add(1);
+            last_refusal = why;
+            std::fprintf(stderr, "newsched %s: refused a peer: %s; retrying\n", where.c_str(), why.c_str());
+        };
+        auto out_of_time = [&] {
+            return std::runtime_error(where + ": no valid " + (_role == remote_role::SEND ? "receiver" : "sender") +
+                                      " within " + std::to_string((int)_opt.timeout_s) + " s" +
+                                      (last_refusal.empty() ? "" : " (last peer refused: " + last_refusal + ")"));
+        };
         if (_role == remote_role::SEND) {
-            _ch = connect_retry(_opt.host, _opt.base_port + _crossing, _opt.timeout_s, _closing);
-            _ch->send_bytes(&mine, sizeof(mine));
-            if (!_ch->recv_bytes(&peer, sizeof(peer))) throw std::runtime_error("remote edge: peer closed in handshake");
-            if (peer.magic != M_HELLO || peer.crossing != _crossing || peer.item_size != _isz)
-                throw std::runtime_error("remote edge: handshake mismatch on crossing " + std::to_string(_crossing));
+            int force_self = self_connect_hook();
+            for (;;) { // rendezvous, connect, hello; a wrong peer is dropped and the rendezvous retried
+                const double left = _opt.timeout_s - since(t0);
+                if (left <= 0) throw out_of_time();
+                const int port = _opt.rendezvous_dir.empty()
+                                     ? _opt.base_port + _crossing
+                                     : rdv_lookup(_opt.rendezvous_dir, _crossing, _opt.nonce, left, _closing);
+                auto ch = connect_retry(_opt.host, port, left, _closing, force_self);
+                ch->send_bytes(&mine, sizeof(mine));
+                if (!recv_hello(*ch, peer, _opt.timeout_s - since(t0), _closing)) {
+                    if (_closing.load()) throw std::runtime_error("remote edge: cancelled");
+                    refused("no hello from " + _opt.host + ":" + std::to_string(port));
+                    continue;
+                }
+                const std::string why = refuse_reason(peer, R_RECV, _opt.nonce);
+                if (why.empty()) {
+                    _ch = std::move(ch);
+                    break;
+                }
+                refused(why);
+                ch->reset_on_close();
+                std::this_thread::sleep_for(std::chrono::milliseconds(20));
+            }
+            // the right job and role: anything else that differs is a configuration error
+            if (peer.crossing != _crossing || peer.item_size != _isz)
+                throw std::runtime_error(where + ": handshake mismatch (peer crossing " + std::to_string(peer.crossing) +
+                                         ", item size " + std::to_string(peer.item_size) + " vs " + std::to_string(_isz) + ")");
             _max_chunk = (int)peer.max_chunk;
             int32_t chosen = peer.chosen;
             if (chosen == T_P2P) {
@@ -983,7 +1172,7 @@ void domain_adapter_remote::buffer_ready()
                 std::string why;
                 try {
                     _tr = std::make_shared<p2p_transport>(_device, offer, [this] { return read_reverse(100); }, &_closing,
-                                                          _opt.timeout_s);
+                                                          _opt.stall_timeout_s);
                 } catch (const std::exception& e) {
                     status = 1;
                     why = e.what();
@@ -1001,17 +1190,28 @@ void domain_adapter_remote::buffer_ready()
             else if (chosen == T_SOCKET)
                 _tr = std::make_shared<socket_transport>(dev_side);
             else if (chosen != T_P2P)
-                throw std::runtime_error("remote edge: bad transport answer");
+                throw std::runtime_error(where + ": the receiver answered no transport (code " + std::to_string(chosen) + ")");
         } else {
-            int lfd;
-            {
-                std::lock_guard<std::mutex> g(g_listen_m);
-                lfd = listen_fds().at(std::make_pair(_opt.base_port + _crossing, _crossing));
+            for (;;) { // accept until this crossing's sender says hello
+                const double left = _opt.timeout_s - since(t0);
+                if (left <= 0) throw out_of_time();
+                auto ch = accept_one(_lfd, left, _closing);
+                if (!recv_hello(*ch, peer, _opt.timeout_s - since(t0), _closing)) {
+                    if (_closing.load()) throw std::runtime_error("remote edge: cancelled");
+                    refused("a client connected and sent no hello");
+                    continue;
+                }
+                const std::string why = refuse_reason(peer, R_SEND, _opt.nonce);
+                if (why.empty()) {
+                    _ch = std::move(ch);
+                    break;
+                }
+                refused(why);
+                ch->reset_on_close();
             }
-            _ch = accept_one(lfd, _opt.timeout_s);
-            if (!_ch->recv_bytes(&peer, sizeof(peer))) throw std::runtime_error("remote edge: peer closed in handshake");
-            if (peer.magic != M_HELLO || peer.crossing != _crossing || peer.item_size != _isz)
-                throw std::runtime_error("remote edge: handshake mismatch on crossing " + std::to_string(_crossing));
+            if (peer.crossing != _crossing || peer.item_size != _isz)
+                throw std::runtime_error(where + ": handshake mismatch (peer crossing " + std::to_string(peer.crossing) +
+                                         ", item size " + std::to_string(peer.item_size) + " vs " + std::to_string(_isz) + ")");
             // messages must fit the empty ring in one contiguous span
             buffer_info_t wi{};
             _buffer->write_info(wi);

@@ -401,6 +401,60 @@ TEST(HipDomain, DecimatingChainC5)
     }
 }
 
+// Kernel timing through the polyphase-FFT kernel: its launch must record the event
+// pair the block arms (nsh::launch), so kernel_ms() reads recorded events -- for the fused C5
+// cascade and for a single decim-16 fir_filter_ccf, which AUTO resolves to k_fir_pfft. Both are
+// parity-checked on the same run.
+TEST(HipDomain, TimedPfftLaunches)
+{
+    const size_t n = size_t(1) << 20;
+    const auto h = lowpass(127, 0.225);
+    {
+        auto ref = synth(n);
+        for (int i = 0; i < 4; ++i) ref = fir_ref(ref, h, 2);
+        auto src = hip::synth_source::make(0, n);
+        std::vector<hip::fir_filter_ccf::sptr> st;
+        for (int i = 0; i < 4; ++i) st.push_back(hip::fir_filter_ccf::make(h, 2));
+        auto snk = blocks::vector_sink_c::make(1, n / 16);
+        auto fg = flowgraph::make();
+        fg->connect(src, 0, st[0], 0);
+        for (int i = 1; i < 4; ++i) fg->connect(st[i - 1], 0, st[i], 0);
+        fg->connect(st[3], 0, snk, 0)->set_custom_buffer(HIP_BUFFER_ARGS_D2H);
+        auto sched = schedulers::scheduler_hip::make("hip", 0, 1u << 19);
+        fg->set_scheduler(sched);
+        fg->validate();
+        ASSERT_TRUE(sched->fusion_plan().fused.size() == 1u);
+        auto c = std::dynamic_pointer_cast<hip::fir_filter_cascade_ccf>(sched->fusion_plan().fused[0]);
+        ASSERT_TRUE(c != nullptr);
+        c->enable_timing(true);
+        fg->run();
+        EXPECT_TRUE(close_normwise(snk->data(), ref));
+        const double ms = c->kernel_ms(); // throws if any armed pair went unrecorded
+        std::printf("  cascade: %llu launches, %.3f ms\n", (unsigned long long)c->launches(), ms);
+        EXPECT_TRUE(ms > 0.0);
+    }
+    {
+        const auto h16 = lowpass(127, 0.03);
+        const auto ref = fir_ref(synth(n), h16, 16);
+        auto src = hip::synth_source::make(0, n);
+        auto fir = hip::fir_filter_ccf::make(h16, 16);
+        auto snk = blocks::vector_sink_c::make(1, n / 16);
+        auto fg = flowgraph::make();
+        fg->connect(src, 0, fir, 0);
+        fg->connect(fir, 0, snk, 0)->set_custom_buffer(HIP_BUFFER_ARGS_D2H);
+        auto sched = schedulers::scheduler_hip::make("hip", 0, 1u << 19);
+        fg->set_scheduler(sched);
+        fg->validate();
+        fir->enable_timing(true);
+        fg->run();
+        EXPECT_TRUE(fir->kernel() == "k_fir_pfft<16,1>");
+        EXPECT_TRUE(close_normwise(snk->data(), ref));
+        const double ms = fir->kernel_ms();
+        std::printf("  decim-16 fir: %llu timed launches, %.3f ms\n", (unsigned long long)fir->timed_launches(), ms);
+        EXPECT_TRUE(fir->timed_launches() > 0 && ms > 0.0);
+    }
+}
+
 TEST(HipDomain, CrossThreadDeviceEdges)
 {
     // hip blocks on separate scheduler_mt threads: each thread has its own stream, so

@@ -44,8 +44,12 @@ static int rank() { return env_int("QA_RANK", 0); }
 static remote_edge_options opts()
 {
     remote_edge_options o;
+    // the harness gives every case a fresh rendezvous directory (QA_RDV) and a job nonce; QA_PORT
+    // alone selects the fixed-port mode (the self-connect case)
+    if (const char* d = std::getenv("QA_RDV")) o.rendezvous_dir = d;
+    if (const char* n = std::getenv("QA_NONCE")) o.nonce = std::strtoull(n, nullptr, 10);
     o.base_port = env_int("QA_PORT", 29650);
-    o.timeout_s = 60;
+    o.timeout_s = env_int("QA_TIMEOUT", 60);
     if (const char* t = std::getenv("QA_TRANSPORT")) o.transport = t; // default "auto"
     return o;
 }
@@ -705,4 +709,86 @@ TEST(RemoteCpu, RendezvousMisorderTimesOut)
     }
     std::printf("  rank %d: run() raised: %s\n", rank(), what.empty() ? "(nothing)" : what.c_str());
     EXPECT_TRUE(what.find("rendezvous timed out") != std::string::npos);
+}
+
+// Self-connect (GPUTEST_r04's failure, made deterministic): fixed-port mode, the receiver
+// [rank 1] starts listening only after 1.5 s, and the sender's first connect attempt binds its
+// source to the destination port (NSH_REMOTE_TEST_SELF_CONNECT), which with nobody listening
+// yields a socket connected to itself. QA_SELF_MODE=socket: the socket-level check must reject
+// it; QA_SELF_MODE=hello: that check is skipped (hook value "hello") and the hello's role check
+// must refuse the echo of the sender's own hello. Either way the sender retries, pairs with the
+// real receiver, and the data arrive bit-exact.
+TEST(RemoteCpu, SelfConnectRejected)
+{
+    const char* mode = std::getenv("QA_SELF_MODE");
+    const bool hello_mode = mode && std::string(mode) == "hello";
+    if (rank() == 1) std::this_thread::sleep_for(std::chrono::milliseconds(1500));
+    const size_t n = 60000;
+    auto x = synth(n, 21);
+    auto src = blocks::vector_source_c::make(x);
+    auto cp0 = blocks::copy::make(sizeof(gr_complex));
+    auto cp1 = blocks::copy::make(sizeof(gr_complex));
+    auto snk = blocks::vector_sink_c::make(1, n);
+    auto fg = flowgraph::make();
+    fg->connect(src, 0, cp0, 0);
+    fg->connect(cp0, 0, cp1, 0);
+    fg->connect(cp1, 0, snk, 0);
+    auto s0 = sched_for(0, schedulers::scheduler_mt::make("r0", 8192));
+    auto s1 = sched_for(1, schedulers::scheduler_mt::make("r1", 8192));
+    fg->set_schedulers({ s0, s1 });
+    auto o = opts();
+    o.base_port += 160;
+    auto da = domain_adapter_remote_conf::make(o);
+    domain_conf_vec dc{ domain_conf(s0, { src, cp0 }, da), domain_conf(s1, { cp1, snk }, da) };
+    fg->partition(dc);
+    fg->run();
+    if (rank() == 1) EXPECT_TRUE(snk->data() == x);
+    if (rank() == 0) {
+        std::printf("  self-connects rejected: %llu, peers refused: %llu\n",
+                    (unsigned long long)remote::self_connects_rejected(), (unsigned long long)remote::peers_refused());
+        if (hello_mode)
+            EXPECT_TRUE(remote::peers_refused() >= 1);
+        else
+            EXPECT_TRUE(remote::self_connects_rejected() >= 1);
+    }
+    expect_transport(da);
+}
+
+// Two jobs on one port: the ranks carry different nonces (QA_NONCE + rank), as if each had met
+// another job's process on a reused port. The receiver refuses the sender's hello, the sender
+// sees its connection dropped, both retry until QA_TIMEOUT and fg->run() raises in both
+// processes; the receiver names the nonce. Nothing is paired, nothing is transferred.
+TEST(RemoteCpu, ForeignNonceRefused)
+{
+    const size_t n = 20000;
+    auto src = blocks::vector_source_c::make(synth(n, 4));
+    auto cp0 = blocks::copy::make(sizeof(gr_complex));
+    auto cp1 = blocks::copy::make(sizeof(gr_complex));
+    auto snk = blocks::vector_sink_c::make(1, n);
+    auto fg = flowgraph::make();
+    fg->connect(src, 0, cp0, 0);
+    fg->connect(cp0, 0, cp1, 0);
+    fg->connect(cp1, 0, snk, 0);
+    auto s0 = sched_for(0, schedulers::scheduler_mt::make("r0", 8192));
+    auto s1 = sched_for(1, schedulers::scheduler_mt::make("r1", 8192));
+    fg->set_schedulers({ s0, s1 });
+    auto o = opts();
+    o.base_port += 170;
+    o.nonce += (uint64_t)rank() + 1;
+    auto conf = domain_adapter_remote_conf::make(o);
+    domain_conf_vec dc{ domain_conf(s0, { src, cp0 }, conf), domain_conf(s1, { cp1, snk }, conf) };
+    fg->partition(dc);
+    std::string what;
+    try {
+        fg->run();
+    } catch (const std::exception& e) {
+        what = e.what();
+    }
+    std::printf("  rank %d: run() raised: %s\n", rank(), what.empty() ? "(nothing)" : what.c_str());
+    std::printf("  peers refused: %llu\n", (unsigned long long)remote::peers_refused());
+    EXPECT_TRUE(!what.empty());
+    if (rank() == 1) {
+        EXPECT_TRUE(what.find("another job") != std::string::npos);
+        EXPECT_TRUE(remote::peers_refused() >= 1);
+    }
 }

@@ -877,3 +877,59 @@ def test_time_next_launch_events(torch_cuda):
     assert L.nsh_event_elapsed_ms(ev[0], ev[1], C.byref(ms2)) == 0 and ms2.value == ms.value
     for e in ev:
         L.nsh_event_destroy(e)
+
+
+def test_armed_timing_cleared_on_early_return(torch_cuda):
+    """An event pair armed before a FIR call that launches nothing (n_out = 0) is dropped when the
+    call returns (launch_events_guard): the next, unrelated FIR launch does not record
+    it, so the events stay unrecorded."""
+    import ctypes as C
+    torch = torch_cuda
+    L = nsh.lib()
+    h = _firwin127()
+    plan = nsh.FirPlan(h, 1, nsh.FIR_MFMA)
+    n = 1 << 16
+    dx = dev(torch, orc.synth(n, 5))
+    dy = torch.empty(n, dtype=torch.complex64, device="cuda")
+    hout = torch.empty(126, dtype=torch.complex64, device="cuda")
+    ev = [C.c_void_p(), C.c_void_p()]
+    for e in ev:
+        assert L.nsh_event_create(C.byref(e)) == 0
+    assert L.nsh_time_next_launch(ev[0], ev[1]) == 0
+    plan(dx, 0, hout, dy, 0)  # nothing to do: returns before any launch
+    plan(dx, 0, hout, dy, n)  # must not be timed
+    torch.cuda.synchronize()
+    ms = C.c_float()
+    assert L.nsh_event_elapsed_ms(ev[0], ev[1], C.byref(ms)) != 0  # never recorded
+    for e in ev:
+        L.nsh_event_destroy(e)
+    plan.close()
+
+
+def test_pfft_plan_timed(torch_cuda):
+    """A decim-16 plan (AUTO -> k_fir_pfft) records the armed pair with its own dispatch."""
+    import ctypes as C
+    import scipy.signal as ss
+    torch = torch_cuda
+    L = nsh.lib()
+    h = ss.firwin(127, 0.03).astype(np.float32)
+    plan = nsh.FirPlan(h, 16, nsh.FIR_AUTO)
+    assert plan.kernel.startswith("k_fir_pfft"), plan.kernel
+    n_out = 1 << 16
+    x = orc.synth(16 * n_out, 9)
+    dx = dev(torch, x)
+    dy = torch.empty(n_out, dtype=torch.complex64, device="cuda")
+    hout = torch.empty(126, dtype=torch.complex64, device="cuda")
+    ev = [C.c_void_p(), C.c_void_p()]
+    for e in ev:
+        assert L.nsh_event_create(C.byref(e)) == 0
+    assert L.nsh_time_next_launch(ev[0], ev[1]) == 0
+    plan(dx, 0, hout, dy, n_out)
+    torch.cuda.synchronize()
+    ms = C.c_float()
+    assert L.nsh_event_elapsed_ms(ev[0], ev[1], C.byref(ms)) == 0 and ms.value > 0
+    ok, err, _ = orc.tol_ok(host(dy), orc.fir_ccf(x, h, 16))
+    assert ok, err
+    for e in ev:
+        L.nsh_event_destroy(e)
+    plan.close()

@@ -12,8 +12,10 @@ send holds the sender's stream until the peer's stream has reached the matching 
 negative control, a mis-ordered receive, deadlocks and is reported as a rendezvous timeout)."""
 import os
 import random
+import shutil
 import socket
 import subprocess
+import tempfile
 
 import pytest
 
@@ -23,9 +25,18 @@ EXE = os.path.join(ROOT, "build", "tests", "qa_remote_edge")
 FAKE_RCCL = os.path.join(ROOT, "build", "tests", "libfake_rccl.so")
 
 
-def free_port_block(width=64):
+def fixed_port_block(width=256):
+    """A free block of ports BELOW the kernel's ephemeral range (ip_local_port_range), for the
+    fixed-port cases: a port inside that range can be handed to some connect() as its source
+    port while nobody listens on it -- the self-connect of GPUTEST_r04."""
+    try:
+        with open("/proc/sys/net/ipv4/ip_local_port_range") as f:
+            lo = int(f.read().split()[0])
+    except (OSError, ValueError, IndexError):
+        lo = 32768
+    hi = max(lo - width, 12000)
     for _ in range(200):
-        base = random.randrange(20000, 60000 - width)
+        base = random.randrange(10000, hi)
         ok = True
         for p in range(base, base + width):
             s = socket.socket()
@@ -43,28 +54,73 @@ def free_port_block(width=64):
     raise RuntimeError("no free port block")
 
 
-def run_pair(case, timeout=120, env_extra=None, ranks=2):
+def run_pair(case, timeout=120, env_extra=None, ranks=2, fixed_port=False, expect_ok=True):
+    """Run `case` as `ranks` processes. Default: a fresh rendezvous directory and job nonce
+    (receivers listen on kernel-chosen ports and publish them there); fixed_port=True: the
+    fixed-port mode on a block below the ephemeral range."""
     if not (os.path.exists(EXE) and os.path.exists(FAKE_RCCL)):
         subprocess.run(["make", "-s", "-C", ROOT, "tests"], check=True)
-    port = free_port_block(192)
+    rdv = tempfile.mkdtemp(prefix="nsh_rdv_")
+    base = dict(QA_NONCE=str(random.getrandbits(62)))
+    if fixed_port:
+        base["QA_PORT"] = str(fixed_port_block())
+    else:
+        base["QA_RDV"] = rdv
     procs = []
-    for r in range(ranks):
-        env = dict(os.environ, QA_RANK=str(r), QA_PORT=str(port), **(env_extra or {}))
-        procs.append(subprocess.Popen([EXE, case], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
-    outs = []
-    for p in procs:
-        try:
-            out, _ = p.communicate(timeout=timeout)
-        except subprocess.TimeoutExpired:
-            for q in procs:
-                q.kill()
-            raise
-        outs.append(out)
+    try:
+        for r in range(ranks):
+            env = dict(os.environ, QA_RANK=str(r), **base, **(env_extra or {}))
+            procs.append(subprocess.Popen([EXE, case], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                                          text=True))
+        outs = []
+        for p in procs:
+            try:
+                out, _ = p.communicate(timeout=timeout)
+            except subprocess.TimeoutExpired:
+                for q in procs:
+                    q.kill()
+                raise
+            outs.append(out)
+    finally:
+        shutil.rmtree(rdv, ignore_errors=True)
     for r, (p, out) in enumerate(zip(procs, outs)):
         print(f"--- rank {r} ---\n{out}")
         assert p.returncode == 0, f"rank {r} failed:\n{out}"
         assert "0 failure(s)" in out and "1 test(s)" in out, out
     return outs
+
+
+@pytest.mark.parametrize("mode", ["socket", "hello"])
+def test_self_connect_rejected(mode):
+    """GPUTEST_r04's failure forced deterministically: the sender's first connect binds its source
+    to the destination port while the receiver is not yet listening, so the socket is connected to
+    itself. mode=socket: the getsockname == getpeername check rejects it; mode=hello: with that check
+    skipped, the hello's role check refuses the echo of the sender's own hello. Either way the
+    sender retries and pairs with the real receiver; the data arrive bit-exact."""
+    outs = run_pair("RemoteCpu.SelfConnectRejected", fixed_port=True,
+                    env_extra={"NSH_REMOTE_TEST_SELF_CONNECT": "1" if mode == "socket" else "hello",
+                               "QA_SELF_MODE": mode})
+    if mode == "socket":
+        assert "rejected a socket connected to itself" in outs[0]
+    else:
+        assert "own sender" in outs[0]
+
+
+def test_foreign_nonce_refused():
+    """Two jobs meeting on one port (different nonces): the receiver refuses the hello, nothing
+    pairs, and fg->run() raises in both processes after the timeout, naming the nonce."""
+    outs = run_pair("RemoteCpu.ForeignNonceRefused", fixed_port=True, env_extra={"QA_TIMEOUT": "4"})
+    assert "another job" in outs[1]
+
+
+def test_rendezvous_dir_isolates_jobs():
+    """Two pipelines of the same case at once, each with its own rendezvous directory and nonce:
+    kernel-chosen ports, no collisions, both bit-exact."""
+    import concurrent.futures as cf
+    with cf.ThreadPoolExecutor(2) as ex:
+        futs = [ex.submit(run_pair, "RemoteCpu.ChainRestart") for _ in range(2)]
+        for f in futs:
+            f.result()
 
 
 @pytest.mark.parametrize("case", ["RemoteCpu.ChainRestart", "RemoteCpu.TwoCrossingsBothWays",
