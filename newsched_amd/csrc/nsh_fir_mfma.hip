@@ -829,6 +829,416 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma11(const float2* __restrict_
     if (ch <= c_last) step(vb, vc, va, ch);
 }
 
+// ---- k_fir_mfma13: the decimators' lockstep walk, exact chunks queued (round 5) ------------
+// k_fir_mfma11's per-chunk work (polyphase split at a per-chunk scale, the same MFMA tile) in a
+// different walk: the persistent workgroups of an XCD (x = blockIdx mod 8, W of them) take its
+// eighth of the chunks in lockstep -- at step i workgroup k of XCD x filters chunk
+// x per_x + k + i W -- so each XCD streams one contiguous window of W chunks at a time instead of
+// W separate ranges (profiles/r04zw_v11_xcd_ab.log: D = 4 9.5 % faster, bit-identical). Each
+// chunk's halo (the D H input samples before it, the tail of the chunk its neighbour filters in the
+// same step: an L2 hit) is loaded with it and staged raw in an LDS stash, one step ahead, for the
+// split; scale and exact-path test cover the chunk and its halo (k_fir_mfma11's scale covered the
+// whole previous chunk: outputs match it within the split's rounding, bit for bit wherever both
+// pick the same scale). Chunks the split cannot carry are not filtered here: the workgroup appends
+// them to the launch's exact queue and k_fir_exact13 (same stream, right after) filters them -- so a
+// periodic pattern of exact chunks, which the lockstep walk would put on one workgroup per XCD,
+// cannot unbalance it (r04zw: every 64th chunk exact 968 vs 548 us with the exact forms inline).
+template <int D, int QH>
+__device__ __forceinline__ void load13(const float2* __restrict__ in, const float2* __restrict__ hist_in, int L, int64_t n_in,
+                                       int64_t ch, float4 (&v)[4], float4& hv)
+{
+    using G = geom11<D, QH>;
+    const int tid = threadIdx.x;
+    const __amdgpu_buffer_rsrc_t r = chunk_rsrc<G::CHUNK_IN>(in, ch, n_in);
+#pragma unroll
+    for (int u = 0; u < G::UNITS; ++u)
+#pragma unroll
+        for (int f = 0; f < D; ++f) {
+            const nsh::buf_f4 t = __builtin_bit_cast(
+                nsh::buf_f4, __builtin_amdgcn_raw_buffer_load_b128(r, ((tid + G::NT * u) * D + f) * 16, 0, D == 2 ? NSH_V11_AUX2 : NSH_V11_AUX4));
+            v[u * D + f] = make_float4(t.x, t.y, t.z, t.w);
+        }
+    // the halo: input samples [ch CHUNK_IN - 2 HP, ch CHUNK_IN), two per thread tid < HP, from `in`
+    // (ch > 0) or the history (ch = 0: element g + L - 1; out-of-range lanes and a null history read
+    // zeros); one buffer resource either way, no branch between the loads. A chunk index past the
+    // stream (an empty prefetch) reads zeros.
+    __amdgpu_buffer_rsrc_t hr;
+    int off0, off1;
+    if (ch > 0) {
+        hr = chunk_rsrc<2 * G::HP>(in + ch * G::CHUNK_IN - 2 * G::HP, 0, ch * G::CHUNK_IN <= n_in ? 2 * G::HP : 0);
+        off0 = 16 * tid;
+        off1 = off0 + 8;
+    } else {
+        hr = chunk_rsrc<1 << 20>(hist_in, 0, hist_in ? L - 1 : 0);
+        const int e = 2 * tid - 2 * G::HP + (L - 1);
+        off0 = e >= 0 ? 8 * e : 1 << 30;
+        off1 = e + 1 >= 0 ? 8 * (e + 1) : 1 << 30;
+    }
+    hv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (tid < G::HP) {
+        const nsh::buf_f2 a = __builtin_bit_cast(nsh::buf_f2, __builtin_amdgcn_raw_buffer_load_b64(hr, off0, 0, 0));
+        const nsh::buf_f2 b = __builtin_bit_cast(nsh::buf_f2, __builtin_amdgcn_raw_buffer_load_b64(hr, off1, 0, 0));
+        hv = make_float4(a.x, a.y, b.x, b.y);
+    }
+}
+
+template <int D, int QH>
+__global__ __launch_bounds__(256, 2) void k_fir_mfma13(const float2* __restrict__ in,
+                                                      const float2* __restrict__ hist_in,
+                                                      float2* __restrict__ hist_out,
+                                                      float2* __restrict__ out,
+                                                      const _Float16* __restrict__ frag, // per phase: [2][KS][64] x8, [2][64] x4
+                                                      unsigned* __restrict__ xq,         // this launch's exact-queue set
+                                                      int64_t subcap,
+                                                      int L,
+                                                      int sh,
+                                                      int64_t n_out,
+                                                      int64_t per_x)
+{
+    using G = geom11<D, QH>;
+    constexpr int KS = G::KS;
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    float4* stash = reinterpret_cast<float4*>(lds + 2 * G::BUF); // [2][HP] raw halos, one step ahead
+    unsigned* slot_max = reinterpret_cast<unsigned*>(lds + G::SLOTS);
+    unsigned* slot_mnz = slot_max + 8;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int64_t n_in = n_out * D;
+    if (blockIdx.x == 0)
+        for (int j = tid; j < L - 1; j += G::NT) hist_out[j] = virt(in, hist_in, n_in - (L - 1) + j, n_in, L);
+
+    const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
+    const int W = (int)(gridDim.x >> 3);
+    const int64_t xb = (int64_t)(blockIdx.x & 7) * per_x;
+    const int64_t xe = xb + per_x < nchunks ? xb + per_x : nchunks;
+    const int64_t c_first = xb + (blockIdx.x >> 3);
+    if (c_first >= xe) return; // whole workgroup, before any barrier
+    // the workgroup's i-th chunk; past its XCD's range an empty buffer range (loads return 0)
+    auto chunk_at = [&](int64_t i) { const int64_t c = c_first + i * W; return c < xe ? c : nchunks; };
+    const int64_t n_steps = (xe - c_first + W - 1) / W;
+
+    f16x8 B0[D][KS + 1], B1[D][KS + 1];
+    f16x4 T0[D], T1[D];
+#pragma unroll
+    for (int r = 0; r < D; ++r) {
+        const _Float16* fr = frag + (size_t)r * G::PER_PHASE;
+#pragma unroll
+        for (int st = 0; st < KS; ++st) {
+            B0[r][st] = reinterpret_cast<const f16x8*>(fr)[(0 * KS + st) * 64 + lane];
+            B1[r][st] = reinterpret_cast<const f16x8*>(fr)[(1 * KS + st) * 64 + lane];
+        }
+        const f16x4* tf = reinterpret_cast<const f16x4*>(fr + 2 * KS * 64 * 8);
+        T0[r] = tf[lane];
+        T1[r] = tf[64 + lane];
+    }
+
+    const int rho = lane & 15;
+    const int c = rho & 1, b = rho >> 1;
+    const int g = lane >> 4;
+    const int phase = lane & 15;
+    const int row_base = c * G::IM_OFF + (G::HR + wave * (G::WAVE_OUT / 16) + b) * 32;
+    auto reduce = [&](const float4 (&v)[4], const float4& hv, unsigned& m, unsigned& z) {
+        float mf = max_abs4(hv);
+        z = min_nz1(hv);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            mf = __builtin_elementwise_maximum(mf, max_abs4(v[u]));
+            z = min(z, min_nz1(v[u]));
+        }
+        m = wave_max(__float_as_uint(mf));
+        z = wave_min(z);
+    };
+    auto put_halo = [&](float4* st, const float4& hv) {
+        if (tid < G::HP) st[tid] = hv;
+    };
+    // chunk + its raw halo (stash) -> the split phase planes
+    auto put_split = [&](unsigned char* buf, const float4* hsrc, const float4 (&v)[4], int sc) {
+        if (tid < D * (G::H / 2)) { // halo: phase r, pair pi from the raw halo samples
+            const int r = tid / (G::H / 2), pi = tid % (G::H / 2);
+            const int sr = r == 0 ? 0 : D - r;
+            const int pa = D * (2 * pi) + sr, pb = D * (2 * pi + 1) + sr;
+            const float2 a = f4_sample(hsrc[pa >> 1], pa & 1), bb = f4_sample(hsrc[pb >> 1], pb & 1);
+            store_pair11<D, QH>(buf, r, 2 * pi, a.x, bb.x, a.y, bb.y, sc);
+        }
+#pragma unroll
+        for (int u = 0; u < G::UNITS; ++u) {
+            const int i0 = 2 * (tid + G::NT * u);
+#pragma unroll
+            for (int r = 0; r < D; ++r) {
+                const int sr = r == 0 ? 0 : D - r;
+                const int la = sr, lb = D + sr;
+                const float2 a = f4_sample(v[u * D + la / 2], la & 1);
+                const float2 bb = f4_sample(v[u * D + lb / 2], lb & 1);
+                store_pair11<D, QH>(buf, r, G::H + i0, a.x, bb.x, a.y, bb.y, sc);
+            }
+        }
+    };
+    auto mfma_tile = [&](const unsigned char* cur, int unscale, nf2 (&o)[2 * G::TILES]) {
+        f32x4 hi[G::TILES], lo[G::TILES], hi_t[G::TILES], lo_t[G::TILES];
+#pragma unroll
+        for (int t = 0; t < G::TILES; ++t) {
+            hi[t] = f32x4{ 0.f, 0.f, 0.f, 0.f };
+            lo[t] = f32x4{ 0.f, 0.f, 0.f, 0.f };
+            hi_t[t] = f32x4{ 0.f, 0.f, 0.f, 0.f };
+            lo_t[t] = f32x4{ 0.f, 0.f, 0.f, 0.f };
+        }
+#pragma unroll
+        for (int r = 0; r < D; ++r) {
+            const unsigned char* ph = cur + r * G::PH;
+#pragma unroll
+            for (int st = 0; st < KS; ++st) {
+                const int q = 2 * st + (g >> 1);
+#pragma unroll
+                for (int t = 0; t < G::TILES; ++t) {
+                    const int off = row_base + t * 8 * 32 - q * 32 + (g & 1) * 16;
+                    const f16x8 A0 = *reinterpret_cast<const f16x8*>(ph + off);
+                    const f16x8 A1 = *reinterpret_cast<const f16x8*>(ph + off + G::PLANE);
+                    hi[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0, B0[r][st], hi[t], 0, 0, 0);
+                    lo[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A0, B1[r][st], lo[t], 0, 0, 0);
+                    lo[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A1, B0[r][st], lo[t], 0, 0, 0);
+                }
+            }
+            if constexpr (G::TAIL) { // separate accumulators, single ds_read_b64 (k_fir_mfma11)
+#pragma unroll
+                for (int t = 0; t < G::TILES; ++t) {
+                    const int off = row_base + t * 8 * 32 - (QH - 1) * 32 + g * 8;
+                    const f16x4 A0 = *reinterpret_cast<const f16x4*>(ph + off);
+                    asm volatile("" ::: "memory");
+                    const f16x4 A1 = *reinterpret_cast<const f16x4*>(ph + off + G::PLANE);
+                    asm volatile("" ::: "memory");
+                    hi_t[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(A0, T0[r], hi_t[t], 0, 0, 0);
+                    lo_t[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(A0, T1[r], lo_t[t], 0, 0, 0);
+                    lo_t[t] = __builtin_amdgcn_mfma_f32_16x16x16f16(A1, T0[r], lo_t[t], 0, 0, 0);
+                }
+            }
+        }
+        nf2 sum[2 * G::TILES];
+#pragma unroll
+        for (int t = 0; t < G::TILES; ++t)
+#pragma unroll
+            for (int half = 0; half < 2; ++half)
+                sum[2 * t + half] = (nf2{ hi[t][2 * half], hi[t][2 * half + 1] } + nf2{ hi_t[t][2 * half], hi_t[t][2 * half + 1] }) +
+                                    (nf2{ lo[t][2 * half], lo[t][2 * half + 1] } + nf2{ lo_t[t][2 * half], lo_t[t][2 * half + 1] });
+        unscale_tile(sum, unscale, o);
+    };
+    auto store_tile = [&](int64_t ch, const nf2 (&o)[2 * G::TILES]) {
+        const __amdgpu_buffer_rsrc_t r = chunk_rsrc<G::CHUNK>(out, ch, n_out);
+#pragma unroll
+        for (int oi = 0; oi < 2 * G::TILES; ++oi)
+            buf_store_f2(r, (wave * G::WAVE_OUT + ((oi >> 1) * 8 + 2 * g + (oi & 1)) * 16 + phase) * 8, o[oi]);
+    };
+    // the workgroup's decision for a chunk from its slot set (SGPRs: scalar branches on it)
+    struct decision {
+        int s;
+        bool ex;
+    };
+    auto decide = [&](int par, int64_t ch) {
+        const unsigned m = __builtin_amdgcn_readfirstlane(
+            max(max(slot_max[4 * par], slot_max[4 * par + 1]), max(slot_max[4 * par + 2], slot_max[4 * par + 3])));
+        const unsigned z = __builtin_amdgcn_readfirstlane(
+            min(min(slot_mnz[4 * par], slot_mnz[4 * par + 1]), min(slot_mnz[4 * par + 2], slot_mnz[4 * par + 3])));
+        const int s = scale_of(m);
+        const bool ex = chunk_needs_exact(m, z, s);
+        if (ex && tid == 0 && ch < nchunks) { // to k_fir_exact13 (a vector atomic and a vector store from one lane)
+            const unsigned k = blockIdx.x % XQ_N;
+            const unsigned i = __hip_atomic_fetch_add(xq + XQ_LINE * k, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (i < (unsigned)subcap)
+                __hip_atomic_store(xq + XQ_E + k * subcap + i, (unsigned)(ch << 1) | (m >= 0x7f800000u ? 1u : 0u),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return decision{ s, ex };
+    };
+
+    // ---- prologue: chunk 0 (+ halo) staged; chunks 1, 2 in flight, chunk 1 reduced
+    float4 va[4], vb[4], vc[4];
+    float4 ha, hb, hc;
+    load13<D, QH>(in, hist_in, L, n_in, chunk_at(0), va, ha);
+    {
+        unsigned m, z;
+        reduce(va, ha, m, z);
+        put_halo(stash + G::HP, ha);
+        if (lane == 0) {
+            slot_max[wave] = m;
+            slot_mnz[wave] = z;
+        }
+    }
+    nsh::lds_barrier();
+    decision d_cur = decide(0, chunk_at(0));
+    if (!d_cur.ex) put_split(lds, stash + G::HP, va, d_cur.s);
+    load13<D, QH>(in, hist_in, L, n_in, chunk_at(1), va, ha);
+    load13<D, QH>(in, hist_in, L, n_in, chunk_at(2), vb, hb);
+    {
+        unsigned m, z;
+        reduce(va, ha, m, z);
+        nsh::lds_barrier(); // slots [0..3] and stash[1] read above
+        put_halo(stash, ha);
+        if (lane == 0) {
+            slot_max[4 + wave] = m;
+            slot_mnz[4 + wave] = z;
+        }
+    }
+    nsh::lds_barrier();
+
+    // step i: chunk i+1 (nxt, its halo in stash[i & 1]) split into the other buffer, chunk i filtered
+    // from this one, chunk i+2 (nn) reduced and its halo stashed, chunk i+3 requested into ld
+    auto step = [&](float4 (&nxt)[4], float4 (&nn)[4], float4& hnn, float4 (&ld)[4], float4& hld, int64_t i) {
+        const int pi = (int)(i & 1), pn = pi ^ 1;
+        const unsigned char* cur = lds + pi * G::BUF;
+        unsigned char* nbuf = lds + pn * G::BUF;
+        const decision d_nxt = decide(pn, chunk_at(i + 1));
+        load13<D, QH>(in, hist_in, L, n_in, chunk_at(i + 3), ld, hld);
+        if (!d_nxt.ex) put_split(nbuf, stash + pi * G::HP, nxt, d_nxt.s);
+        if (!d_cur.ex) {
+            nf2 o[2 * G::TILES];
+            mfma_tile(cur, -(d_cur.s + sh), o);
+            store_tile(chunk_at(i), o);
+        }
+        unsigned m, z;
+        reduce(nn, hnn, m, z);
+        put_halo(stash + pn * G::HP, hnn);
+        if (lane == 0) {
+            slot_max[4 * pi + wave] = m;
+            slot_mnz[4 * pi + wave] = z;
+        }
+        d_cur = d_nxt;
+        nsh::lds_barrier();
+    };
+    int64_t i = 0;
+    for (; i + 2 < n_steps; i += 3) {
+        step(va, vb, hb, vc, hc, i);
+        step(vb, vc, hc, va, ha, i + 1);
+        step(vc, va, ha, vb, hb, i + 2);
+    }
+    if (i < n_steps) step(va, vb, hb, vc, hc, i++);
+    if (i < n_steps) step(vb, vc, hc, va, ha, i);
+}
+
+// The chunks k_fir_mfma13 queued, on the exact forms of k_fir_mfma11: finite -> the exact-fp32 tile
+// (filtered undecimated, every D-th output kept), inf/NaN -> the fp32 direct form. A persistent walk
+// over the queue (NSH_X12_PER_CU workgroups per CU), one chunk per workgroup step; it zeroes the next
+// launch's counters (k_fir_exact12's protocol).
+template <int D, int QH>
+__global__ __launch_bounds__(256) void k_fir_exact13(const float2* __restrict__ in,
+                                                    const float2* __restrict__ hist_in,
+                                                    float2* __restrict__ out,
+                                                    const float4* __restrict__ timg32, // tile taps [4][TWF]
+                                                    const float* __restrict__ taps,
+                                                    const unsigned* __restrict__ xq, // this launch's set
+                                                    unsigned* __restrict__ xq_next,  // the next launch's set
+                                                    int64_t subcap,
+                                                    int L,
+                                                    int64_t n_out)
+{
+    using G = geom11x<D, QH>;
+    using GF = typename G::GF;
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int g = lane >> 4;
+    const int phase = lane & 15;
+    if (blockIdx.x == 0 && tid < 64)
+        __hip_atomic_store(xq_next + XQ_LINE * tid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned incl = __hip_atomic_load(xq + XQ_LINE * lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    incl = min(incl, (unsigned)subcap);
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const unsigned t = __shfl_up(incl, d);
+        if (lane >= d) incl += t;
+    }
+    const unsigned cnt = __builtin_amdgcn_readlane(incl, 63);
+    if (cnt == 0) return; // nothing queued (the common case)
+    auto entry = [&](unsigned i) {
+        const int k = __popcll(__ballot(incl <= i));
+        const unsigned start = k ? __shfl(incl, k - 1) : 0u;
+        return __hip_atomic_load(xq + XQ_E + k * subcap + (i - start), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    {   // the tile's taps, once per workgroup (read after the first chunk's barrier)
+        float4 t32[2];
+        nsh_f32t::load_taps<GF>(timg32, t32, tid, G::NT);
+        nsh_f32t::put_taps_at<GF>(lds + G::TAPF, t32, tid, G::NT);
+    }
+    const int64_t n_in = n_out * D;
+    const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
+    for (unsigned i = blockIdx.x; i < cnt; i += gridDim.x) {
+        const unsigned e = entry(i);
+        const int64_t ch = (int64_t)(e >> 1);
+        if (ch >= nchunks) continue; // never for a queue this launch filled (defensive)
+        const bool f32t = !(e & 1u);
+        float4 v[4], hv;
+        load13<D, QH>(in, hist_in, L, n_in, ch, v, hv);
+        nsh::lds_barrier(); // the previous chunk's reads of LDS are done
+        if (f32t) {
+            if (tid < G::HP) nsh_f32t::put<GF>(lds, hv, 2 * tid);
+#pragma unroll
+            for (int u = 0; u < G::UNITS; ++u)
+#pragma unroll
+                for (int f = 0; f < D; ++f) nsh_f32t::put<GF>(lds, v[u * D + f], GF::H + 2 * ((tid + G::NT * u) * D + f));
+        } else {
+            float4* rb = reinterpret_cast<float4*>(lds);
+            if (tid < G::HP) rb[tid] = hv;
+#pragma unroll
+            for (int u = 0; u < G::UNITS; ++u)
+#pragma unroll
+                for (int f = 0; f < D; ++f) rb[G::HP + (tid + G::NT * u) * D + f] = v[u * D + f];
+        }
+        nsh::lds_barrier();
+        nf2 o[2 * G::TILES];
+        if (f32t) {
+            typedef float f32x4 __attribute__((ext_vector_type(4)));
+            f32x4 acc[4];
+            nsh_f32t::tile_at<GF, G::QF>(lds, lds + G::TAPF, wave, lane, acc);
+            nf2* scr = reinterpret_cast<nf2*>(lds + G::SCR) + wave * G::WAVE_OUT;
+            const int ii = lane & 15;
+            if (ii % D == 0) {
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) scr[(16 * (8 * t + 2 * g + u) + ii) / D] = nf2{ acc[t][2 * u], acc[t][2 * u + 1] };
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int oi = 0; oi < 2 * G::TILES; ++oi) o[oi] = scr[((oi >> 1) * 8 + 2 * g + (oi & 1)) * 16 + phase];
+        } else if constexpr (D == 4 || NSH_DECIM2_SHARED) {
+#pragma unroll 1
+            for (int t = 0; t < G::TILES; ++t) {
+                nf2 acc[2];
+                direct_group<2, 16 * D, D * G::H, D * (G::H - 16)>(
+                    reinterpret_cast<const nf2*>(lds), D * G::H + D * (wave * G::WAVE_OUT + (8 * t + 2 * g) * 16 + phase), taps, L, acc);
+                if (t == 0) {
+                    o[0] = acc[0];
+                    o[1] = acc[1];
+                } else {
+                    o[2 * G::TILES - 2] = acc[0];
+                    o[2 * G::TILES - 1] = acc[1];
+                }
+            }
+        } else {
+            const float2* raw = reinterpret_cast<const float2*>(lds);
+            for (int oi = 0; oi < 2 * G::TILES; ++oi) {
+                const int blk = (oi >> 1) * 8 + 2 * g + (oi & 1);
+                const int j = D * G::H + D * (wave * G::WAVE_OUT + blk * 16 + phase);
+                float re = 0.f, im = 0.f;
+                for (int k = 0; k < L; ++k) {
+                    const float2 x = raw[j - k];
+                    re = fmaf(taps[k], x.x, re);
+                    im = fmaf(taps[k], x.y, im);
+                }
+                o[oi] = nf2{ re, im };
+            }
+        }
+        const __amdgpu_buffer_rsrc_t r = chunk_rsrc<G::CHUNK>(out, ch, n_out);
+#pragma unroll
+        for (int oi = 0; oi < 2 * G::TILES; ++oi)
+            buf_store_f2(r, (wave * G::WAVE_OUT + ((oi >> 1) * 8 + 2 * g + (oi & 1)) * 16 + phase) * 8, o[oi]);
+    }
+}
+
 // The plan's exact queue for stream s: two sets of at least `words` u32 each (stride returned), and
 // the set this launch uses (the stream's launch count & 1). Grown (rare: the first call with more
 // chunks than any before on this stream) after the stream has drained, so no launch still uses the
@@ -901,16 +1311,68 @@ int launch_v11(const nsh_fir_plan* p, const float2* in, const float2* hin, float
     return 0;
 }
 
+// The lockstep walk (k_fir_mfma13 + k_fir_exact13) for decim D, the contiguous walk
+// (k_fir_mfma11, exact forms inline) otherwise: bit D of the plan's dec_walk, set at plan creation
+// from NSH_DEC_WALK_MASK (environment; default below: D = 4 only) -- tests run both walks.
+template <int D, int QH>
+int launch_v13(const nsh_fir_plan* p, const float2* in, const float2* hin, float2* hout, float2* out, int64_t n_out,
+               hipStream_t s)
+{
+    using G = geom11<D, QH>;
+    using GX = geom11x<D, QH>;
+    if (p->QFT != GX::QF) return nsh::fail_msg("nsh_fir_ccf(mfma decim): tile tap image does not match the kernel");
+    NSH_CK(set_lds_attr((const void*)k_fir_mfma13<D, QH>, G::LDS, p->dev));
+    NSH_CK(set_lds_attr((const void*)k_fir_exact13<D, QH>, GX::LDS, p->dev));
+    const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
+    const int n_cu = plan_cus(p);
+    const int W = n_cu * p->walk_wgpc / 8 > 0 ? n_cu * p->walk_wgpc / 8 : 1; // one lockstep row per XCD
+    const int64_t per_x = (nchunks + 7) / 8;
+    const int64_t grid = 8 * (int64_t)W;
+    const int64_t steps = (per_x + W - 1) / W;
+    const int64_t subcap = xq_subcap(grid) * steps; // a sub-queue's workgroups can queue every chunk they walk
+    hipError_t e;
+    int64_t stride = 0;
+    int set = 0;
+    unsigned* xq = exact_queue(p, s, XQ_E + XQ_N * subcap, stride, set, e);
+    if (!xq) return nsh::fail(e, "nsh_fir_ccf(mfma decim): exact queue");
+    unsigned* cur = xq + set * stride;
+    unsigned* nxt = xq + (set ^ 1) * stride;
+    const nsh::launch_events t = nsh::take_launch_events(); // one pair over both kernels
+    nsh::launch_timed((k_fir_mfma13<D, QH>), dim3((unsigned)grid), dim3(G::NT), G::LDS, s, t.start, (hipEvent_t) nullptr, in,
+                      hin, hout, out, (const _Float16*)p->fragd8_dev, cur, subcap, p->L, p->sh8, n_out, per_x);
+    if ((e = hipGetLastError()) != hipSuccess) {
+        xq_reset(p, s);
+        return nsh::fail(e, "nsh_fir_ccf(mfma decim v13)");
+    }
+    const int64_t xcap = (int64_t)n_cu * NSH_X12_PER_CU;
+    nsh::launch_timed((k_fir_exact13<D, QH>), dim3((unsigned)(nchunks < xcap ? nchunks : xcap)), dim3(G::NT), GX::LDS, s,
+                      (hipEvent_t) nullptr, t.stop, in, hin, out, (const float4*)p->tf32q_dev, (const float*)p->taps_dev,
+                      (const unsigned*)cur, nxt, subcap, p->L, n_out);
+    if ((e = hipGetLastError()) != hipSuccess) {
+        xq_reset(p, s);
+        return nsh::fail(e, "nsh_fir_ccf(mfma decim v13 exact chunks)");
+    }
+    return 0;
+}
+
+template <int D, int QH>
+int launch_walk(const nsh_fir_plan* p, const float2* in, const float2* hin, float2* hout, float2* out, int64_t n_out,
+                hipStream_t s)
+{
+    if (p->dec_walk & (1 << D)) return launch_v13<D, QH>(p, in, hin, hout, out, n_out, s);
+    return launch_v11<D, QH>(p, in, hin, hout, out, n_out, s);
+}
+
 template <int D>
 int launch_dec(const nsh_fir_plan* p, const float2* in, const float2* hin, float2* hout, float2* out, int64_t n_out,
                hipStream_t s)
 {
     switch (p->QHD) {
-    case 2: return launch_v11<D, 2>(p, in, hin, hout, out, n_out, s);
-    case 3: return launch_v11<D, 3>(p, in, hin, hout, out, n_out, s);
-    case 4: return launch_v11<D, 4>(p, in, hin, hout, out, n_out, s);
-    case 5: return launch_v11<D, 5>(p, in, hin, hout, out, n_out, s);
-    case 6: return launch_v11<D, 6>(p, in, hin, hout, out, n_out, s);
+    case 2: return launch_walk<D, 2>(p, in, hin, hout, out, n_out, s);
+    case 3: return launch_walk<D, 3>(p, in, hin, hout, out, n_out, s);
+    case 4: return launch_walk<D, 4>(p, in, hin, hout, out, n_out, s);
+    case 5: return launch_walk<D, 5>(p, in, hin, hout, out, n_out, s);
+    case 6: return launch_walk<D, 6>(p, in, hin, hout, out, n_out, s);
     default: return nsh::fail_msg("nsh_fir_ccf(mfma decim): unsupported tap count");
     }
 }
@@ -983,8 +1445,15 @@ static hipError_t f32_tile_image(nsh_fir_plan* p, int QF)
     return e;
 }
 
+#ifndef NSH_DEC_WALK_MASK
+#define NSH_DEC_WALK_MASK 16
+#endif
 int nsh_fir_mfma_prepare_decim(nsh_fir_plan* p)
 {
+    const char* wm = std::getenv("NSH_DEC_WALK_MASK");
+    p->dec_walk = wm && *wm ? std::atoi(wm) : NSH_DEC_WALK_MASK;
+    const char* wg = std::getenv("NSH_WALK_WGPC"); // probes: resident workgroups per CU of the walk
+    p->walk_wgpc = wg && std::atoi(wg) >= 1 && std::atoi(wg) <= 4 ? std::atoi(wg) : 2;
     // polyphase taps h'_0[j] = h[D j], h'_r[j] = h[D (j - 1) + r] (r >= 1, j >= 1)
     const int D = p->D, QH = decim_qh(p), KS = QH / 2;
     const bool tail = QH % 2;
@@ -1079,7 +1548,7 @@ std::string nsh_fir_mfma_kernel_name(const nsh_fir_plan* p)
     auto t = [](const char* k, int a, int b = -1) {
         return std::string(k) + "<" + std::to_string(a) + (b >= 0 ? "," + std::to_string(b) : std::string()) + ">";
     };
-    if (p->D > 1) return t("k_fir_mfma11", p->D, p->QHD);
+    if (p->D > 1) return t((p->dec_walk & (1 << p->D)) ? "k_fir_mfma13" : "k_fir_mfma11", p->D, p->QHD);
     return t("k_fir_mfma12", p->Q);
 }
 

@@ -42,6 +42,8 @@ struct nsh_fir_plan {
     mutable std::mutex xq_mu;
     mutable std::vector<xqueue> xq;
     void* casc = nullptr; // NSH_FIR_PFFT: a one-stage nsh_fir_cascade plan (k_fir_pfft)
+    int dec_walk = 0;     // decim 2 / 4: bit D set = the lockstep walk (k_fir_mfma13), else k_fir_mfma11
+    int walk_wgpc = 2;    // k_fir_mfma13: workgroups per CU (the lockstep row is 8 x n_cu x this / 8 wide)
     int n_cu = 0;         // the device's CU count, queried once (0 = not yet)
     std::string kernel;   // the kernel nsh_fir_ccf launches (rocprof name without namespace)
 };

@@ -249,16 +249,19 @@ def test_fir_decim_vs_oracle(torch_cuda, decim):
         np.testing.assert_array_equal(hout, h_ref)
 
 
-@pytest.fixture
-def dec_form():
-    """The polyphase MFMA kernel: k_fir_mfma11 (fp16x2, per-chunk scale, exact path)."""
-    return "v11"
+@pytest.fixture(params=["v11", "v13"])
+def dec_form(request, monkeypatch):
+    """The polyphase MFMA kernels (fp16x2, per-chunk scale, exact forms): k_fir_mfma11 (contiguous
+    walk, exact chunks inline) and k_fir_mfma13 (lockstep walk per XCD, exact chunks queued for
+    k_fir_exact13), chosen at plan creation by NSH_DEC_WALK_MASK (bit D)."""
+    monkeypatch.setenv("NSH_DEC_WALK_MASK", "0" if request.param == "v11" else "20")
+    return request.param
 
 
 def _dec_plan(h, decim, form):
     plan = nsh.FirPlan(h, decim, nsh.FIR_MFMA)
     assert plan.algo == nsh.FIR_MFMA
-    want = "k_fir_mfma11<" if form == "v11" else "k_fir_mfma7<"
+    want = {"v11": "k_fir_mfma11<", "v13": "k_fir_mfma13<"}[form]
     assert plan.kernel.startswith(want), plan.kernel
     return plan
 
@@ -301,9 +304,8 @@ def test_fir_decim_mfma_edge_values(torch_cuda, dec_form, decim):
     seg = len(x) // 4
     x[:seg] *= np.float32(1e-30)
     x[3 * seg:] *= np.float32(1e30)
-    if dec_form == "v11":  # the bf16x3 form has no exact path: finite inputs only
-        x[seg + 5000] = np.complex64(complex(np.inf, 0.5))
-        x[seg + 9000] = np.complex64(complex(np.nan, 0.0))
+    x[seg + 5000] = np.complex64(complex(np.inf, 0.5))
+    x[seg + 9000] = np.complex64(complex(np.nan, 0.0))
     x[2 * seg + 100] *= np.float32(2.0 ** 60)
     x[2 * seg + 6000:2 * seg + 10_000] = 0
     x[2 * seg + 12_000] = np.complex64(complex(1e-40, 0.0))
@@ -317,6 +319,72 @@ def test_fir_decim_mfma_edge_values(torch_cuda, dec_form, decim):
     for a, b in regions:
         ok, err, scale = orc.tol_ok(y[a:b], ref[a:b])
         assert ok, (decim, a, b, err, scale)
+
+
+@pytest.mark.parametrize("decim", [2, 4])
+@pytest.mark.parametrize("period", [1, 3, 64])
+def test_fir_decim_mfma_periodic_exact_chunks(torch_cuda, dec_form, decim, period):
+    """Every period-th 2048-input chunk holds a 2^40 spike (its range is beyond the fp16x2 split:
+    the exact-fp32 tile), every (period+1)-th a NaN, over 2^20 + 37 inputs, called twice on one
+    stream with the history handed on (k_fir_mfma13's exact queue alternates its two counter sets
+    per call). The NaN pattern equals the oracle's; every chunk's finite outputs meet the tolerance
+    on that chunk's own scale."""
+    torch = torch_cuda
+    h = _firwin127()
+    n = (1 << 20) + 37 * decim
+    x = orc.synth(n, 77 + period)
+    x[100::2048 * period] *= np.float32(2.0 ** 40)
+    x[1500::2048 * (period + 1)] = complex(np.nan, 0.25)
+    plan = _dec_plan(h, decim, dec_form)
+    half = (n // decim // 2) * decim
+    y1, hy = run_fir(torch, plan, x[:half], half // decim)
+    y2, _ = run_fir(torch, plan, x[half:], (n - half) // decim, hist=hy)
+    y = np.concatenate([y1, y2])
+    ref = orc.fir_ccf(x[: n // decim * decim], h, decim)
+    _assert_nonfinite_pattern(y, ref)
+    c = 2048 // decim
+    for a in range(0, y.size, c):
+        yy, rr = y[a:a + c], ref[a:a + c]
+        fin = np.isfinite(rr.real) & np.isfinite(rr.imag)
+        if fin.any():
+            ok, err, scale = orc.tol_ok(yy[fin], rr[fin])
+            assert ok, (a, err, scale)
+
+
+def test_fir_decim4_walks_agree_full_stream(torch_cuda, monkeypatch):
+    """D = 4 over 2^26 inputs: the lockstep walk (k_fir_mfma13) and the contiguous walk
+    (k_fir_mfma11) within the split's rounding of each other everywhere, and the lockstep walk
+    against the oracle on windows at XCD-range and chunk boundaries."""
+    torch = torch_cuda
+    h = _firwin127()
+    n_in = 1 << 26
+    n_out = n_in // 4
+    dx = torch.empty(n_in, dtype=torch.complex64, device="cuda")
+    nsh.synth(dx, n_in, 0)
+    ys = {}
+    for form, mask in (("v11", "0"), ("v13", "16")):
+        monkeypatch.setenv("NSH_DEC_WALK_MASK", mask)
+        plan = _dec_plan(h, 4, form)
+        hout = torch.zeros(126, dtype=torch.complex64, device="cuda")
+        y = torch.empty(n_out, dtype=torch.complex64, device="cuda")
+        plan(dx, 0, hout, y, n_out)
+        ys[form] = y
+        plan.close()
+    torch.cuda.synchronize()
+    d = (ys["v11"] - ys["v13"]).abs().max().item()
+    scale = ys["v11"].abs().max().item()
+    assert d <= 1e-6 * scale, (d, scale)
+    del dx
+    chunks = n_out // 512
+    per_x = (chunks + 7) // 8
+    for o in (0, 512 * per_x - 300, 512 * 3 * per_x + 7, n_out - 1000):
+        o = max(0, min(o, n_out - 1000))
+        lo = 4 * o - 126
+        xw = orc.synth(4 * 1000 + 126, max(lo, 0)) if lo >= 0 else np.concatenate(
+            [np.zeros(-lo, np.complex64), orc.synth(4 * 1000 + 126 + lo, 0)])
+        ref = orc.fir_ccf(xw[126:], h, 4, hist=xw[:126])
+        ok, err, scale = orc.tol_ok(ys["v13"][o:o + 1000].cpu().numpy(), ref)
+        assert ok, (o, err, scale)
 
 
 def test_fir_decim2_golden_chain(torch_cuda, golden):
@@ -507,7 +575,7 @@ def test_fir_mfma_exact_paths(torch_cuda, v8_form, ntaps, decim, kind):
     plan = nsh.FirPlan(h, decim, nsh.FIR_MFMA)
     if ntaps == 127:
         assert plan.kernel.startswith({1: "k_fir_mfma12",
-                                       2: "k_fir_mfma11", 4: "k_fir_mfma11"}[decim]), plan.kernel
+                                       2: "k_fir_mfma11", 4: "k_fir_mfma13"}[decim]), plan.kernel
     y, hy = run_fir(torch, plan, x, n // decim)
     yd, hd = run_fir(torch, nsh.FirPlan(h, decim, nsh.FIR_DIRECT), x, n // decim)
     np.testing.assert_array_equal(hy.view(np.uint32), hd.view(np.uint32))
