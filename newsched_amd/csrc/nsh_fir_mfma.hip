@@ -830,6 +830,9 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma11(const float2* __restrict_
 }
 
 // ---- k_fir_mfma13: the decimators' lockstep walk, exact chunks queued (round 5) ------------
+#ifndef NSH_V13_XWIN
+#define NSH_V13_XWIN 0
+#endif
 // k_fir_mfma11's per-chunk work (polyphase split at a per-chunk scale, the same MFMA tile) in a
 // different walk: the persistent workgroups of an XCD (x = blockIdx mod 8, W of them) take its
 // eighth of the chunks in lockstep -- at step i workgroup k of XCD x filters chunk
@@ -912,13 +915,19 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma13(const float2* __restrict_
 
     const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
     const int W = (int)(gridDim.x >> 3);
+#if NSH_V13_XWIN
+    // probe form: one global lockstep row -- at step i XCD x takes window 8 i + x of W chunks
+    const int64_t xe = nchunks, c_first = (int64_t)(blockIdx.x & 7) * W + (blockIdx.x >> 3), hop = 8 * (int64_t)W;
+    (void)per_x;
+#else
     const int64_t xb = (int64_t)(blockIdx.x & 7) * per_x;
     const int64_t xe = xb + per_x < nchunks ? xb + per_x : nchunks;
-    const int64_t c_first = xb + (blockIdx.x >> 3);
+    const int64_t c_first = xb + (blockIdx.x >> 3), hop = W;
+#endif
     if (c_first >= xe) return; // whole workgroup, before any barrier
-    // the workgroup's i-th chunk; past its XCD's range an empty buffer range (loads return 0)
-    auto chunk_at = [&](int64_t i) { const int64_t c = c_first + i * W; return c < xe ? c : nchunks; };
-    const int64_t n_steps = (xe - c_first + W - 1) / W;
+    // the workgroup's i-th chunk; past its range an empty buffer range (loads return 0)
+    auto chunk_at = [&](int64_t i) { const int64_t c = c_first + i * hop; return c < xe ? c : nchunks; };
+    const int64_t n_steps = (xe - c_first + hop - 1) / hop;
 
     f16x8 B0[D][KS + 1], B1[D][KS + 1];
     f16x4 T0[D], T1[D];
