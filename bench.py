@@ -247,6 +247,20 @@ def run_c5(a, dist, backend, rank, world, device, torch, orc, nsr):
     return res
 
 
+def leg_clock(work, nsh, real_ms=8.0):
+    """The shader clock while `work` (untimed repeats of a leg, >= real_ms long) runs: a one-wave
+    sampler on a side stream (nsh_clock_sample: SQ cycles over the 100 MHz real-time counter),
+    MI355X_MICROARCH.md's DVFS give-back read in-process (tools/pmc_clock.sh measures the same with
+    GRBM_GUI_ACTIVE). None if it could not be taken."""
+    try:
+        cs = nsh.ClockSampler(real_ms)
+        cs.start()
+        work()
+        return round(cs.mhz(), 1)
+    except Exception:  # a measurement aid, never fatal to the line
+        return None
+
+
 def run_fp32_leg(a, n, taps, first, device, barrier, dist, tdev, torch, orc, nsr, nsh):
     """The same C3 flowgraph with the exact-fp32 matrix form (NSH_FIR_MFMA_F32: no operand
     split, fp32 products and sums) -- what the ceiling is without split precision."""
@@ -271,6 +285,7 @@ def run_fp32_leg(a, n, taps, first, device, barrier, dist, tdev, torch, orc, nsr
     launches = st["launches"] - l0
     kms, samples = st["kernel_ms"] - st0["kernel_ms"], st["samples"] - st0["samples"]
     avg_ms = kms / launches
+    mhz = leg_clock(lambda: [fb.run() for _ in range(10)], nsh)
     m = 4096
     y = fb.tail(m)
     lo = first + n - m - (taps.size - 1)
@@ -281,7 +296,7 @@ def run_fp32_leg(a, n, taps, first, device, barrier, dist, tdev, torch, orc, nsr
     world = dist.get_world_size() if dist is not None else 1
     return {"kernel": st["kernel"], "steps": steps, "value": round(world * n * steps / el / 1e6, 1), "unit": "MSamples/s",
             "avg_launch_us": round(avg_ms * 1e3, 2), "achieved_GBs": round(achieved, 1),
-            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "clock_mhz": mhz,
             "parity": {"max_abs_err": err, "ok": bool(ok)}}
 
 
@@ -355,6 +370,14 @@ def run_c5_fused_leg(a, first, device, barrier, dist, tdev, torch, orc, nsh):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     avg_ms = sum(e0.elapsed_time(e1) for e0, e1 in ev) / steps
+
+    def more():
+        with torch.cuda.stream(s):
+            for _ in range(24):
+                plan(x, hist, hout, y, n_out, stream=s)
+        s.synchronize()
+
+    mhz = leg_clock(more, nsh)
     m = 4096
     lo = first + n - 16 * m - C5_HALO
     xr = orc.synth(16 * m + C5_HALO, lo)
@@ -368,7 +391,7 @@ def run_c5_fused_leg(a, first, device, barrier, dist, tdev, torch, orc, nsh):
             "fir_filter_cascade_ccf, 2^%d resident input samples per GPU" % a.c5_fused_log2n,
             "steps": steps, "value": round(world * n * steps / el / 1e6, 1), "unit": "MSamples/s (input)",
             "avg_launch_us": round(avg_ms * 1e3, 2), "achieved_GBs": round(achieved, 1),
-            "bytes_per_input_sample": 8.5, "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "bytes_per_input_sample": 8.5, "frac": round(achieved / HBM_PEAK_GBS, 4), "clock_mhz": mhz,
             "parity": {"check": "last 4096 outputs vs the oracle's 4-stage chain (double accumulation)",
                        "max_abs_err": err, "ok": bool(ok)}}
 
@@ -482,6 +505,12 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     st = fb.stats()
+
+    def more():  # untimed: the clock the FIR runs at under the same stream of batches
+        fb.set_batches(24)
+        fb.run()
+
+    clock_mhz = leg_clock(more, nsh)
     kms = st["kernel_ms"] - st0["kernel_ms"]
     samples = st["samples"] - st0["samples"]
     algo_used = {1: "direct", 2: "mfma", 5: "mfma_f32"}.get(st["algo"], str(st["algo"]))
@@ -548,6 +577,7 @@ def main():
             "flowgraph_achieved": round(BYTES_PER_SAMPLE * n / (step_us * 1e-6) / 1e9, 1),
             "flowgraph_frac": round(BYTES_PER_SAMPLE * n / (step_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
             "overhead_us_per_step": round(step_us - avg_launch_ms * 1e3 * launches_per_run, 2),  # incl. the run's start / drain
+            "clock_mhz": clock_mhz,  # shader clock over an untimed repeat (leg_clock)
         },
         "parity": {"check": "last 4096 outputs of the last step vs oracle (double accumulation), every rank",
                    "max_abs_err": err, "scale": scale, "ok": bool(ok)},

@@ -74,6 +74,13 @@ int nsh_stream_wait_event(void* stream, void* event);
  * the per-work() cudaEventRecord pairs a CUDA block would use for kernel timing (the reference
  * blocks do not time their kernels). */
 int nsh_time_next_launch(void* start_event, void* stop_event);
+/* The shader clock while other work runs: one wave on `stream` (meant to be a second stream beside
+ * the measured kernel's) reads the SQ cycle counter and the 100 MHz real-time counter, sleeps for
+ * real_ticks (<= 2^32) ticks of the latter, reads both again and writes {cycles, ticks} to out_dev
+ * (2 x uint64, device memory): MHz = 100 * cycles / ticks. The wave's end is bounded by the real-
+ * time counter and by an iteration cap. A measurement helper (bench.py records the clock each
+ * timed leg ran at); no reference counterpart. */
+int nsh_clock_sample(void* out_dev, int64_t real_ticks, void* stream);
 
 /* ---- memory ----------------------------------------------------------------------- */
 enum nsh_copy_kind { NSH_H2D = 0, NSH_D2H = 1, NSH_D2D = 2, NSH_DEFAULT = 3 };

@@ -47,6 +47,7 @@
 #include "nsh_cplx.hpp"
 
 #include <cmath>
+#include <cstdlib>
 #include <mutex>
 #include <set>
 #include <string>
@@ -140,12 +141,12 @@ struct img_bases {
     cf* b2;
     cf* n;
 };
-__device__ __forceinline__ img_bases bases_of(cf* img)
+__device__ __forceinline__ img_bases bases_of(cf* img, int j)
 {
-    const int j = threadIdx.x & 63;
     return img_bases{ img + 8 * j + (j >> 1), img + j + (j >> 4), img + 72 * (j >> 3) + (j & 7), img + j + 3 * (j >> 5),
                       img + j };
 }
+__device__ __forceinline__ img_bases bases_of(cf* img) { return bases_of(img, threadIdx.x & 63); }
 
 #ifndef NSH_PFFT_REGX2
 #define NSH_PFFT_REGX2 0
@@ -619,6 +620,369 @@ __global__ __launch_bounds__(64 * P / PW, 1) void k_fir_pfft(pfft_args a)
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// ---- k_fir_pfft2: the P = 16 frame without a ring, phase images double-buffered (round 5) ----
+//
+// Opt-in (NSH_PFFT_FORM=2 at plan creation; tests run both forms). The form above spends a quarter
+// of each frame in phase B (the phase sum and the ring stores, between its two barriers) with the
+// VALU idle, and a second product set to overlap it with the next frame's transforms does not fit
+// next to the 64 KiB ring. This form drops the ring: each lane loads its rows straight from HBM in
+// 16-B loads and a half-wave swap regroups them the way Stockham's first pass wants (lane l of wave
+// w ends with one phase at window rows 4 w + g + 64 r, r = 0..7; load_frame), runs pass 1 in
+// registers and stores its outputs into that phase's image: exchange 1 becomes the cross-wave
+// row -> phase transpose the ring did. The Q overlap rows a frame shares with the previous one are
+// loaded again (mostly L2 hits: 9.04 vs 8.65 HBM B per input sample, PMC r05o). With the ring gone,
+// two sets of 16 phase images fit (frame f in set f & 1), and the frame pipelines:
+//   top: request frame f + 1's rows (16 VGPRs in flight through the frame)
+//   A0:  frame f's pass-1 outputs (computed at the end of the previous A) -> set s
+//   B1
+//   A:   the inverse of frame f - 2 (one of waves 0..3, own image); every wave: pass 2, exchange 2,
+//        pass 3, times F_p, products into its image of set s; waves 8..15: the phase sum of frame
+//        f - 1 (set s ^ 1) into Z[(f - 1) & 1]; every wave: frame f + 1's rows -> wave max ->
+//        half-wave swap -> pass 1, kept in registers
+//   B2
+// Measured (profiles/r05g-r05o, one process against k_fir_pfft): correct (the pfft suite on both
+// forms), 32 % fewer LDS-active cycles and no bank conflicts, the same VALU and load counts -- and
+// 0-11 % slower: without its row loads it runs 519 us per 2^28 inputs (k_fir_pfft without its
+// loads ~525), its loads then cost ~110 us against ~45 for k_fir_pfft's, the wave's vector-memory
+// issue busy twice as long per load instruction. Two earlier shapes lost more: 8-B loads (128 load
+// instructions per frame held the late waves 2-4k cycles at issue) and a load path whose register
+// copies waited for the loads right after issuing them.
+// Scaling: the frame's maximum is known only after B1 (each wave sees its own rows), so pass 1 runs
+// unscaled and the 2^k scale multiplies its outputs -- exact, and pass 1 cannot overflow or lose
+// precision to subnormals for frames whose maximum lies in [2^-100, 2^124); a frame outside that
+// range (finite, nonzero) reloads its rows, scales them, redoes pass 1 and takes one more barrier.
+// A frame holding inf/NaN runs the staged chain (or the one-stage direct form) as in k_fir_pfft,
+// reading its window from HBM.
+constexpr int IMG2 = 571; // odd: a 16-lane group's exchange-1 stores (16 phases, one position) hit 16 bank pairs
+
+// timing-only ablation hooks for tools/probe (0 in every product build): 1 = each row-load
+// instruction reads one contiguous 1 KiB, 2 = no row loads
+#ifndef NSH_PFFT2_ABLATE
+#define NSH_PFFT2_ABLATE 0
+#endif
+#ifndef NSH_PFFT2_LD_AUX
+#define NSH_PFFT2_LD_AUX 0 // row loads: default policy (the overlap rows are read again by the next frame)
+#endif
+
+// Frame f's window, x[P (f V - Q) + i], i < P M, in 16-B loads: lane l = 32 h + q of wave w loads
+// phases 2 m, 2 m + 1 (m = q & 7) of rows n = 4 w + g + 64 (4 h + k), k = 0..3, g = 2 ((q >> 3) & 1)
+// + (q >> 4) -- each load instruction reads two 512-B runs of 4 whole rows -- into v[k] (phase 2 m)
+// and v[4 + k] (phase 2 m + 1); swap_halves then leaves lane l with phase pp = 2 m + h at rows
+// 4 w + g + 64 r, r = 0..7 (Stockham's pass-1 input at position jp = 4 w + g).
+__device__ __forceinline__ int row_of_lane(int w, int l)
+{
+    const int q = l & 31;
+    return 4 * w + 2 * ((q >> 3) & 1) + (q >> 4) + 256 * (l >> 5);
+}
+template <int P>
+__device__ __forceinline__ void load_frame(cf (&v)[8], const pfft_args& a, int64_t n_in, int64_t f, int w, int j)
+{
+    const int64_t b = (int64_t)P * (f * a.V - a.Q);
+    const int e0 = P * row_of_lane(w, j) + 2 * (j & 7); // element of load k = 0 (loads k: + 64 P k)
+    if (b >= 0) {
+        const __amdgpu_buffer_rsrc_t r = span_rsrc(a.x + b, n_in - b, (int64_t)P * M);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const nsh::buf_f4 t = __builtin_bit_cast(
+                nsh::buf_f4, __builtin_amdgcn_raw_buffer_load_b128(r, (e0 + 64 * P * k) * 8, 0, NSH_PFFT2_LD_AUX));
+            v[k] = cf{ t.x, t.y };
+            v[4 + k] = cf{ t.z, t.w };
+        }
+    } else { // the stream's first frame: history, then zeros before it
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float2 u0 = virt(a.x, a.hist_in, b + e0 + 64 * P * k, n_in, a.L);
+            const float2 u1 = virt(a.x, a.hist_in, b + e0 + 64 * P * k + 1, n_in, a.L);
+            v[k] = cf{ u0.x, u0.y };
+            v[4 + k] = cf{ u1.x, u1.y };
+        }
+    }
+}
+// Frame f >= 1 (no history: f V - Q >= V - Q > 0) as raw 16-B loads into x, branch-free: the
+// loads of the next frame are issued at the top of a phase A and consumed at its end, and any
+// register copy between them would wait for them (a branchy load, joined by copies, did: every
+// wave stalled for the HBM round trip right after its loads). live = false: no bytes (reads 0).
+template <int P>
+__device__ __forceinline__ void load_rows16(nsh::buf_f4 (&x)[4], const pfft_args& a, int64_t n_in, int64_t f, bool live,
+                                            int e0)
+{
+    const int64_t b = (int64_t)P * (f * a.V - a.Q);
+    const __amdgpu_buffer_rsrc_t r = span_rsrc(a.x + b, live ? n_in - b : 0, (int64_t)P * M);
+#if NSH_PFFT2_ABLATE & 2 // timing only: no row loads
+    (void)r;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) x[k] = nsh::buf_f4{ (float)k, 1.f, 2.f, (float)e0 };
+#else
+#if NSH_PFFT2_ABLATE & 1 // timing only: each load instruction one contiguous 1 KiB (wrong rows)
+    e0 = 2 * (threadIdx.x & 63) + 128 * (threadIdx.x >> 6);
+#endif
+#pragma unroll
+    for (int k = 0; k < 4; ++k) // one address VGPR: the load's distance in the scalar offset
+        x[k] = __builtin_bit_cast(nsh::buf_f4,
+                                  __builtin_amdgcn_raw_buffer_load_b128(r, e0 * 8, 512 * P * k, NSH_PFFT2_LD_AUX));
+#endif
+}
+__device__ __forceinline__ void unpack_rows(cf (&v)[8], const nsh::buf_f4 (&x)[4])
+{
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        v[k] = cf{ x[k].x, x[k].y };
+        v[4 + k] = cf{ x[k].z, x[k].w };
+    }
+}
+// lanes l < 32 keep phase 2 m (rows r = 0..3 theirs, 4..7 from lane l + 32), lanes l >= 32 keep
+// phase 2 m + 1 (rows 0..3 from lane l - 32, 4..7 theirs): v[k] <-> v[4 + k] across the halves
+__device__ __forceinline__ void swap_halves(cf (&v)[8])
+{
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const auto x = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[k].x), __float_as_uint(v[4 + k].x), false, false);
+        const auto y = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[k].y), __float_as_uint(v[4 + k].y), false, false);
+        v[k] = cf{ __uint_as_float(x[0]), __uint_as_float(y[0]) };
+        v[4 + k] = cf{ __uint_as_float(x[1]), __uint_as_float(y[1]) };
+    }
+}
+
+__device__ __forceinline__ unsigned maxbits8(const cf (&v)[8])
+{
+    unsigned m = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) m = max(m, max(absbits(v[k].x), absbits(v[k].y)));
+    return m;
+}
+
+template <int P>
+__global__ __launch_bounds__(64 * P, 1) void k_fir_pfft2(pfft_args a)
+{
+    static_assert(P == 16, "the ring-less form is built for 16 phases (16 waves)");
+    constexpr int NT = 64 * P, SET = P * IMG2;
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    cf* sets = reinterpret_cast<cf*>(lds);              // [2][P][IMG2] phase images, frame f in set f & 1
+    cf* zb = sets + 2 * SET;                             // [2][M] conj(Z), frame f in f & 1
+    cf* iimg = zb + 2 * M;                               // [IMG2] the inverse wave's exchange image
+    unsigned* mx = reinterpret_cast<unsigned*>(iimg + IMG2 + 1); // [2][P] per-wave max bits of the frame's rows
+
+    const int tid = threadIdx.x, j = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int64_t f0 = (int64_t)blockIdx.x * a.fpw;
+    const int64_t f1 = min(a.nf, f0 + a.fpw);
+    if (f0 >= f1) return; // whole workgroup
+    const int64_t n_in = a.n_out * P;
+    const int L = a.L, Q = a.Q, V = a.V;
+    // pass 1: phase pp at Stockham position jp (= 4 w + g); its outputs go to image pp at 8 jp + r
+    const int pp = 2 * (j & 7) + (j >> 5), jp = row_of_lane(w, j) & 63;
+    const int e0 = P * row_of_lane(w, j) + 2 * (j & 7); // this lane's first element of a window
+    const int e1off = pp * IMG2 + 8 * jp + (jp >> 1);
+
+    if (a.hist_out && blockIdx.x == gridDim.x - 1) // the next call's history: the L-1 samples before x[n_in]
+        for (int k = tid; k < L - 1; k += NT) a.hist_out[k] = virt(a.x, a.hist_in, n_in - (L - 1) + k, n_in, L);
+
+    cf t2[8], t3[8], fw[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        const float2 u = a.tw[8 * (((j & 7) * r) & 63)], v = a.tw[(j * r) & (M - 1)];
+        t2[r] = cf{ u.x, u.y };
+        t3[r] = cf{ v.x, v.y };
+        const float2 fv = a.F[w * M + j + 64 * r];
+        fw[r] = cf{ fv.x, fv.y };
+    }
+
+    // the inverse of frame fi (conj(Z) in zb[fi & 1]) by this wave, its exchanges in iimg
+    // (the lane's addresses of the inverse and the phase sum are recomputed from an opaque copy of
+    // the lane id each time: hoisted out of the frame loop they would hold VGPRs the transform needs)
+    auto inverse = [&](int64_t fi, int ksi) {
+        int jj = j;
+        asm volatile("" : "+v"(jj));
+        cf v[1][8];
+        const cf* z = zb + (int)(fi & 1) * M + jj;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) v[0][r] = z[64 * r];
+        fft512_multi<1>(v, bases_of(iimg, jj), t2, t3);
+        const int64_t rowi = fi * V;
+        const __amdgpu_buffer_rsrc_t ro = span_rsrc(a.out + rowi, a.n_out - rowi, V);
+        const float us = __uint_as_float((unsigned)(127 - ksi) << 23);
+        const cf u2 = cf{ us, -us }; // 2^-k and the output conjugation
+        const int ob = (jj - Q) * 8;
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+            if (jj + 64 * r >= Q) nsh::buf_store_f2(ro, ob + 512 * r, v[0][r] * u2);
+    };
+    // the phase sum of frame fi (products in set fi & 1) into zb[fi & 1], by waves 8..15, in a fixed
+    // order (deterministic)
+    auto phase_sum = [&](int64_t fi) {
+        int k = tid - NT / 2;
+        asm volatile("" : "+v"(k));
+        const cf* src = sets + (int)(fi & 1) * SET + k;
+        cf zz = cf{ 0.f, 0.f };
+#pragma unroll
+        for (int h = 0; h < P; h += 8) { // eight loads in flight at a time (register budget), summed in order
+            cf pv[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                pv[q] = src[(h + q) * IMG2];
+                asm volatile("" ::: "memory"); // single ds_read_b64 each (paired reads run at half rate)
+            }
+#pragma unroll
+            for (int q = 0; q < 8; ++q) zz = (h + q == 0) ? pv[0] : zz + pv[q];
+        }
+        zb[(int)(fi & 1) * M + k] = cf{ zz.x, -zz.y }; // conj: the inverse runs as a forward transform
+    };
+
+    // v: the next frame's rows, loaded during the current frame's phase A, then its pass 1
+    cf v[8];
+    auto pass1_of = [&](int64_t fn) { // rows of frame fn in v -> its wave max in mx[fn & 1], pass 1 in v
+        const unsigned m = nsh::wave_umax(maxbits8(v));
+        if (j == 0) mx[(int)(fn & 1) * P + w] = m;
+        swap_halves(v);
+        dft8<false>(v);
+    };
+    load_frame<P>(v, a, n_in, f0, w, j);
+    pass1_of(f0);
+    // the pipeline: in frame f's phase A, the phase sum of frame f - 1 and the inverse of frame f - 2
+    bool sum1 = false, inv2 = false; // owed: the phase sum of f - 1, the inverse of f - 2
+    int ks1 = 0, ks2 = 0;            // their scales
+
+    for (int64_t f = f0; f < f1; ++f) {
+        const int s = (int)(f & 1);
+        cf* cur = sets + s * SET;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) asm volatile("" : "+v"(fw[r]));
+#pragma unroll
+        for (int r = 1; r < 8; ++r) asm volatile("" : "+v"(t2[r]), "+v"(t3[r]));
+        PFFT_T(0);
+        // the next frame's rows, requested here and consumed at the end of this frame's phase A:
+        // ~1.7 us of HBM latency under this load (phase trace), most of a frame
+        nsh::buf_f4 nx[4];
+        load_rows16<P>(nx, a, n_in, f + 1, f + 1 < f1, e0);
+        // A0: frame f's pass-1 outputs (computed at the end of the previous phase A) into set s
+#pragma unroll
+        for (int r = 0; r < 8; ++r) cur[e1off + r] = v[r];
+        PFFT_T(1);
+        nsh::lds_barrier(); // B1: exchange 1 of frame f complete
+        PFFT_T(2);
+
+        const unsigned wm = nsh::wave_umax(j < P ? mx[s * P + j] : 0u);
+        const bool bad = wm >= 0x7f800000u; // inf or NaN in the window
+        int ks = 127 - (int)(wm >> 23);
+        ks = ks > 126 ? 126 : (ks < -126 ? -126 : ks);
+        const bool scale = ks < -40 || ks > 40;
+        if (!scale) ks = 0;
+        const float sc = __uint_as_float((unsigned)(ks + 127) << 23);
+        // pass 1 unscaled is safe for maxima in [2^-100, 2^124); outside it, redo pass 1 on scaled rows
+        const bool redo = !bad && (wm >= (251u << 23) || (wm != 0u && wm < (27u << 23)));
+        if (redo) { // workgroup-uniform
+            cf u[8];
+            load_frame<P>(u, a, n_in, f, w, j);
+            swap_halves(u);
+#pragma unroll
+            for (int r = 0; r < 8; ++r) u[r] *= sc;
+            dft8<false>(u);
+#pragma unroll
+            for (int r = 0; r < 8; ++r) cur[e1off + r] = u[r]; // no wave has read set s since B1
+            nsh::lds_barrier();
+        }
+
+        // A: the inverse of frame f - 2 (one of waves 0..3, rotating over the SIMDs), phase w of
+        // frame f, then the phase sum of frame f - 1 (waves 8..15; set s ^ 1 is rewritten only by
+        // frame f + 1's pass 1, after B2)
+        if (inv2 && w == (int)((f - 2) & 3)) inverse(f - 2, ks2);
+        PFFT_T(3);
+        const int64_t rowf = f * V;
+        if (!bad) {
+            const img_bases ib = bases_of(cur + w * IMG2);
+            cf u[8];
+#pragma unroll
+            for (int r = 0; r < 8; ++r) u[r] = ib.b1[68 * r];
+            if (scale && !redo) {
+#pragma unroll
+                for (int r = 0; r < 8; ++r) u[r] *= sc;
+            }
+#pragma unroll
+            for (int r = 1; r < 8; ++r) u[r] = cmul_tw(u[r], t2[r]);
+            dft8<false>(u); // pass 2 -> dst[(j >> 3) 64 + (j & 7) + 8 r]
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int r = 0; r < 8; ++r) ib.x2[8 * r + (r >= 4 ? 3 : 0)] = u[r];
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int r = 0; r < 8; ++r) u[r] = ib.b2[72 * r];
+#pragma unroll
+            for (int r = 1; r < 8; ++r) u[r] = cmul_tw(u[r], t3[r]);
+            dft8<false>(u); // pass 3 -> X[j + 64 r]
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int r = 0; r < 8; ++r) ib.n[64 * r] = cmul_tw(u[r], fw[r]);
+        } else if (a.nst < 2) {
+            // one stage: the fp32 direct form on its taps (heq = h) over the window in HBM
+            const int64_t wb = (int64_t)P * (rowf - Q);
+            for (int t = tid; t < V; t += NT) {
+                const int q = Q + t;
+                cf acc = cf{ 0.f, 0.f };
+                for (int n = 0; n < L; ++n) {
+                    const float2 x = virt(a.x, a.hist_in, wb + P * q - n, n_in, L);
+                    acc = __builtin_elementwise_fma(cf{ a.heq[n], a.heq[n] }, cf{ x.x, x.y }, acc);
+                }
+                if (rowf + t < a.n_out) a.out[rowf + t] = make_float2(acc.x, acc.y);
+            }
+        } else {
+            // the staged chain, stage by stage in the fp32 direct form (as k_fir_pfft), its window
+            // read from HBM, stage outputs ping-ponging between two buffers in set s
+            const int64_t wb = (int64_t)P * (rowf - Q);
+            cf* buf[2] = { cur, cur + a.n1 };
+            const float* hs = a.stap;
+            int n_prev = P * M;
+            for (int st = 0; st < a.nst; ++st) {
+                const int Ds = a.sd[st], Ls = a.sl[st];
+                const int n_cur = (n_prev - 1) / Ds + 1;
+                const cf* src = buf[(st + 1) & 1];
+                cf* dst = buf[st & 1];
+                for (int i = tid; i < n_cur; i += NT) {
+                    cf acc = cf{ 0.f, 0.f };
+                    for (int k = 0; k < Ls; ++k) {
+                        const int jj = Ds * i - k;
+                        if (jj < 0) break;
+                        cf u;
+                        if (st == 0) {
+                            const float2 x = virt(a.x, a.hist_in, wb + jj, n_in, L);
+                            u = cf{ x.x, x.y };
+                        } else {
+                            u = src[jj];
+                        }
+                        acc = __builtin_elementwise_fma(cf{ hs[k], hs[k] }, u, acc);
+                    }
+                    dst[i] = acc;
+                }
+                hs += Ls;
+                n_prev = n_cur;
+                nsh::lds_barrier();
+            }
+            const cf* last = buf[(a.nst - 1) & 1]; // y[m] at local m = Q + t
+            for (int t = tid; t < V; t += NT)
+                if (rowf + t < a.n_out) a.out[rowf + t] = make_float2(last[Q + t].x, last[Q + t].y);
+        }
+        PFFT_T(4);
+        if (sum1 && w >= P / 2) phase_sum(f - 1);
+        if (f + 1 < f1) {
+            unpack_rows(v, nx);
+            pass1_of(f + 1);
+        }
+        PFFT_T(5);
+        nsh::lds_barrier(); // B2: the products of frame f and Z of frame f - 1 complete
+        PFFT_T(6);
+        inv2 = sum1;
+        ks2 = ks1;
+        sum1 = !bad;
+        ks1 = ks;
+    }
+    // drain the pipeline: the phase sum of the last frame and the inverses of the last two
+    if (inv2 && w == (int)((f1 - 2) & 3)) inverse(f1 - 2, ks2);
+    if (sum1) {
+        if (w >= P / 2) phase_sum(f1 - 1);
+        nsh::lds_barrier();
+        if (w == (int)((f1 - 1) & 3)) inverse(f1 - 1, ks1);
+    }
+}
+
 hipError_t set_lds_attr(const void* fn, int bytes, int dev)
 {
     static std::mutex mtx;
@@ -645,6 +1009,18 @@ constexpr int lds_bytes()
     static_assert(((M * P + P * IMG + IMG) * 8) % 16 == 0, "LDS carves must stay 16-B aligned");
     return (M * P + P * IMG + IMG) * 8 + 2 * P * 4;
 }
+template <int P>
+constexpr int lds_bytes2()
+{
+    return (2 * P * IMG2 + 2 * M + IMG2 + 1) * 8 + 2 * P * 4;
+}
+static_assert(lds_bytes2<16>() <= 160 * 1024, "k_fir_pfft2's LDS");
+
+// The C5 (P = 16) form: 1 = k_fir_pfft (default), 2 = k_fir_pfft2 (round 5, measured level or slower; environment
+// NSH_PFFT_FORM at plan creation, for one-process A/B and the tests of both)
+#ifndef NSH_PFFT_FORM16
+#define NSH_PFFT_FORM16 1
+#endif
 
 } // namespace
 
@@ -656,6 +1032,7 @@ struct nsh_fir_casc_plan {
     int V = 0;    // outputs per frame
     int n_cu = 256;
     int wg_per_cu = 1;
+    int form = 1; // 2: k_fir_pfft2 (P = 16)
     float2* F = nullptr;
     float2* tw = nullptr;
     float* heq = nullptr;
@@ -743,7 +1120,7 @@ int nsh_fir_cascade_plan_create(int dev, const float* const* taps_host, const in
     std::vector<float> st;
     if (nstages >= 2 && nstages <= MAX_STAGES) {
         const int n1 = (D * M - 1) / decims[0] + 1, n2 = (n1 - 1) / decims[1] + 1;
-        if ((int64_t)(n1 + n2) <= (int64_t)D * IMG) {
+        if ((int64_t)(n1 + n2) <= (int64_t)D * IMG2) { // the smaller of both forms' image sets
             p->nst = nstages;
             p->n1 = n1;
             for (int s = 0; s < nstages; ++s) {
@@ -761,9 +1138,21 @@ int nsh_fir_cascade_plan_create(int dev, const float* const* taps_host, const in
     if (e == hipSuccess) e = hipMemcpy(p->F, F.data(), F.size() * sizeof(float2), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(p->tw, tw.data(), tw.size() * sizeof(float2), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(p->heq, hf.data(), hf.size() * sizeof(float), hipMemcpyHostToDevice);
+    if (D == 16) {
+        const char* fe = std::getenv("NSH_PFFT_FORM");
+        p->form = fe && *fe ? std::atoi(fe) : NSH_PFFT_FORM16;
+        if (p->form != 1 && p->form != 2) {
+            delete p;
+            return nsh::fail_msg("nsh_fir_cascade_plan_create: NSH_PFFT_FORM must be 1 or 2");
+        }
+    }
     if (e == hipSuccess) {
-        const void* fn = D == 16 ? (const void*)k_fir_pfft<16, PW16> : (const void*)k_fir_pfft<8, PW8>;
-        e = set_lds_attr(fn, D == 16 ? lds_bytes<16>() : lds_bytes<8>(), p->dev);
+        if (p->form == 2)
+            e = set_lds_attr((const void*)k_fir_pfft2<16>, lds_bytes2<16>(), p->dev);
+        else if (D == 16)
+            e = set_lds_attr((const void*)k_fir_pfft<16, PW16>, lds_bytes<16>(), p->dev);
+        else
+            e = set_lds_attr((const void*)k_fir_pfft<8, PW8>, lds_bytes<8>(), p->dev);
     }
     if (e != hipSuccess) {
         if (p->F) (void)hipFree(p->F);
@@ -773,7 +1162,8 @@ int nsh_fir_cascade_plan_create(int dev, const float* const* taps_host, const in
         delete p;
         return nsh::fail(e, "nsh_fir_cascade_plan_create");
     }
-    p->kernel = "k_fir_pfft<" + std::to_string(D) + "," + std::to_string(D == 16 ? PW16 : PW8) + ">";
+    p->kernel = p->form == 2 ? std::string("k_fir_pfft2<16>")
+                             : "k_fir_pfft<" + std::to_string(D) + "," + std::to_string(D == 16 ? PW16 : PW8) + ">";
     *plan = p;
     return 0;
 }
@@ -838,7 +1228,9 @@ int nsh_fir_cascade_ccf(void* plan, const float* in, const float* hist_in, float
     }
 #endif
     wg = (a.nf + a.fpw - 1) / a.fpw;
-    if (p->D == 16)
+    if (p->form == 2)
+        nsh::launch((k_fir_pfft2<16>), dim3((unsigned)wg), dim3(64 * 16), lds_bytes2<16>(), nsh::S(stream), a);
+    else if (p->D == 16)
         nsh::launch((k_fir_pfft<16, PW16>), dim3((unsigned)wg), dim3(pshape<16, PW16>::NT), lds_bytes<16>(),
                     nsh::S(stream), a);
     else

@@ -19,6 +19,22 @@ void clear_error() { t_err.clear(); }
 
 using namespace nsh;
 
+// nsh_clock_sample: one wave, lane 0 reads the counters; the store is a vector store from lane 0
+__global__ __launch_bounds__(64) void k_clock_sample(unsigned long long* out, unsigned long long ticks)
+{
+    if (threadIdx.x != 0) return;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime(), c0 = __builtin_amdgcn_s_memtime();
+    unsigned long long t1 = t0;
+    for (int it = 0; it < (1 << 22) && t1 - t0 < ticks; ++it) { // <= 2^22 sleeps (~1.7 s at 2.4 GHz)
+        __builtin_amdgcn_s_sleep(127);                            // 127 x 64 cycles
+        t1 = __builtin_amdgcn_s_memrealtime();
+    }
+    const unsigned long long c1 = __builtin_amdgcn_s_memtime();
+    t1 = __builtin_amdgcn_s_memrealtime();
+    out[0] = c1 - c0;
+    out[1] = t1 - t0;
+}
+
 extern "C" {
 
 int nsh_abi_version(void) { return NSH_ABI_VERSION; }
@@ -113,6 +129,16 @@ int nsh_time_next_launch(void* start_event, void* stop_event)
     e.stop = reinterpret_cast<hipEvent_t>(stop_event);
     return 0;
 }
+int nsh_clock_sample(void* out_dev, int64_t real_ticks, void* stream)
+{
+    if (!out_dev) return nsh::fail_msg("nsh_clock_sample: null output");
+    if (real_ticks < 1 || real_ticks > ((int64_t)1 << 32)) return nsh::fail_msg("nsh_clock_sample: real_ticks out of range");
+    hipLaunchKernelGGL(k_clock_sample, dim3(1), dim3(64), 0, nsh::S(stream), (unsigned long long*)out_dev,
+                       (unsigned long long)real_ticks);
+    NSH_CK_LAUNCH("nsh_clock_sample");
+    return 0;
+}
+
 int nsh_event_query(void* event)
 {
     hipError_t e = hipEventQuery(reinterpret_cast<hipEvent_t>(event));

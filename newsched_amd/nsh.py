@@ -44,6 +44,7 @@ SIGNATURES = {
     "nsh_event_elapsed_ms": (_i, [_vp, _vp, C.POINTER(_f)]),
     "nsh_stream_wait_event": (_i, [_vp, _vp]),
     "nsh_time_next_launch": (_i, [_vp, _vp]),
+    "nsh_clock_sample": (_i, [_vp, _i64, _vp]),
     "nsh_malloc": (_i, [_i, _sz, C.POINTER(_vp)]),
     "nsh_free": (_i, [_vp]),
     "nsh_host_alloc": (_i, [_sz, C.POINTER(_vp)]),
@@ -152,6 +153,26 @@ def mul_cc(a, b, y, n: int, stream=None):
 def mul_const_vcc(x, y, k, vlen: int, nitems: int, stream=None):
     """y[i][j] = x[i][j] * k[j] over nitems items of vlen samples (k: device, vlen complex)."""
     check(lib().nsh_mul_const_vcc(ptr(x), ptr(y), ptr(k), vlen, nitems, stream_ptr(stream)), "nsh_mul_const_vcc")
+
+
+class ClockSampler:
+    """nsh_clock_sample on a side stream: start() before the work to observe, mhz() after it
+    (waits for the sample). One wave sleeping between two counter reads, ~real_ms long."""
+
+    def __init__(self, real_ms: float = 8.0):
+        import torch
+
+        self._ticks = max(1, int(real_ms * 1e5))  # 100 MHz real-time counter
+        self._out = torch.zeros(2, dtype=torch.int64, device="cuda")
+        self._s = torch.cuda.Stream()
+
+    def start(self):
+        check(lib().nsh_clock_sample(ptr(self._out), self._ticks, stream_ptr(self._s)), "nsh_clock_sample")
+
+    def mhz(self) -> float:
+        self._s.synchronize()
+        cyc, ticks = (int(v) for v in self._out.cpu().tolist())
+        return 100.0 * cyc / ticks if ticks > 0 else float("nan")
 
 
 def synth(y, n: int, first_index: int = 0, seed: int = 0x6E736368, stream=None):

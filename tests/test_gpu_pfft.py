@@ -12,6 +12,11 @@ stage-by-stage chain (oracle.fir_ccf per stage, double accumulation, fp32 betwee
   envelope), a loud burst beside a quiet signal (the frame-relative accuracy contract),
   determinism.
 
+Every test runs on both forms of the 16-phase kernel (NSH_PFFT_FORM at plan creation): 1 =
+k_fir_pfft<16,1> (the default) and 2 = k_fir_pfft2<16> (round 5: no LDS ring, pass 1 on the loaded
+rows, double-buffered phase images; opt-in); decimation-8 plans have one form
+(k_fir_pfft<8,1>).
+
 Tolerance: the north-star 1e-5 (oracle.tol_ok) on the final outputs."""
 import numpy as np
 import pytest
@@ -20,6 +25,14 @@ from oracle import oracle as orc
 from newsched_amd import nsh
 
 pytestmark = pytest.mark.gpu
+
+KERNEL16 = {"2": "k_fir_pfft2<16>", "1": "k_fir_pfft<16,1>"}
+
+
+@pytest.fixture(autouse=True, params=["1", "2"], ids=["form1", "form2"])
+def pfft_form(request, monkeypatch):
+    monkeypatch.setenv("NSH_PFFT_FORM", request.param)
+    return request.param
 
 
 def _firwin(n, cutoff):
@@ -74,9 +87,9 @@ def run_pfft(torch, plan, x, n_out, hist=None, want_hist=True):
     return dy.cpu().numpy()[:n_out], (dho.cpu().numpy() if want_hist else None)
 
 
-def test_c5_plan_shape(torch_cuda):
+def test_c5_plan_shape(torch_cuda, pfft_form):
     p = nsh.FirCascadePlan(C5)
-    assert p.decim == 16 and p.hist_len == 1890 and p.kernel == "k_fir_pfft<16,1>"
+    assert p.decim == 16 and p.hist_len == 1890 and p.kernel == KERNEL16[pfft_form]
 
 
 @pytest.mark.parametrize("n_out", [1, 2, 118, 119, 392, 393, 394, 786, 787, 5000, 393 * 256, 393 * 256 + 1,
@@ -378,7 +391,7 @@ def test_c5_many_calls_ring_offsets(torch_cuda):
 
 @pytest.mark.parametrize("decim", [8, 16])
 @pytest.mark.parametrize("ntaps", [1, 31, 127, 511, 2049])
-def test_firplan_auto_pfft(torch_cuda, decim, ntaps):
+def test_firplan_auto_pfft(torch_cuda, decim, ntaps, pfft_form):
     """nsh_fir_plan_create(AUTO) routes decim 8 and 16 to the polyphase-FFT kernel (one-stage
     cascade): same nsh_fir_ccf contract (ntaps-1 history, ping-pong), against the oracle over
     calls of several sizes."""
@@ -390,7 +403,7 @@ def test_firplan_auto_pfft(torch_cuda, decim, ntaps):
     h = np.asarray(__import__("scipy.signal", fromlist=["firwin"]).firwin(ntaps, 0.8 / decim), np.float32) \
         if ntaps > 1 else np.array([0.75], np.float32)
     plan = nsh.FirPlan(h, decim)
-    assert plan.algo == nsh.FIR_PFFT and plan.kernel == "k_fir_pfft<%d,1>" % decim
+    assert plan.algo == nsh.FIR_PFFT and plan.kernel == (KERNEL16[pfft_form] if decim == 16 else "k_fir_pfft<8,1>")
     cuts = [0, 3, 500, 501, 9000, 40000]
     x = orc.synth(decim * cuts[-1], ntaps)
     ref = orc.fir_ccf(x, h, decim)

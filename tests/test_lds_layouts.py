@@ -62,3 +62,29 @@ def test_v12_tap_copies_conflict_free(Q):
                 m0 = 32 * Q - 1 - rho + 16 * (st & 1) + 8 * h - 32 * (st >> 1)
                 addr.append((m0 & 3) * copy + 2 * (m0 & ~3) + half)
             assert cycles(addr, B64, 8) == 2, (Q, st, half)
+
+
+def _pfft2_x1_store_cycles(img, w, r):
+    """k_fir_pfft2's exchange-1 stores (ds_write_b64 / ds_write2_b64: 4 groups of 16 contiguous
+    lanes, 8-B entries, entry mod 16 = bank pair): after the half-wave swap lane l = 32 h + q of
+    wave w holds phase pp = 2 (q & 7) + h at Stockham position jp = 4 w + 2 ((q >> 3) & 1) + (q >> 4)
+    (row_of_lane) and stores entry pp * img + 8 jp + (jp >> 1) + r."""
+    tot = 0
+    for grp in range(4):
+        ent = []
+        for l in range(16 * grp, 16 * grp + 16):
+            q = l & 31
+            pp, jp = 2 * (q & 7) + (l >> 5), 4 * w + 2 * ((q >> 3) & 1) + (q >> 4)
+            ent.append((pp * img + 8 * jp + (jp >> 1) + r) % 16)
+        tot += max(ent.count(b) for b in set(ent))
+    return tot
+
+
+def test_pfft2_exchange1_stores_conflict_free():
+    """IMG2 = 571 (odd): a group's 8 phases of one parity at two positions 2 apart land on 16
+    distinct bank pairs (odd stride, and positions 2 apart shift by 17 entries); an even image
+    stride (the ring form's 572) would conflict."""
+    for w in range(16):
+        for r in range(8):
+            assert _pfft2_x1_store_cycles(571, w, r) == 4
+    assert _pfft2_x1_store_cycles(572, 0, 0) > 4
