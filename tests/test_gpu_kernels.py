@@ -687,7 +687,8 @@ def test_fir_mfma12_exact_chunk_zero_from_history(torch_cuda, kind):
 @pytest.mark.parametrize("decim", [1, 2, 4])
 @pytest.mark.parametrize("ntaps", [127, 61])
 def test_fir_mfma_exact_tile_mixed_stream(torch_cuda, ntaps, decim):
-    """The exact-fp32 tile inside the default kernels (k_fir_mfma12, k_fir_mfma11) on a stream that
+    """The exact-fp32 tile behind the default kernels (k_fir_mfma12 / k_fir_exact12, k_fir_mfma11,
+    k_fir_mfma13 / k_fir_exact13) on a stream that
     mixes ordinary chunks, chunks holding a finite 2^35 spike (beyond the split's range: the tile)
     and chunks holding a sample 2^-35 below their maximum, cut into two calls at an unaligned point
     with the history handed over, the second call ending inside a chunk. The tile's fp32 products
@@ -703,7 +704,7 @@ def test_fir_mfma_exact_tile_mixed_stream(torch_cuda, ntaps, decim):
     for c in rng.choice(23, 4, replace=False):
         x[c * 2048 + int(rng.integers(0, 2048))] *= np.float32(2.0 ** -35)
     plan = nsh.FirPlan(h, decim, nsh.FIR_MFMA)
-    assert plan.kernel.startswith("k_fir_mfma12" if decim == 1 else "k_fir_mfma11"), plan.kernel
+    assert plan.kernel.startswith({1: "k_fir_mfma12", 2: "k_fir_mfma11", 4: "k_fir_mfma13"}[decim]), plan.kernel
     n1 = 9 * (2048 // decim) + 333  # first call: ends inside a chunk
     y1, h1 = run_fir(torch, plan, x[: n1 * decim], n1)
     y2, _ = run_fir(torch, plan, x[n1 * decim:], n_out - n1, hist=h1)
@@ -771,7 +772,7 @@ def test_fir_plan_kernels():
     assert nsh.FirPlan(h, 1, nsh.FIR_AUTO).kernel == "k_fir_mfma12<5>"
     assert nsh.FirPlan(h, 1, nsh.FIR_DIRECT).kernel == "k_fir_direct<1,8>"
     assert nsh.FirPlan(h, 2, nsh.FIR_MFMA).kernel == "k_fir_mfma11<2,5>"
-    assert nsh.FirPlan(h, 4, nsh.FIR_MFMA).kernel == "k_fir_mfma11<4,3>"
+    assert nsh.FirPlan(h, 4, nsh.FIR_MFMA).kernel == "k_fir_mfma13<4,3>"  # the lockstep walk (round 5)
     for L in (1, 17, 33, 65, 97, 129, 161):
         assert nsh.FirPlan(np.ones(L, np.float32), 1, nsh.FIR_MFMA).kernel == "k_fir_mfma12<%d>" % ((L + 30) // 32 + 1)
 

@@ -14,4 +14,6 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o bench --output-
 tools/pmc_fir.sh $O/pmc && python3 tools/pmc_summary.py $O/pmc $((1<<25)) $O/pmc_fir.json > /dev/null && echo "pmc ok" &&
 tools/pmc_fir.sh $O/pmc_casc --algo casc && python3 tools/pmc_summary.py $O/pmc_casc $((1<<25)) $O/pmc_casc.json > /dev/null && echo "pmc casc ok" &&
 timeout -k 10 120 python tools/pfft_bench.py > $O/pfft_bench.json 2> $O/pfft_bench.err && echo "pfft bench ok" &&
-timeout -k 10 400 build/tools/bench_configs 28 30 > $O/configs.jsonl 2> $O/configs.err && echo "configs ok"
+timeout -k 10 400 build/tools/bench_configs 28 30 > $O/configs.jsonl 2> $O/configs.err && echo "configs ok" &&
+# the exact-fp32 form's clock by the PMC method, beside bench.py's in-process sampler (clock_mhz)
+[ "${CLOCK:-1}" = 1 ] && tools/pmc_clock.sh $O/clock_f32 --algo f32 > /dev/null && tools/pmc_clock.sh $O/clock_fir --algo mfma > /dev/null && echo "clock ok"
