@@ -324,6 +324,9 @@ struct pshape {
 #ifndef NSH_PFFT_RINGORDER
 #define NSH_PFFT_RINGORDER 1 // the window transformed in ring order (rotated), the rotation undone at the output
 #endif
+#ifndef NSH_PFFT_SPLIT_WIN
+#define NSH_PFFT_SPLIT_WIN 1
+#endif
 #ifndef NSH_PFFT_SPLIT_READS
 #define NSH_PFFT_SPLIT_READS 1
 #endif
@@ -482,7 +485,14 @@ __global__ __launch_bounds__(64 * P / PW, 1) void k_fir_pfft(pfft_args a)
             for (int i = 0; i < PW; ++i) {
                 const cf* rb = ring + ring_at<P>(j, w * PW + i);
 #pragma unroll
-                for (int r = 0; r < 8; ++r) v[i][r] = (NSH_PFFT_ABLATE & 16) ? cf{ sc, (float)r } : rb[64 * P * r];
+                for (int r = 0; r < 8; ++r) {
+                    v[i][r] = (NSH_PFFT_ABLATE & 16) ? cf{ sc, (float)r } : rb[64 * P * r];
+                    // single ds_read_b64 each: paired (ds_read2st64_b64) they are served in 16-lane
+                    // groups, where lanes 2 t and 2 t + 1 share a swizzle -- 2-way conflicts on every
+                    // window read (2.7 M conflict cycles per 2^25 inputs, r04zm); in the 32-lane
+                    // groups of single reads the two rows of a pair sit 16 bank pairs apart
+                    if (NSH_PFFT_SPLIT_WIN) asm volatile("" ::: "memory");
+                }
             }
 #else
             // rows rowf + j + 64 r share one swizzle (64 r moves s / (32 / P) by a multiple of P)
