@@ -670,6 +670,9 @@ constexpr int IMG2 = 571; // odd: a 16-lane group's exchange-1 stores (16 phases
 #ifndef NSH_PFFT2_ABLATE
 #define NSH_PFFT2_ABLATE 0
 #endif
+#ifndef NSH_PFFT2_LOAD_AT
+#define NSH_PFFT2_LOAD_AT 1 // the next frame's row loads: 1 = after B1 (and the inverse), 0 = at the frame top (r05u: 6 % slower)
+#endif
 #ifndef NSH_PFFT2_LD_AUX
 #define NSH_PFFT2_LD_AUX 0 // row loads: default policy (the overlap rows are read again by the next frame)
 #endif
@@ -863,7 +866,7 @@ __global__ __launch_bounds__(64 * P, 1) void k_fir_pfft2(pfft_args a)
         // the next frame's rows, requested here and consumed at the end of this frame's phase A:
         // ~1.7 us of HBM latency under this load (phase trace), most of a frame
         nsh::buf_f4 nx[4];
-        load_rows16<P>(nx, a, n_in, f + 1, f + 1 < f1, e0);
+        if (NSH_PFFT2_LOAD_AT == 0) load_rows16<P>(nx, a, n_in, f + 1, f + 1 < f1, e0);
         // A0: frame f's pass-1 outputs (computed at the end of the previous phase A) into set s
 #pragma unroll
         for (int r = 0; r < 8; ++r) cur[e1off + r] = v[r];
@@ -896,6 +899,7 @@ __global__ __launch_bounds__(64 * P, 1) void k_fir_pfft2(pfft_args a)
         // frame f, then the phase sum of frame f - 1 (waves 8..15; set s ^ 1 is rewritten only by
         // frame f + 1's pass 1, after B2)
         if (inv2 && w == (int)((f - 2) & 3)) inverse(f - 2, ks2);
+        if (NSH_PFFT2_LOAD_AT == 1) load_rows16<P>(nx, a, n_in, f + 1, f + 1 < f1, e0);
         PFFT_T(3);
         const int64_t rowf = f * V;
         if (!bad) {
