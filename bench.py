@@ -335,7 +335,7 @@ def run_copy_leg(n, barrier, torch, nsh):
 def run_c5_fused_leg(a, first, device, barrier, dist, tdev, torch, orc, nsh):
     """BASELINE config C5's chain 4 x fir_filter_ccf(firwin(127, 0.45), 2) as the fused kernel
     scheduler_hip puts in its place (hip::fir_filter_cascade_ccf -> nsh_fir_cascade_ccf,
-    k_fir_pfft<16>): 2^log2n resident input samples per GPU, one launch per step, HIP events on
+    k_fir_pfft2<16>): 2^log2n resident input samples per GPU, one launch per step, HIP events on
     the launch stream; roofline against the chain's 8.5 B per input sample (read 8, write 0.5)."""
     n = 1 << a.c5_fused_log2n
     taps = firwin(127, 0.45)
@@ -415,7 +415,7 @@ def main():
     ap.add_argument("--cpu-log2n", type=int, default=28, help="CPU baseline sample (default: the full stream)")
     ap.add_argument("--c5", choices=["auto", "on", "off"], default="auto", help="C5 pipeline leg (auto: at world > 1)")
     ap.add_argument("--c5-fused", choices=["on", "off"], default="on",
-                    help="C5's chain as the fused kernel (k_fir_pfft<16>) on resident input, every rank")
+                    help="C5's chain as the fused kernel (k_fir_pfft2<16>) on resident input, every rank")
     ap.add_argument("--c5-fused-log2n", type=int, default=28)
     ap.add_argument("--c5-log2n", type=int, default=26)
     ap.add_argument("--c5-steps", type=int, default=5)

@@ -670,8 +670,14 @@ constexpr int IMG2 = 571; // odd: a 16-lane group's exchange-1 stores (16 phases
 #ifndef NSH_PFFT2_ABLATE
 #define NSH_PFFT2_ABLATE 0
 #endif
+#ifndef NSH_PFFT2_SUM_LOW
+#define NSH_PFFT2_SUM_LOW 1 // the phase sum on waves 0..7 (1; r05v: 4 % faster) or 8..15 (0)
+#endif
+#ifndef NSH_PFFT2_PRIO
+#define NSH_PFFT2_PRIO 0 // probe: s_setprio in phase A (1: waves 8..15 -> 1; 2: 12..15 -> 2, 8..11 -> 1; 3: inverse wave -> 3)
+#endif
 #ifndef NSH_PFFT2_LOAD_AT
-#define NSH_PFFT2_LOAD_AT 1 // the next frame's row loads: 1 = after B1 (and the inverse), 0 = at the frame top (r05u: 6 % slower)
+#define NSH_PFFT2_LOAD_AT 1 // the next frame's row loads: 1 = after B1 (and the inverse), 0 = at the frame top (r05u: 6 % slower), 2 = waves 8..15 at the top, 0..7 after B1
 #endif
 #ifndef NSH_PFFT2_LD_AUX
 #define NSH_PFFT2_LD_AUX 0 // row loads: default policy (the overlap rows are read again by the next frame)
@@ -823,7 +829,7 @@ __global__ __launch_bounds__(64 * P, 1) void k_fir_pfft2(pfft_args a)
     // the phase sum of frame fi (products in set fi & 1) into zb[fi & 1], by waves 8..15, in a fixed
     // order (deterministic)
     auto phase_sum = [&](int64_t fi) {
-        int k = tid - NT / 2;
+        int k = NSH_PFFT2_SUM_LOW ? tid : tid - NT / 2;
         asm volatile("" : "+v"(k));
         const cf* src = sets + (int)(fi & 1) * SET + k;
         cf zz = cf{ 0.f, 0.f };
@@ -866,7 +872,8 @@ __global__ __launch_bounds__(64 * P, 1) void k_fir_pfft2(pfft_args a)
         // the next frame's rows, requested here and consumed at the end of this frame's phase A:
         // ~1.7 us of HBM latency under this load (phase trace), most of a frame
         nsh::buf_f4 nx[4];
-        if (NSH_PFFT2_LOAD_AT == 0) load_rows16<P>(nx, a, n_in, f + 1, f + 1 < f1, e0);
+        if (NSH_PFFT2_LOAD_AT == 0 || (NSH_PFFT2_LOAD_AT == 2 && w >= P / 2))
+            load_rows16<P>(nx, a, n_in, f + 1, f + 1 < f1, e0);
         // A0: frame f's pass-1 outputs (computed at the end of the previous phase A) into set s
 #pragma unroll
         for (int r = 0; r < 8; ++r) cur[e1off + r] = v[r];
@@ -898,8 +905,21 @@ __global__ __launch_bounds__(64 * P, 1) void k_fir_pfft2(pfft_args a)
         // A: the inverse of frame f - 2 (one of waves 0..3, rotating over the SIMDs), phase w of
         // frame f, then the phase sum of frame f - 1 (waves 8..15; set s ^ 1 is rewritten only by
         // frame f + 1's pass 1, after B2)
-        if (inv2 && w == (int)((f - 2) & 3)) inverse(f - 2, ks2);
-        if (NSH_PFFT2_LOAD_AT == 1) load_rows16<P>(nx, a, n_in, f + 1, f + 1 < f1, e0);
+        if (NSH_PFFT2_PRIO == 1 && w >= 8) __builtin_amdgcn_s_setprio(1);
+        if (NSH_PFFT2_PRIO == 2 && w >= 12) __builtin_amdgcn_s_setprio(2);
+        if (NSH_PFFT2_PRIO == 2 && w >= 8 && w < 12) __builtin_amdgcn_s_setprio(1);
+        if (inv2 && w == (int)((f - 2) & 3)) {
+            if (NSH_PFFT2_PRIO == 3) __builtin_amdgcn_s_setprio(3);
+            inverse(f - 2, ks2);
+            if (NSH_PFFT2_PRIO == 3) __builtin_amdgcn_s_setprio(0);
+        }
+        if (NSH_PFFT2_LOAD_AT == 1 || (NSH_PFFT2_LOAD_AT == 2 && w < P / 2)) {
+            // the youngest waves (last in issue arbitration) request their rows first
+            if (NSH_PFFT2_PRIO == 4 && w >= 12) __builtin_amdgcn_s_setprio(3);
+            if (NSH_PFFT2_PRIO == 4 && w >= 8 && w < 12) __builtin_amdgcn_s_setprio(2);
+            load_rows16<P>(nx, a, n_in, f + 1, f + 1 < f1, e0);
+            if (NSH_PFFT2_PRIO == 4 && w >= 8) __builtin_amdgcn_s_setprio(0);
+        }
         PFFT_T(3);
         const int64_t rowf = f * V;
         if (!bad) {
@@ -975,12 +995,13 @@ __global__ __launch_bounds__(64 * P, 1) void k_fir_pfft2(pfft_args a)
                 if (rowf + t < a.n_out) a.out[rowf + t] = make_float2(last[Q + t].x, last[Q + t].y);
         }
         PFFT_T(4);
-        if (sum1 && w >= P / 2) phase_sum(f - 1);
+        if (sum1 && (NSH_PFFT2_SUM_LOW ? w < P / 2 : w >= P / 2)) phase_sum(f - 1);
         if (f + 1 < f1) {
             unpack_rows(v, nx);
             pass1_of(f + 1);
         }
         PFFT_T(5);
+        if (NSH_PFFT2_PRIO == 1 || NSH_PFFT2_PRIO == 2) __builtin_amdgcn_s_setprio(0);
         nsh::lds_barrier(); // B2: the products of frame f and Z of frame f - 1 complete
         PFFT_T(6);
         inv2 = sum1;
@@ -991,7 +1012,7 @@ __global__ __launch_bounds__(64 * P, 1) void k_fir_pfft2(pfft_args a)
     // drain the pipeline: the phase sum of the last frame and the inverses of the last two
     if (inv2 && w == (int)((f1 - 2) & 3)) inverse(f1 - 2, ks2);
     if (sum1) {
-        if (w >= P / 2) phase_sum(f1 - 1);
+        if (NSH_PFFT2_SUM_LOW ? w < P / 2 : w >= P / 2) phase_sum(f1 - 1);
         nsh::lds_barrier();
         if (w == (int)((f1 - 1) & 3)) inverse(f1 - 1, ks1);
     }
@@ -1030,10 +1051,10 @@ constexpr int lds_bytes2()
 }
 static_assert(lds_bytes2<16>() <= 160 * 1024, "k_fir_pfft2's LDS");
 
-// The C5 (P = 16) form: 1 = k_fir_pfft (default), 2 = k_fir_pfft2 (round 5, measured level or slower; environment
+// The C5 (P = 16) form: 2 = k_fir_pfft2 (round 5, default: 2.2-2.5 % faster, r05y), 1 = k_fir_pfft (environment
 // NSH_PFFT_FORM at plan creation, for one-process A/B and the tests of both)
 #ifndef NSH_PFFT_FORM16
-#define NSH_PFFT_FORM16 1
+#define NSH_PFFT_FORM16 2
 #endif
 
 } // namespace

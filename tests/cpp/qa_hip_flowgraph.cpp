@@ -393,7 +393,7 @@ TEST(HipDomain, DecimatingChainC5)
             if (fused) {
                 auto c = std::dynamic_pointer_cast<hip::fir_filter_cascade_ccf>(sched->fusion_plan().fused[0]);
                 ASSERT_TRUE(c != nullptr);
-                EXPECT_TRUE(c->kernel() == "k_fir_pfft<16,1>");
+                EXPECT_TRUE(c->kernel() == "k_fir_pfft2<16>");
                 EXPECT_TRUE(c->launches() > 4u);
                 EXPECT_TRUE(st[0]->launches() == 0u); // the staged blocks were replaced
             }
@@ -447,7 +447,7 @@ TEST(HipDomain, TimedPfftLaunches)
         fg->validate();
         fir->enable_timing(true);
         fg->run();
-        EXPECT_TRUE(fir->kernel() == "k_fir_pfft<16,1>");
+        EXPECT_TRUE(fir->kernel() == "k_fir_pfft2<16>");
         EXPECT_TRUE(close_normwise(snk->data(), ref));
         const double ms = fir->kernel_ms();
         std::printf("  decim-16 fir: %llu timed launches, %.3f ms\n", (unsigned long long)fir->timed_launches(), ms);

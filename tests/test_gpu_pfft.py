@@ -12,10 +12,10 @@ stage-by-stage chain (oracle.fir_ccf per stage, double accumulation, fp32 betwee
   envelope), a loud burst beside a quiet signal (the frame-relative accuracy contract),
   determinism.
 
-Every test runs on both forms of the 16-phase kernel (NSH_PFFT_FORM at plan creation): 1 =
-k_fir_pfft<16,1> (the default) and 2 = k_fir_pfft2<16> (round 5: no LDS ring, pass 1 on the loaded
-rows, double-buffered phase images; opt-in); decimation-8 plans have one form
-(k_fir_pfft<8,1>).
+Every test runs on both forms of the 16-phase kernel (NSH_PFFT_FORM at plan creation): 2 =
+k_fir_pfft2<16> (round 5, the default: no LDS ring, pass 1 on the loaded rows, double-buffered
+phase images) and 1 = k_fir_pfft<16,1> (the ring form); decimation-8 plans have one
+form (k_fir_pfft<8,1>).
 
 Tolerance: the north-star 1e-5 (oracle.tol_ok) on the final outputs."""
 import numpy as np
@@ -29,7 +29,7 @@ pytestmark = pytest.mark.gpu
 KERNEL16 = {"2": "k_fir_pfft2<16>", "1": "k_fir_pfft<16,1>"}
 
 
-@pytest.fixture(autouse=True, params=["1", "2"], ids=["form1", "form2"])
+@pytest.fixture(autouse=True, params=["2", "1"], ids=["form2", "form1"])
 def pfft_form(request, monkeypatch):
     monkeypatch.setenv("NSH_PFFT_FORM", request.param)
     return request.param

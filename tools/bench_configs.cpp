@@ -406,7 +406,7 @@ int main(int argc, char** argv)
             auto y = g.tail(m);
             const double gbs = 8.5 * n / s / 1e9;
             const char* var = fused ? "G=1: 4 x fir_filter_ccf(127 taps, decim 2), fused by scheduler_hip into one "
-                                      "fir_filter_cascade_ccf (k_fir_pfft<16>, default)"
+                                      "fir_filter_cascade_ccf (k_fir_pfft2<16>, default)"
                                     : "G=1: 4 x fir_filter_ccf(127 taps, decim 2), FIR fusion off (4 launches, every "
                                       "stage streams its own input)";
             emit(std::string("{\"config\": \"C5\", \"variant\": \"") + var + "\", \"value\": " + num(n / s / 1e6) +

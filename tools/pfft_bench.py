@@ -1,4 +1,4 @@
-"""C5 kernel timing: the fused chain k_fir_pfft<16> (nsh_fir_cascade_ccf) vs the four staged
+"""C5 kernel timing: the fused chain k_fir_pfft2<16> (nsh_fir_cascade_ccf) vs the four staged
 decimate-by-2 launches it replaces, same process, interleaved rounds, HIP events on the launch
 stream, >= 1 s warm-up. Input 2^LOG2 resident samples; bytes per input sample: 8.5 fused (read 8,
 write 0.5), 22.5 staged.
