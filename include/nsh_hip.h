@@ -161,7 +161,7 @@ int nsh_synth_cf32(float* out, int64_t n, uint64_t first_index, uint64_t seed, v
  * (decim 1, ntaps <= 257, finite taps; no operand split: fp32 products and sums, chunks with
  * inf/NaN through the fp32 direct form in the same launch). NSH_FIR_PFFT (decim 8 and 16; AUTO
  * picks it there when ceil((ntaps-1)/decim) <= 256 and the taps are finite): the polyphase-FFT
- * overlap-save kernel of nsh_fir_cascade_ccf with one stage (k_fir_pfft<decim,1>; within fp32
+ * overlap-save kernel of nsh_fir_cascade_ccf with one stage (k_fir_pfft2<16> / k_fir_pfft<8,1>; within fp32
  * transform rounding of the direct form, frame-relative, see nsh_fir_cascade_ccf below); decim 16
  * is only available as PFFT. */
 enum nsh_fir_algo {
@@ -185,7 +185,7 @@ int nsh_fir_ccf(void* plan, const float* in, const float* hist_in, float* hist_o
  * nsh_fir_ccf calls and the intermediate streams). The chain composes into one decimating filter
  *   y[m] = sum_n heq[n] x[m D - n],   D = prod D_s,   heq = h_1 * (h_2 up D_1) * (h_3 up D_1 D_2) ...
  * (composed in double at plan creation), computed by polyphase-FFT overlap-save
- * (k_fir_pfft<D>, D = 8 or 16; ceil((len(heq) - 1) / D) <= 256). Per call: in = n_out * D
+ * (k_fir_pfft2<16> / k_fir_pfft<8,1>; ceil((len(heq) - 1) / D) <= 256). Per call: in = n_out * D
  * samples; hist_in / hist_out = nsh_fir_cascade_hist_len(plan) = len(heq) - 1 input samples, as
  * for nsh_fir_ccf (NULL hist_in reads as zeros; hist_out may be NULL; no aliasing). A chain whose
  * stages all start from zero history is equivalent to this plan from a zero history.
@@ -205,7 +205,7 @@ int nsh_fir_cascade_plan_create(int dev, const float* const* taps_host, const in
 int nsh_fir_cascade_plan_destroy(void* plan);
 int nsh_fir_cascade_decim(void* plan);         /* D = prod D_s */
 int nsh_fir_cascade_hist_len(void* plan);      /* len(heq) - 1 */
-const char* nsh_fir_cascade_kernel(void* plan); /* "k_fir_pfft<16,1>" */
+const char* nsh_fir_cascade_kernel(void* plan); /* "k_fir_pfft2<16>" (D = 16; "k_fir_pfft<16,1>" with NSH_PFFT_FORM=1), "k_fir_pfft<8,1>" */
 int nsh_fir_cascade_ccf(void* plan, const float* in, const float* hist_in, float* hist_out, float* out,
                         int64_t n_out, void* stream);
 
