@@ -67,6 +67,7 @@ namespace {
 using nsh::cf;
 using nsh::cmulw;
 using nsh::dft4;
+using nsh::dft8;
 using nsh::rot;
 
 #ifndef NSH_PFFT_ASM_CMUL
@@ -108,25 +109,6 @@ __device__ __forceinline__ int ring_at(int s, int p)
     return s * P + (p ^ ((s / (32 / P)) & (P - 1)));
 }
 
-// In-place DFT8, natural order in and out: X[k] = E[k] + W_8^k O[k], X[k + 4] = E[k] - W_8^k O[k]
-template <bool INV>
-__device__ __forceinline__ void dft8(cf (&v)[8])
-{
-    constexpr float R2 = 0.70710678118654757f;
-    dft4<INV>(v[0], v[2], v[4], v[6]); // E[0..3] in v[0], v[2], v[4], v[6]
-    dft4<INV>(v[1], v[3], v[5], v[7]); // O[0..3] in v[1], v[3], v[5], v[7]
-    const cf w1 = cf{ R2, INV ? R2 : -R2 }, w3 = cf{ -R2, INV ? R2 : -R2 };
-    const cf o1 = cmulw(v[3], w1), o2 = rot<INV>(v[5]), o3 = cmulw(v[7], w3);
-    const cf e0 = v[0], e1 = v[2], e2 = v[4], e3 = v[6], o0 = v[1];
-    v[0] = e0 + o0;
-    v[4] = e0 - o0;
-    v[1] = e1 + o1;
-    v[5] = e1 - o1;
-    v[2] = e2 + o2;
-    v[6] = e2 - o2;
-    v[3] = e3 + o3;
-    v[7] = e3 - o3;
-}
 
 // A wave's image addresses (one base register each, the rest immediate offsets):
 //   x1 + r        = e1(8 j + r)       = 8 j + (j >> 1) + r
