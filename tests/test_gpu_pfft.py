@@ -92,8 +92,8 @@ def test_c5_plan_shape(torch_cuda, pfft_form):
     assert p.decim == 16 and p.hist_len == 1890 and p.kernel == KERNEL16[pfft_form]
 
 
-@pytest.mark.parametrize("n_out", [1, 2, 118, 119, 392, 393, 394, 786, 787, 5000, 393 * 256, 393 * 256 + 1,
-                                   100_003, 1 << 20])
+@pytest.mark.parametrize("n_out", [1, 2, 118, 119, 383, 384, 385, 392, 393, 394, 768, 769, 786, 787, 5000,
+                                   384 * 256 + 1, 393 * 256, 393 * 256 + 1, 100_003, 1 << 20])
 def test_c5_vs_oracle_chain(torch_cuda, n_out):
     p = nsh.FirCascadePlan(C5)
     x = orc.synth(16 * n_out, n_out % 977)
@@ -123,6 +123,8 @@ CHAINS = {
     "d2-d8": [(_firwin(31, 0.45), 2), (_firwin(200, 0.1), 8)],
     "single-d16": [(_firwin(1501, 0.05), 16)],
     "single-d16-short": [(_firwin(7, 0.05), 16)],
+    "single-d16-q188": [(_firwin(3000, 0.04), 16)],  # Q = 188: frames of 324 outputs
+    "d2-d8-q129": [(_firwin(31, 0.45), 2), (_firwin(1011, 0.05), 8)],
     "d8-3x2": [(_firwin(127, 0.45), 2)] * 3,
     "single-d8": [(_firwin(900, 0.1), 8)],
     "d8-4x2": [(_firwin(127, 0.45), 2), (_firwin(61, 0.4), 4)],
