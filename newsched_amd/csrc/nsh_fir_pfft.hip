@@ -647,8 +647,7 @@ __global__ __launch_bounds__(64 * P / PW, 1) void k_fir_pfft(pfft_args a)
 // reading its window from HBM.
 constexpr int IMG2 = 571; // odd: a 16-lane group's exchange-1 stores (16 phases, one position) hit 16 bank pairs
 
-// timing-only ablation hooks for tools/probe (0 in every product build): 1 = each row-load
-// instruction reads one contiguous 1 KiB, 2 = no row loads
+// timing-only ablation hook for tools/probe (0 in every product build): 2 = no row loads
 #ifndef NSH_PFFT2_ABLATE
 #define NSH_PFFT2_ABLATE 0
 #endif
@@ -661,48 +660,67 @@ constexpr int IMG2 = 571; // odd: a 16-lane group's exchange-1 stores (16 phases
 #ifndef NSH_PFFT2_LOAD_AT
 #define NSH_PFFT2_LOAD_AT 1 // the next frame's row loads: 1 = after B1 (and the inverse), 0 = at the frame top (r05u: 6 % slower), 2 = waves 8..15 at the top, 0..7 after B1
 #endif
+// Row-load cache policy: a frame's rows V .. M - 1 (V >= 384 for Q <= 128) are the next frame's
+// first rows, read again one frame later (mostly L2 hits); rows below V are read for the last
+// time. Load 3 holds rows 384 .. 511 and keeps the default policy; loads 0..2 stream
+// (nontemporal), so they do not push the overlap rows out of L2 before they are read again:
+// 8.72 vs 9.00 HBM B per input, time level or 0.3 % faster (r05zi); nontemporal on all four
+// loses the overlap hits (10.44 B, 2 % slower).
 #ifndef NSH_PFFT2_LD_AUX
-#define NSH_PFFT2_LD_AUX 0 // row loads: default policy (the overlap rows are read again by the next frame)
+#define NSH_PFFT2_LD_AUX 2 // loads 0..2
+#endif
+#ifndef NSH_PFFT2_LD_AUX3
+#define NSH_PFFT2_LD_AUX3 0 // load 3
 #endif
 
 // Frame f's window, x[P (f V - Q) + i], i < P M, in 16-B loads: lane l = 32 h + q of wave w loads
-// phases 2 m, 2 m + 1 (m = q & 7) of rows n = 4 w + g + 64 (4 h + k), k = 0..3, g = 2 ((q >> 3) & 1)
-// + (q >> 4) -- each load instruction reads two 512-B runs of 4 whole rows -- into v[k] (phase 2 m)
-// and v[4 + k] (phase 2 m + 1); swap_halves then leaves lane l with phase pp = 2 m + h at rows
-// 4 w + g + 64 r, r = 0..7 (Stockham's pass-1 input at position jp = 4 w + g).
-__device__ __forceinline__ int row_of_lane(int w, int l)
+// phases 2 m, 2 m + 1 (m = q & 7) of rows jp + 64 (2 k + h), k = 0..3, jp = 4 w + g,
+// g = 2 ((q >> 3) & 1) + (q >> 4) -- each load instruction reads two 512-B runs of 4 whole rows --
+// into v[2 k] (phase 2 m) and v[2 k + 1] (phase 2 m + 1); swap_pairs then leaves lane l with phase
+// pp = 2 m + h at rows jp + 64 r, r = 0..7 (Stockham's pass-1 input at position jp). Load k holds
+// the row blocks 2 k, 2 k + 1: load 3 the overlap rows the next frame reads again.
+__device__ __forceinline__ int jp_of_lane(int w, int l)
 {
     const int q = l & 31;
-    return 4 * w + 2 * ((q >> 3) & 1) + (q >> 4) + 256 * (l >> 5);
+    return 4 * w + 2 * ((q >> 3) & 1) + (q >> 4);
+}
+// this lane's element of load k = 0 in a window (load k: + 128 P k)
+template <int P>
+__device__ __forceinline__ int e0_of_lane(int w, int l)
+{
+    return P * (jp_of_lane(w, l) + 64 * (l >> 5)) + 2 * (l & 7);
 }
 template <int P>
 __device__ __forceinline__ void load_frame(cf (&v)[8], const pfft_args& a, int64_t n_in, int64_t f, int w, int j)
 {
     const int64_t b = (int64_t)P * (f * a.V - a.Q);
-    const int e0 = P * row_of_lane(w, j) + 2 * (j & 7); // element of load k = 0 (loads k: + 64 P k)
+    const int e0 = e0_of_lane<P>(w, j);
     if (b >= 0) {
         const __amdgpu_buffer_rsrc_t r = span_rsrc(a.x + b, n_in - b, (int64_t)P * M);
+        nsh::buf_f4 t[4];
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+            t[k] = __builtin_bit_cast(nsh::buf_f4, __builtin_amdgcn_raw_buffer_load_b128(r, (e0 + 128 * P * k) * 8, 0, NSH_PFFT2_LD_AUX));
+        t[3] = __builtin_bit_cast(nsh::buf_f4, __builtin_amdgcn_raw_buffer_load_b128(r, (e0 + 384 * P) * 8, 0, NSH_PFFT2_LD_AUX3));
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const nsh::buf_f4 t = __builtin_bit_cast(
-                nsh::buf_f4, __builtin_amdgcn_raw_buffer_load_b128(r, (e0 + 64 * P * k) * 8, 0, NSH_PFFT2_LD_AUX));
-            v[k] = cf{ t.x, t.y };
-            v[4 + k] = cf{ t.z, t.w };
+            v[2 * k] = cf{ t[k].x, t[k].y };
+            v[2 * k + 1] = cf{ t[k].z, t[k].w };
         }
     } else { // the stream's first frame: history, then zeros before it
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const float2 u0 = virt(a.x, a.hist_in, b + e0 + 64 * P * k, n_in, a.L);
-            const float2 u1 = virt(a.x, a.hist_in, b + e0 + 64 * P * k + 1, n_in, a.L);
-            v[k] = cf{ u0.x, u0.y };
-            v[4 + k] = cf{ u1.x, u1.y };
+            const float2 u0 = virt(a.x, a.hist_in, b + e0 + 128 * P * k, n_in, a.L);
+            const float2 u1 = virt(a.x, a.hist_in, b + e0 + 128 * P * k + 1, n_in, a.L);
+            v[2 * k] = cf{ u0.x, u0.y };
+            v[2 * k + 1] = cf{ u1.x, u1.y };
         }
     }
 }
 // Frame f >= 1 (no history: f V - Q >= V - Q > 0) as raw 16-B loads into x, branch-free: the
-// loads of the next frame are issued at the top of a phase A and consumed at its end, and any
-// register copy between them would wait for them (a branchy load, joined by copies, did: every
-// wave stalled for the HBM round trip right after its loads). live = false: no bytes (reads 0).
+// loads of the next frame are issued in a phase A and consumed at its end, and any register copy
+// between them would wait for them (a branchy load, joined by copies, did: every wave stalled for
+// the HBM round trip right after its loads). live = false: no bytes (reads 0).
 template <int P>
 __device__ __forceinline__ void load_rows16(nsh::buf_f4 (&x)[4], const pfft_args& a, int64_t n_in, int64_t f, bool live,
                                             int e0)
@@ -714,33 +732,33 @@ __device__ __forceinline__ void load_rows16(nsh::buf_f4 (&x)[4], const pfft_args
 #pragma unroll
     for (int k = 0; k < 4; ++k) x[k] = nsh::buf_f4{ (float)k, 1.f, 2.f, (float)e0 };
 #else
-#if NSH_PFFT2_ABLATE & 1 // timing only: each load instruction one contiguous 1 KiB (wrong rows)
-    e0 = 2 * (threadIdx.x & 63) + 128 * (threadIdx.x >> 6);
-#endif
 #pragma unroll
-    for (int k = 0; k < 4; ++k) // one address VGPR: the load's distance in the scalar offset
-        x[k] = __builtin_bit_cast(nsh::buf_f4,
-                                  __builtin_amdgcn_raw_buffer_load_b128(r, e0 * 8, 512 * P * k, NSH_PFFT2_LD_AUX));
+    for (int k = 0; k < 3; ++k) // one address VGPR: the load's distance in the scalar offset
+        x[k] = __builtin_bit_cast(nsh::buf_f4, __builtin_amdgcn_raw_buffer_load_b128(r, e0 * 8, 1024 * P * k, NSH_PFFT2_LD_AUX));
+    x[3] = __builtin_bit_cast(nsh::buf_f4, __builtin_amdgcn_raw_buffer_load_b128(r, e0 * 8, 1024 * P * 3, NSH_PFFT2_LD_AUX3));
 #endif
 }
 __device__ __forceinline__ void unpack_rows(cf (&v)[8], const nsh::buf_f4 (&x)[4])
 {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        v[k] = cf{ x[k].x, x[k].y };
-        v[4 + k] = cf{ x[k].z, x[k].w };
+        v[2 * k] = cf{ x[k].x, x[k].y };
+        v[2 * k + 1] = cf{ x[k].z, x[k].w };
     }
 }
-// lanes l < 32 keep phase 2 m (rows r = 0..3 theirs, 4..7 from lane l + 32), lanes l >= 32 keep
-// phase 2 m + 1 (rows 0..3 from lane l - 32, 4..7 theirs): v[k] <-> v[4 + k] across the halves
-__device__ __forceinline__ void swap_halves(cf (&v)[8])
+// lanes l < 32 keep phase 2 m (row block 2 k theirs, 2 k + 1 from lane l + 32), lanes l >= 32
+// keep phase 2 m + 1 (block 2 k from lane l - 32, 2 k + 1 theirs): v[2 k] <-> v[2 k + 1] across
+// the halves
+__device__ __forceinline__ void swap_pairs(cf (&v)[8])
 {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        const auto x = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[k].x), __float_as_uint(v[4 + k].x), false, false);
-        const auto y = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[k].y), __float_as_uint(v[4 + k].y), false, false);
-        v[k] = cf{ __uint_as_float(x[0]), __uint_as_float(y[0]) };
-        v[4 + k] = cf{ __uint_as_float(x[1]), __uint_as_float(y[1]) };
+        const auto x = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[2 * k].x), __float_as_uint(v[2 * k + 1].x), false,
+                                                        false);
+        const auto y = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[2 * k].y), __float_as_uint(v[2 * k + 1].y), false,
+                                                        false);
+        v[2 * k] = cf{ __uint_as_float(x[0]), __uint_as_float(y[0]) };
+        v[2 * k + 1] = cf{ __uint_as_float(x[1]), __uint_as_float(y[1]) };
     }
 }
 
@@ -771,8 +789,8 @@ __global__ __launch_bounds__(64 * P, 1) void k_fir_pfft2(pfft_args a)
     const int64_t n_in = a.n_out * P;
     const int L = a.L, Q = a.Q, V = a.V;
     // pass 1: phase pp at Stockham position jp (= 4 w + g); its outputs go to image pp at 8 jp + r
-    const int pp = 2 * (j & 7) + (j >> 5), jp = row_of_lane(w, j) & 63;
-    const int e0 = P * row_of_lane(w, j) + 2 * (j & 7); // this lane's first element of a window
+    const int pp = 2 * (j & 7) + (j >> 5), jp = jp_of_lane(w, j);
+    const int e0 = e0_of_lane<P>(w, j); // this lane's element of load 0 in a window
     const int e1off = pp * IMG2 + 8 * jp + (jp >> 1);
 
     if (a.hist_out && blockIdx.x == gridDim.x - 1) // the next call's history: the L-1 samples before x[n_in]
@@ -834,7 +852,7 @@ __global__ __launch_bounds__(64 * P, 1) void k_fir_pfft2(pfft_args a)
     auto pass1_of = [&](int64_t fn) { // rows of frame fn in v -> its wave max in mx[fn & 1], pass 1 in v
         const unsigned m = nsh::wave_umax(maxbits8(v));
         if (j == 0) mx[(int)(fn & 1) * P + w] = m;
-        swap_halves(v);
+        swap_pairs(v);
         dft8<false>(v);
     };
     load_frame<P>(v, a, n_in, f0, w, j);
@@ -875,7 +893,7 @@ __global__ __launch_bounds__(64 * P, 1) void k_fir_pfft2(pfft_args a)
         if (redo) { // workgroup-uniform
             cf u[8];
             load_frame<P>(u, a, n_in, f, w, j);
-            swap_halves(u);
+            swap_pairs(u);
 #pragma unroll
             for (int r = 0; r < 8; ++r) u[r] *= sc;
             dft8<false>(u);
