@@ -627,8 +627,8 @@ __global__ __launch_bounds__(64 * P / PW, 1) void k_fir_pfft(pfft_args a)
 //   top: request frame f + 1's rows (16 VGPRs in flight through the frame)
 //   A0:  frame f's pass-1 outputs (computed at the end of the previous A) -> set s
 //   B1
-//   A:   the inverse of frame f - 2 (one of waves 0..3, own image); every wave: pass 2, exchange 2,
-//        pass 3, times F_p, products into its image of set s; waves 8..15: the phase sum of frame
+//   A:   the inverse of frame f - 2 (one of waves 4..7, own image); every wave: pass 2, exchange 2,
+//        pass 3, times F_p, products into its image of set s; waves 0..7: the phase sum of frame
 //        f - 1 (set s ^ 1) into Z[(f - 1) & 1]; every wave: frame f + 1's rows -> wave max ->
 //        half-wave swap -> pass 1, kept in registers
 //   B2
@@ -651,14 +651,13 @@ constexpr int IMG2 = 571; // odd: a 16-lane group's exchange-1 stores (16 phases
 #ifndef NSH_PFFT2_ABLATE
 #define NSH_PFFT2_ABLATE 0
 #endif
-#ifndef NSH_PFFT2_SUM_LOW
-#define NSH_PFFT2_SUM_LOW 1 // the phase sum on waves 0..7 (1; r05v: 4 % faster) or 8..15 (0)
-#endif
-#ifndef NSH_PFFT2_PRIO
-#define NSH_PFFT2_PRIO 0 // probe: s_setprio in phase A (1: waves 8..15 -> 1; 2: 12..15 -> 2, 8..11 -> 1; 3: inverse wave -> 3)
-#endif
-#ifndef NSH_PFFT2_LOAD_AT
-#define NSH_PFFT2_LOAD_AT 1 // the next frame's row loads: 1 = after B1 (and the inverse), 0 = at the frame top (r05u: 6 % slower), 2 = waves 8..15 at the top, 0..7 after B1
+// The inverse of a frame runs on wave INV_BASE + (frame & 3), one per SIMD. Waves 4..7 (the
+// second-oldest quartet: the phase sum's waves 0..3 start their transforms without it, and waves
+// 4..7 arrive ~1.8k cycles early at B2 in the phase trace) measured 0.6-0.8 % faster than 0..3 in four two-library
+// A/Bs (r05zq; r05zo 2-3 %); 8..11 and 12..15 are 5-18 % slower (r05zp); after the wave's row loads
+// instead of before them, level or slower (r05zo).
+#ifndef NSH_PFFT2_INV_BASE
+#define NSH_PFFT2_INV_BASE 4
 #endif
 // Row-load cache policy: a frame's rows V .. M - 1 (V >= 384 for Q <= 128) are the next frame's
 // first rows, read again one frame later (mostly L2 hits); rows below V are read for the last
@@ -826,10 +825,11 @@ __global__ __launch_bounds__(64 * P, 1) void k_fir_pfft2(pfft_args a)
         for (int r = 0; r < 8; ++r)
             if (jj + 64 * r >= Q) nsh::buf_store_f2(ro, ob + 512 * r, v[0][r] * u2);
     };
-    // the phase sum of frame fi (products in set fi & 1) into zb[fi & 1], by waves 8..15, in a fixed
-    // order (deterministic)
+    // the phase sum of frame fi (products in set fi & 1) into zb[fi & 1], by waves 0..7, in a fixed
+    // order (deterministic). (The oldest waves: the youngest, last in issue arbitration, wait longest
+    // at their row loads and must not carry the sum as well -- 4 % faster, r05v.)
     auto phase_sum = [&](int64_t fi) {
-        int k = NSH_PFFT2_SUM_LOW ? tid : tid - NT / 2;
+        int k = tid;
         asm volatile("" : "+v"(k));
         const cf* src = sets + (int)(fi & 1) * SET + k;
         cf zz = cf{ 0.f, 0.f };
@@ -847,6 +847,7 @@ __global__ __launch_bounds__(64 * P, 1) void k_fir_pfft2(pfft_args a)
         zb[(int)(fi & 1) * M + k] = cf{ zz.x, -zz.y }; // conj: the inverse runs as a forward transform
     };
 
+    auto inv_wave = [](int64_t fi) { return (int)(fi & 3) + NSH_PFFT2_INV_BASE; };
     // v: the next frame's rows, loaded during the current frame's phase A, then its pass 1
     cf v[8];
     auto pass1_of = [&](int64_t fn) { // rows of frame fn in v -> its wave max in mx[fn & 1], pass 1 in v
@@ -869,11 +870,7 @@ __global__ __launch_bounds__(64 * P, 1) void k_fir_pfft2(pfft_args a)
 #pragma unroll
         for (int r = 1; r < 8; ++r) asm volatile("" : "+v"(t2[r]), "+v"(t3[r]));
         PFFT_T(0);
-        // the next frame's rows, requested here and consumed at the end of this frame's phase A:
-        // ~1.7 us of HBM latency under this load (phase trace), most of a frame
-        nsh::buf_f4 nx[4];
-        if (NSH_PFFT2_LOAD_AT == 0 || (NSH_PFFT2_LOAD_AT == 2 && w >= P / 2))
-            load_rows16<P>(nx, a, n_in, f + 1, f + 1 < f1, e0);
+        nsh::buf_f4 nx[4]; // the next frame's rows, requested after B1
         // A0: frame f's pass-1 outputs (computed at the end of the previous phase A) into set s
 #pragma unroll
         for (int r = 0; r < 8; ++r) cur[e1off + r] = v[r];
@@ -902,24 +899,13 @@ __global__ __launch_bounds__(64 * P, 1) void k_fir_pfft2(pfft_args a)
             nsh::lds_barrier();
         }
 
-        // A: the inverse of frame f - 2 (one of waves 0..3, rotating over the SIMDs), phase w of
-        // frame f, then the phase sum of frame f - 1 (waves 8..15; set s ^ 1 is rewritten only by
-        // frame f + 1's pass 1, after B2)
-        if (NSH_PFFT2_PRIO == 1 && w >= 8) __builtin_amdgcn_s_setprio(1);
-        if (NSH_PFFT2_PRIO == 2 && w >= 12) __builtin_amdgcn_s_setprio(2);
-        if (NSH_PFFT2_PRIO == 2 && w >= 8 && w < 12) __builtin_amdgcn_s_setprio(1);
-        if (inv2 && w == (int)((f - 2) & 3)) {
-            if (NSH_PFFT2_PRIO == 3) __builtin_amdgcn_s_setprio(3);
-            inverse(f - 2, ks2);
-            if (NSH_PFFT2_PRIO == 3) __builtin_amdgcn_s_setprio(0);
-        }
-        if (NSH_PFFT2_LOAD_AT == 1 || (NSH_PFFT2_LOAD_AT == 2 && w < P / 2)) {
-            // the youngest waves (last in issue arbitration) request their rows first
-            if (NSH_PFFT2_PRIO == 4 && w >= 12) __builtin_amdgcn_s_setprio(3);
-            if (NSH_PFFT2_PRIO == 4 && w >= 8 && w < 12) __builtin_amdgcn_s_setprio(2);
-            load_rows16<P>(nx, a, n_in, f + 1, f + 1 < f1, e0);
-            if (NSH_PFFT2_PRIO == 4 && w >= 8) __builtin_amdgcn_s_setprio(0);
-        }
+        // A: the inverse of frame f - 2 (one of waves 4..7, rotating over the SIMDs), the next frame's
+        // rows requested (after B1: 6 % faster than at the frame top, r05u; s_setprio variants and
+        // loads split over phase A slower, r05w, r05x, r05z, r05zb), phase w of frame f, the phase sum
+        // of frame f - 1 (waves 0..7; set s ^ 1 is rewritten only by frame f + 1's pass 1, after B2),
+        // the next frame's pass 1
+        if (inv2 && w == inv_wave(f - 2)) inverse(f - 2, ks2);
+        load_rows16<P>(nx, a, n_in, f + 1, f + 1 < f1, e0);
         PFFT_T(3);
         const int64_t rowf = f * V;
         if (!bad) {
@@ -995,13 +981,12 @@ __global__ __launch_bounds__(64 * P, 1) void k_fir_pfft2(pfft_args a)
                 if (rowf + t < a.n_out) a.out[rowf + t] = make_float2(last[Q + t].x, last[Q + t].y);
         }
         PFFT_T(4);
-        if (sum1 && (NSH_PFFT2_SUM_LOW ? w < P / 2 : w >= P / 2)) phase_sum(f - 1);
+        if (sum1 && w < P / 2) phase_sum(f - 1);
         if (f + 1 < f1) {
             unpack_rows(v, nx);
             pass1_of(f + 1);
         }
         PFFT_T(5);
-        if (NSH_PFFT2_PRIO == 1 || NSH_PFFT2_PRIO == 2) __builtin_amdgcn_s_setprio(0);
         nsh::lds_barrier(); // B2: the products of frame f and Z of frame f - 1 complete
         PFFT_T(6);
         inv2 = sum1;
@@ -1010,11 +995,11 @@ __global__ __launch_bounds__(64 * P, 1) void k_fir_pfft2(pfft_args a)
         ks1 = ks;
     }
     // drain the pipeline: the phase sum of the last frame and the inverses of the last two
-    if (inv2 && w == (int)((f1 - 2) & 3)) inverse(f1 - 2, ks2);
+    if (inv2 && w == inv_wave(f1 - 2)) inverse(f1 - 2, ks2);
     if (sum1) {
-        if (NSH_PFFT2_SUM_LOW ? w < P / 2 : w >= P / 2) phase_sum(f1 - 1);
+        if (w < P / 2) phase_sum(f1 - 1);
         nsh::lds_barrier();
-        if (w == (int)((f1 - 1) & 3)) inverse(f1 - 1, ks1);
+        if (w == inv_wave(f1 - 1)) inverse(f1 - 1, ks1);
     }
 }
 
