@@ -259,7 +259,7 @@ int twiddles(int dev, const float2** tw)
 #define NSH_CHAN_CAP4 16384
 #endif
 #ifndef NSH_CHAN_CAP
-#define NSH_CHAN_CAP 256 // probe builds with NSH_CHAN_FPW != 4
+#define NSH_CHAN_CAP (65536 / NSH_CHAN_FPW) // probe builds with NSH_CHAN_FPW != 4: the same frames per workgroup step
 #endif
 unsigned frame_grid(int64_t nframes, int fw, int64_t cap)
 {
