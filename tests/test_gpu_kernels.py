@@ -822,6 +822,40 @@ def test_fft_roundtrip_large(torch_cuda):
     assert ok, (e, s)
 
 
+@pytest.mark.parametrize("log2n", [27, 28])
+def test_fft_chan_full_size_grid_walk(torch_cuda, log2n):
+    """2^27 and 2^28 samples (C4's batch): more frames than one sweep of the grid-stride walk
+    (fft1024: 24576 workgroups x 4 frames, channelizer: 16384 x 4), so workgroups walk 2-4 frame
+    groups and the last sweep is partial. The frames around each sweep boundary and the last ones
+    against the oracle; ifft(fft(x)) = 1024 x over the whole stream."""
+    torch = torch_cuda
+    n = 1 << log2n
+    nf = n // 1024
+    x = torch.empty(n, dtype=torch.complex64, device="cuda")
+    nsh.synth(x, n, 5 + log2n)
+    X = torch.empty_like(x)
+    nsh.fft1024(x, X, nf)
+    xr = torch.empty_like(x)
+    nsh.fft1024(X, xr, nf, inverse=True)
+    rng = np.random.default_rng(log2n)
+    w = (rng.standard_normal(1024) + 1j * rng.standard_normal(1024)).astype(np.complex64)
+    y = torch.empty_like(x)
+    nsh.channelizer1024(x, y, dev(torch, w), nf)
+    torch.cuda.synchronize()
+    err = (xr / 1024 - x).abs().max().item()
+    assert err <= 1e-5 * x.abs().max().item(), err
+    del xr
+    frames = sorted({f for b in (98304, 196608, 65536, 131072, 196608, 262144) for f in (b - 1, b, b + 1)
+                     if 0 <= f < nf} | {0, nf - 2, nf - 1})
+    xs = np.concatenate([x[1024 * f:1024 * (f + 1)].cpu().numpy() for f in frames])
+    Xs = np.concatenate([X[1024 * f:1024 * (f + 1)].cpu().numpy() for f in frames])
+    ys = np.concatenate([y[1024 * f:1024 * (f + 1)].cpu().numpy() for f in frames])
+    ok, e, s = orc.tol_ok(Xs, orc.fft1024(xs))
+    assert ok, ("fft", e, s)
+    ok, e, s = orc.tol_ok(ys, orc.channelizer1024(xs, w))
+    assert ok, ("channelizer", e, s)
+
+
 @pytest.mark.parametrize("ntaps", [1, 15, 16, 17, 127, 200, 257])
 def test_fir_mfma_f32_exact_class(torch_cuda, ntaps):
     """The exact-fp32 matrix form (k_fir_f32mfma): fp32 products and sums, no split -- its
