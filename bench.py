@@ -93,16 +93,16 @@ def free_port():
         return s.getsockname()[1]
 
 
-def load_pmc_traffic(kernel, samples_per_launch):
-    """HBM bytes per launch from the committed PMC summary (profiles/pmc_fir.json, produced
-    by tools/pmc_summary.py from separate rocprofv3 --pmc passes, gfx950 FETCH_SIZE x2
-    correction applied there), scaled to this launch size. kernel: the template name the
-    plan reports (nsh_fir_plan_kernel), e.g. "k_fir_mfma9<5>"."""
-    p = os.path.join(ROOT, "profiles", "pmc_fir.json")
+def load_pmc_traffic(kernel, samples_per_launch, summary="pmc_fir.json"):
+    """HBM bytes per launch from a committed PMC summary (profiles/pmc_fir.json for the FIR,
+    profiles/pmc_casc.json for the C5 kernel; produced by tools/pmc_summary.py from separate
+    rocprofv3 --pmc passes, gfx950 FETCH_SIZE x2 correction applied there), scaled to this
+    launch size. kernel: the template name as rocprof reports it, e.g. "k_fir_mfma12<5>"."""
+    p = os.path.join(ROOT, "profiles", summary)
     try:
         with open(p) as f:
             d = json.load(f)
-        return float(d[kernel]["hbm_bytes_per_sample"]) * samples_per_launch, d.get("_source", "profiles/pmc_fir.json")
+        return float(d[kernel]["hbm_bytes_per_sample"]) * samples_per_launch, d.get("_source", "profiles/" + summary)
     except (OSError, KeyError, ValueError, TypeError):
         return None, None
 
@@ -384,16 +384,23 @@ def run_c5_fused_leg(a, first, device, barrier, dist, tdev, torch, orc, nsh):
     for _ in range(4):
         xr = orc.fir_ccf(xr, taps, 2)
     ok, err, _ = orc.tol_ok(y[-m:].cpu().numpy(), xr[-m:])
+    kernel = plan.kernel
     plan.close()
     achieved = 8.5 * n / (avg_ms * 1e-3) / 1e9
     world = dist.get_world_size() if dist is not None else 1
-    return {"kernel": plan.kernel, "workload": "C5: 4 x fir_filter_ccf(firwin(127,0.45), 2) fused into one "
-            "fir_filter_cascade_ccf, 2^%d resident input samples per GPU" % a.c5_fused_log2n,
-            "steps": steps, "value": round(world * n * steps / el / 1e6, 1), "unit": "MSamples/s (input)",
-            "avg_launch_us": round(avg_ms * 1e3, 2), "achieved_GBs": round(achieved, 1),
-            "bytes_per_input_sample": 8.5, "frac": round(achieved / HBM_PEAK_GBS, 4), "clock_mhz": mhz,
-            "parity": {"check": "last 4096 outputs vs the oracle's 4-stage chain (double accumulation)",
-                       "max_abs_err": err, "ok": bool(ok)}}
+    out = {"kernel": kernel, "workload": "C5: 4 x fir_filter_ccf(firwin(127,0.45), 2) fused into one "
+           "fir_filter_cascade_ccf, 2^%d resident input samples per GPU" % a.c5_fused_log2n,
+           "steps": steps, "value": round(world * n * steps / el / 1e6, 1), "unit": "MSamples/s (input)",
+           "avg_launch_us": round(avg_ms * 1e3, 2), "achieved_GBs": round(achieved, 1),
+           "bytes_per_input_sample": 8.5, "frac": round(achieved / HBM_PEAK_GBS, 4), "clock_mhz": mhz,
+           "parity": {"check": "last 4096 outputs vs the oracle's 4-stage chain (double accumulation)",
+                      "max_abs_err": err, "ok": bool(ok)}}
+    tr, src = load_pmc_traffic(kernel, n, "pmc_casc.json")
+    if tr is not None:
+        out["traffic"] = int(tr)
+        out["traffic_source"] = ("HBM B/input sample from separate rocprofv3 --pmc passes (%s), scaled to this "
+                                 "launch size; not measured in this run" % src)
+    return out
 
 
 def main():
