@@ -17,6 +17,9 @@
 // so a frame costs P forward 512-point FFTs, a P-term complex MAC per bin and one inverse
 // FFT -- about 60 FLOP per input sample instead of the cascade's ~480 (direct or Toeplitz).
 //
+// Kernels: k_fir_pfft2<16> (below; the default at P = 16 since round 5: no ring, two image sets, the
+// phase sum and the inverse pipelined into the next frames) and k_fir_pfft<P> (P = 8, and P = 16
+// with NSH_PFFT_FORM=1), which works as follows.
 // Kernel k_fir_pfft<P>: one workgroup of P waves per CU, walking a contiguous range of frames.
 //   * LDS ring of M rows x P samples (row = one P-sample input row, XOR-swizzled so that wave p
 //     reading phase p of 64 consecutive rows is bank-conflict-free); a frame shares Q rows with
@@ -614,31 +617,30 @@ __global__ __launch_bounds__(64 * P / PW, 1) void k_fir_pfft(pfft_args a)
 
 // ---- k_fir_pfft2: the P = 16 frame without a ring, phase images double-buffered (round 5) ----
 //
-// Opt-in (NSH_PFFT_FORM=2 at plan creation; tests run both forms). The form above spends a quarter
-// of each frame in phase B (the phase sum and the ring stores, between its two barriers) with the
-// VALU idle, and a second product set to overlap it with the next frame's transforms does not fit
-// next to the 64 KiB ring. This form drops the ring: each lane loads its rows straight from HBM in
-// 16-B loads and a half-wave swap regroups them the way Stockham's first pass wants (lane l of wave
-// w ends with one phase at window rows 4 w + g + 64 r, r = 0..7; load_frame), runs pass 1 in
-// registers and stores its outputs into that phase's image: exchange 1 becomes the cross-wave
-// row -> phase transpose the ring did. The Q overlap rows a frame shares with the previous one are
-// loaded again (mostly L2 hits: 9.04 vs 8.65 HBM B per input sample, PMC r05o). With the ring gone,
-// two sets of 16 phase images fit (frame f in set f & 1), and the frame pipelines:
-//   top: request frame f + 1's rows (16 VGPRs in flight through the frame)
+// The default C5 form since r05za (NSH_PFFT_FORM=1 selects the ring form above at plan creation;
+// the tests run both). The ring form spends a quarter of each frame in phase B (the phase sum and
+// the ring stores, between its two barriers) with the VALU idle, and a second product set to overlap
+// it with the next frame's transforms does not fit next to the 64 KiB ring. This form drops the
+// ring: each lane loads its rows straight from HBM in 16-B loads and a half-wave swap regroups them
+// the way Stockham's first pass wants (lane l of wave w ends with one phase at window rows
+// 4 w + g + 64 r, r = 0..7; load_frame), runs pass 1 in registers and stores its outputs into that
+// phase's image: exchange 1 becomes the cross-wave row -> phase transpose the ring did. The Q
+// overlap rows a frame shares with the previous one are loaded again, as L2 hits (the split cache
+// policy below: 8.66 HBM B per input sample, as the ring form's 8.65). With the ring gone, two sets
+// of 16 phase images fit (frame f in set f & 1), and the frame pipelines:
 //   A0:  frame f's pass-1 outputs (computed at the end of the previous A) -> set s
 //   B1
-//   A:   the inverse of frame f - 2 (one of waves 4..7, own image); every wave: pass 2, exchange 2,
-//        pass 3, times F_p, products into its image of set s; waves 0..7: the phase sum of frame
-//        f - 1 (set s ^ 1) into Z[(f - 1) & 1]; every wave: frame f + 1's rows -> wave max ->
-//        half-wave swap -> pass 1, kept in registers
+//   A:   the inverse of frame f - 2 (one of waves 4..7, own image); every wave: frame f + 1's row
+//        loads issued (16 VGPRs), pass 2, exchange 2, pass 3, times F_p, products into its image of
+//        set s; waves 0..7: the phase sum of frame f - 1 (set s ^ 1) into Z[(f - 1) & 1]; every
+//        wave: frame f + 1's rows -> wave max -> half-wave swap -> pass 1, kept in registers
 //   B2
-// Measured (profiles/r05g-r05o, one process against k_fir_pfft): correct (the pfft suite on both
-// forms), 32 % fewer LDS-active cycles and no bank conflicts, the same VALU and load counts -- and
-// 0-11 % slower: without its row loads it runs 519 us per 2^28 inputs (k_fir_pfft without its
-// loads ~525), its loads then cost ~110 us against ~45 for k_fir_pfft's, the wave's vector-memory
-// issue busy twice as long per load instruction. Two earlier shapes lost more: 8-B loads (128 load
-// instructions per frame held the late waves 2-4k cycles at issue) and a load path whose register
-// copies waited for the loads right after issuing them.
+// Measured (profiles/r05g-r05zs): 32 % fewer LDS-active cycles than the ring form and
+// no bank conflicts, the same VALU and load counts; 2.2-2.5 % faster than the ring form once its
+// loads sat after B1 and the phase sum on the oldest waves (r05u, r05v, r05y). Without its row loads
+// it runs ~520 us per 2^28 inputs; what the loads cost depends on how their issue interleaves with
+// the young waves' transforms, not on their count (a row-reusing hop with 25 % fewer loads was 4 %
+// slower, r05zd, r05zm).
 // Scaling: the frame's maximum is known only after B1 (each wave sees its own rows), so pass 1 runs
 // unscaled and the 2^k scale multiplies its outputs -- exact, and pass 1 cannot overflow or lose
 // precision to subnormals for frames whose maximum lies in [2^-100, 2^124); a frame outside that
