@@ -830,8 +830,8 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma11(const float2* __restrict_
 }
 
 // ---- k_fir_mfma13: the decimators' lockstep walk, exact chunks queued (round 5) ------------
-#ifndef NSH_V13_XWIN
-#define NSH_V13_XWIN 0
+#ifndef NSH_V13_AUX // chunk loads' cache policy: nontemporal on whole-line loads (no line is read twice)
+#define NSH_V13_AUX (NSH_V13_CLOAD ? 2 : D == 2 ? NSH_V11_AUX2 : NSH_V11_AUX4)
 #endif
 // k_fir_mfma11's per-chunk work (polyphase split at a per-chunk scale, the same MFMA tile) in a
 // different walk: the persistent workgroups of an XCD (x = blockIdx mod 8, W of them) take its
@@ -846,6 +846,13 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma11(const float2* __restrict_
 // them to the launch's exact queue and k_fir_exact13 (same stream, right after) filters them -- so a
 // periodic pattern of exact chunks, which the lockstep walk would put on one workgroup per XCD,
 // cannot unbalance it (r04zw: every 64th chunk exact 968 vs 548 us with the exact forms inline).
+// the chunk's float4 (2 input samples) a lane loads as its unit u, instruction f: the wave's
+// 64 D float4 of unit u in D contiguous 1 KiB runs
+template <int D>
+__device__ __forceinline__ int q13(int u, int f)
+{
+    return 64 * D * ((int)(threadIdx.x >> 6) + 4 * u) + 64 * f + (int)(threadIdx.x & 63);
+}
 template <int D, int QH>
 __device__ __forceinline__ void load13(const float2* __restrict__ in, const float2* __restrict__ hist_in, int L, int64_t n_in,
                                        int64_t ch, float4 (&v)[4], float4& hv)
@@ -857,8 +864,10 @@ __device__ __forceinline__ void load13(const float2* __restrict__ in, const floa
     for (int u = 0; u < G::UNITS; ++u)
 #pragma unroll
         for (int f = 0; f < D; ++f) {
-            const nsh::buf_f4 t = __builtin_bit_cast(
-                nsh::buf_f4, __builtin_amdgcn_raw_buffer_load_b128(r, ((tid + G::NT * u) * D + f) * 16, 0, D == 2 ? NSH_V11_AUX2 : NSH_V11_AUX4));
+            // NSH_V13_CLOAD: float4 q13(u, f) of the chunk (each instruction 1 KiB contiguous), else
+            // (tid + NT u) D + f (a thread's D float4 adjacent, each instruction spread over D KiB)
+            const int q = NSH_V13_CLOAD ? q13<D>(u, f) : (tid + G::NT * u) * D + f;
+            const nsh::buf_f4 t = __builtin_bit_cast(nsh::buf_f4, __builtin_amdgcn_raw_buffer_load_b128(r, q * 16, 0, NSH_V13_AUX));
             v[u * D + f] = make_float4(t.x, t.y, t.z, t.w);
         }
     // the halo: input samples [ch CHUNK_IN - 2 HP, ch CHUNK_IN), two per thread tid < HP, from `in`
@@ -915,15 +924,9 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma13(const float2* __restrict_
 
     const int64_t nchunks = (n_out + G::CHUNK - 1) / G::CHUNK;
     const int W = (int)(gridDim.x >> 3);
-#if NSH_V13_XWIN
-    // probe form: one global lockstep row -- at step i XCD x takes window 8 i + x of W chunks
-    const int64_t xe = nchunks, c_first = (int64_t)(blockIdx.x & 7) * W + (blockIdx.x >> 3), hop = 8 * (int64_t)W;
-    (void)per_x;
-#else
     const int64_t xb = (int64_t)(blockIdx.x & 7) * per_x;
     const int64_t xe = xb + per_x < nchunks ? xb + per_x : nchunks;
     const int64_t c_first = xb + (blockIdx.x >> 3), hop = W;
-#endif
     if (c_first >= xe) return; // whole workgroup, before any barrier
     // the workgroup's i-th chunk; past its range an empty buffer range (loads return 0)
     auto chunk_at = [&](int64_t i) { const int64_t c = c_first + i * hop; return c < xe ? c : nchunks; };
@@ -972,6 +975,32 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma13(const float2* __restrict_
             const float2 a = f4_sample(hsrc[pa >> 1], pa & 1), bb = f4_sample(hsrc[pb >> 1], pb & 1);
             store_pair11<D, QH>(buf, r, 2 * pi, a.x, bb.x, a.y, bb.y, sc);
         }
+#if NSH_V13_CLOAD
+        // float4 q holds samples 2q, 2q + 1: phase offsets 2q mod D (+1) at time 2q / D, the pair
+        // 2q / 2D, its time bit k = q & (D / 2). Lanes q and q ^ (D / 2) hold the same offsets at the
+        // pair's two times: each keeps offset k and takes the partner's (one DPP exchange per float),
+        // then stores one phase pair -- all D phases in each store instruction (PH padded for it)
+        constexpr int XCHG = D == 4 ? 0x4e : 0xb1; // quad_perm [2,3,0,1] / [1,0,3,2]: lane ^ (D / 2)
+#pragma unroll
+        for (int u = 0; u < G::UNITS; ++u)
+#pragma unroll
+            for (int f = 0; f < D; ++f) {
+                const int q = q13<D>(u, f);
+                const bool k = (q & (D / 2)) != 0;
+                const float4 x = v[u * D + f];
+                const float kre = k ? x.z : x.x, kim = k ? x.w : x.y; // offset k: kept
+                const float sre = k ? x.x : x.z, sim = k ? x.y : x.w; // offset 1 - k: the partner's
+                const float rre = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(sre), XCHG, 0xf, 0xf, true));
+                const float rim = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(sim), XCHG, 0xf, 0xf, true));
+                const int sr = D == 4 ? 2 * (q & 1) + (int)k : (int)k;
+                const int r = sr == 0 ? 0 : D - sr;
+                const int s = G::H + 2 * (q / D);
+                if (k)
+                    store_pair11<D, QH>(buf, r, s, rre, kre, rim, kim, sc);
+                else
+                    store_pair11<D, QH>(buf, r, s, kre, rre, kim, rim, sc);
+            }
+#else
 #pragma unroll
         for (int u = 0; u < G::UNITS; ++u) {
             const int i0 = 2 * (tid + G::NT * u);
@@ -984,6 +1013,7 @@ __global__ __launch_bounds__(256, 2) void k_fir_mfma13(const float2* __restrict_
                 store_pair11<D, QH>(buf, r, G::H + i0, a.x, bb.x, a.y, bb.y, sc);
             }
         }
+#endif
     };
     auto mfma_tile = [&](const unsigned char* cur, int unscale, nf2 (&o)[2 * G::TILES]) {
         f32x4 hi[G::TILES], lo[G::TILES], hi_t[G::TILES], lo_t[G::TILES];
@@ -1179,20 +1209,21 @@ __global__ __launch_bounds__(256) void k_fir_exact13(const float2* __restrict__ 
         const bool f32t = !(e & 1u);
         float4 v[4], hv;
         load13<D, QH>(in, hist_in, L, n_in, ch, v, hv);
+        auto q_of = [&](int u, int f) { return NSH_V13_CLOAD ? q13<D>(u, f) : (tid + G::NT * u) * D + f; }; // load13's float4
         nsh::lds_barrier(); // the previous chunk's reads of LDS are done
         if (f32t) {
             if (tid < G::HP) nsh_f32t::put<GF>(lds, hv, 2 * tid);
 #pragma unroll
             for (int u = 0; u < G::UNITS; ++u)
 #pragma unroll
-                for (int f = 0; f < D; ++f) nsh_f32t::put<GF>(lds, v[u * D + f], GF::H + 2 * ((tid + G::NT * u) * D + f));
+                for (int f = 0; f < D; ++f) nsh_f32t::put<GF>(lds, v[u * D + f], GF::H + 2 * q_of(u, f));
         } else {
             float4* rb = reinterpret_cast<float4*>(lds);
             if (tid < G::HP) rb[tid] = hv;
 #pragma unroll
             for (int u = 0; u < G::UNITS; ++u)
 #pragma unroll
-                for (int f = 0; f < D; ++f) rb[G::HP + (tid + G::NT * u) * D + f] = v[u * D + f];
+                for (int f = 0; f < D; ++f) rb[G::HP + q_of(u, f)] = v[u * D + f];
         }
         nsh::lds_barrier();
         nf2 o[2 * G::TILES];

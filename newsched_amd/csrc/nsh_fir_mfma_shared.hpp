@@ -235,6 +235,14 @@ __device__ __forceinline__ void direct_tile9(const unsigned char* lds, const flo
 #ifndef NSH_DECIM2_SHARED // A/B switch: D = 2 on the shared-input exact path (one pair at a time)
 #define NSH_DECIM2_SHARED 0
 #endif
+#ifndef NSH_V13_CLOAD
+// k_fir_mfma13: each chunk-load instruction reads 1 KiB contiguous (nontemporal), lane pairs exchange
+// their samples by DPP before the split stores; 0 = a thread's D float4 side by side (each
+// instruction spread over D KiB, default cache policy). D = 4, bit-identical: faster on three boxes
+// of four (72.5 vs 70.1 %, r05ze; ~1 % in four two-library A/Bs each on two more, r05zzd), 1.3 %
+// slower on one (r05zg)
+#define NSH_V13_CLOAD 1
+#endif
 template <int D, int QH>
 struct geom11 {
     static constexpr int NT = 256;
@@ -249,8 +257,11 @@ struct geom11 {
     static constexpr int NB = (CHUNK + H) / 16;
     static constexpr int PLANE = NB * 32;
     static constexpr int IM_OFF = (2 * PLANE + 255) / 256 * 256 + 128;
-    static constexpr int PH = (IM_OFF + 2 * PLANE + 255) / 256 * 256;
-    static constexpr int BUF = D * PH;
+    // phase planes PH apart; k_fir_mfma13's split stores (NSH_V13_CLOAD) write all D phases in one
+    // instruction, 32 / D pairs each per 32-lane group: PH = 32 * (4 / D) mod 128 B puts them on
+    // disjoint banks
+    static constexpr int PH = (IM_OFF + 2 * PLANE + 255) / 256 * 256 + (NSH_V13_CLOAD ? 128 / D : 0);
+    static constexpr int BUF = (D * PH + 255) / 256 * 256;
     static constexpr int HP = D * H / 2;                      // halo float4 (2 input samples each)
     static constexpr int STASH = HP * 16;
     static constexpr int SLOTS = 2 * BUF + 2 * STASH;
