@@ -1353,7 +1353,7 @@ int launch_v11(const nsh_fir_plan* p, const float2* in, const float2* hin, float
 
 // The lockstep walk (k_fir_mfma13 + k_fir_exact13) for decim D, the contiguous walk
 // (k_fir_mfma11, exact forms inline) otherwise: bit D of the plan's dec_walk, set at plan creation
-// from NSH_DEC_WALK_MASK (environment; default below: D = 4 only) -- tests run both walks.
+// from NSH_DEC_WALK_MASK (environment; default below: D = 2 and 4) -- tests run both walks.
 template <int D, int QH>
 int launch_v13(const nsh_fir_plan* p, const float2* in, const float2* hin, float2* hout, float2* out, int64_t n_out,
                hipStream_t s)
@@ -1485,8 +1485,11 @@ static hipError_t f32_tile_image(nsh_fir_plan* p, int QF)
     return e;
 }
 
+// bit D: decim D on the lockstep walk (k_fir_mfma13) -- D = 4 since round 5 (r05b), D = 2 since its
+// whole-line loads (1.6 % faster, also with exact chunks every 4th / 64th chunk, bit-identical on
+// finite input, r05zzg, r05zzh); 0 selects the contiguous walk k_fir_mfma11 (tests run both)
 #ifndef NSH_DEC_WALK_MASK
-#define NSH_DEC_WALK_MASK 16
+#define NSH_DEC_WALK_MASK 20
 #endif
 int nsh_fir_mfma_prepare_decim(nsh_fir_plan* p)
 {

@@ -575,7 +575,7 @@ def test_fir_mfma_exact_paths(torch_cuda, v8_form, ntaps, decim, kind):
     plan = nsh.FirPlan(h, decim, nsh.FIR_MFMA)
     if ntaps == 127:
         assert plan.kernel.startswith({1: "k_fir_mfma12",
-                                       2: "k_fir_mfma11", 4: "k_fir_mfma13"}[decim]), plan.kernel
+                                       2: "k_fir_mfma13", 4: "k_fir_mfma13"}[decim]), plan.kernel
     y, hy = run_fir(torch, plan, x, n // decim)
     yd, hd = run_fir(torch, nsh.FirPlan(h, decim, nsh.FIR_DIRECT), x, n // decim)
     np.testing.assert_array_equal(hy.view(np.uint32), hd.view(np.uint32))
@@ -704,7 +704,7 @@ def test_fir_mfma_exact_tile_mixed_stream(torch_cuda, ntaps, decim):
     for c in rng.choice(23, 4, replace=False):
         x[c * 2048 + int(rng.integers(0, 2048))] *= np.float32(2.0 ** -35)
     plan = nsh.FirPlan(h, decim, nsh.FIR_MFMA)
-    assert plan.kernel.startswith({1: "k_fir_mfma12", 2: "k_fir_mfma11", 4: "k_fir_mfma13"}[decim]), plan.kernel
+    assert plan.kernel.startswith({1: "k_fir_mfma12", 2: "k_fir_mfma13", 4: "k_fir_mfma13"}[decim]), plan.kernel
     n1 = 9 * (2048 // decim) + 333  # first call: ends inside a chunk
     y1, h1 = run_fir(torch, plan, x[: n1 * decim], n1)
     y2, _ = run_fir(torch, plan, x[n1 * decim:], n_out - n1, hist=h1)
@@ -771,7 +771,7 @@ def test_fir_plan_kernels():
     assert nsh.FirPlan(h, 1, nsh.FIR_MFMA).kernel == "k_fir_mfma12<5>"
     assert nsh.FirPlan(h, 1, nsh.FIR_AUTO).kernel == "k_fir_mfma12<5>"
     assert nsh.FirPlan(h, 1, nsh.FIR_DIRECT).kernel == "k_fir_direct<1,8>"
-    assert nsh.FirPlan(h, 2, nsh.FIR_MFMA).kernel == "k_fir_mfma11<2,5>"
+    assert nsh.FirPlan(h, 2, nsh.FIR_MFMA).kernel == "k_fir_mfma13<2,5>"  # the lockstep walk at D = 2 too (r05zzg)
     assert nsh.FirPlan(h, 4, nsh.FIR_MFMA).kernel == "k_fir_mfma13<4,3>"  # the lockstep walk (round 5)
     for L in (1, 17, 33, 65, 97, 129, 161):
         assert nsh.FirPlan(np.ones(L, np.float32), 1, nsh.FIR_MFMA).kernel == "k_fir_mfma12<%d>" % ((L + 30) // 32 + 1)
