@@ -285,12 +285,12 @@ def run_fp32_leg(a, n, taps, first, device, barrier, dist, tdev, torch, orc, nsr
     launches = st["launches"] - l0
     kms, samples = st["kernel_ms"] - st0["kernel_ms"], st["samples"] - st0["samples"]
     avg_ms = kms / launches
-    mhz = leg_clock(lambda: [fb.run() for _ in range(10)], nsh)
     m = 4096
-    y = fb.tail(m)
+    y = fb.tail(m)  # the timed runs' last output, before the clock's repeats
     lo = first + n - m - (taps.size - 1)
     xw = orc.synth(m + taps.size - 1, lo)
     ok, err, _ = orc.tol_ok(y, orc.fir_ccf(xw[taps.size - 1:], taps, hist=xw[: taps.size - 1]))
+    mhz = leg_clock(lambda: [fb.run() for _ in range(10)], nsh)
     fb.close()
     achieved = BYTES_PER_SAMPLE * (samples / launches) / (avg_ms * 1e-3) / 1e9
     world = dist.get_world_size() if dist is not None else 1
@@ -330,6 +330,127 @@ def run_copy_leg(n, barrier, torch, nsh):
     gbs = BYTES_PER_SAMPLE * n / (ms * 1e-3) / 1e9
     return {"kernel": "k_copy_v4", "avg_launch_us": round(ms * 1e3, 2), "GBs": round(gbs, 1),
             "frac_of_peak": round(gbs / HBM_PEAK_GBS, 4)}
+
+
+C2_KS = [complex(np.float32(np.cos(t)), np.float32(np.sin(t))) for t in (0.1, 0.2, 0.3, 0.4)]  # e^{j{.1,.2,.3,.4}}
+
+
+def c4_weights():
+    """C4's channel weights W[b] = (1 + cos(2 pi b / 1024) / 2) / 1024 (real, complex64)."""
+    b = np.arange(1024)
+    return ((1.0 + 0.5 * np.cos(2 * np.pi * b / 1024.0)) / 1024.0).astype(np.complex64)
+
+
+def chain_specs(a):
+    """The single-GPU BASELINE configs other than C3 (and C5's fused chain), as scheduler_hip
+    flowgraphs over an HBM-resident input ring (nsr.ChainBench): name -> spec."""
+    n = 1 << a.legs_log2n
+    taps_d = firwin(127, 0.45)  # the C5 stage filter, alone, at D = 2 and 4
+    return {
+        "c2": dict(kind="CHAIN_MUL_CONST_CC", params=C2_KS, decim=1, n=n, bps=16.0,
+                   workload="C2: 4 x hip::multiply_const_cc (k = e^{j{0.1,0.2,0.3,0.4}}) fused by scheduler_hip into one "
+                            "launch per work(), 2^%d-sample batches" % a.legs_log2n),
+        "c4": dict(kind="CHAIN_CHANNELIZER", params=c4_weights(), decim=1, n=n, bps=16.0,
+                   workload="C4: hip::fft_vcc(1024) -> hip::multiply_const_vcc(W) -> hip::fft_vcc(1024, inverse) fused by "
+                            "scheduler_hip into the channelizer, 2^%d samples (2^%d frames) per batch"
+                            % (a.legs_log2n, a.legs_log2n - 10)),
+        "decim2": dict(kind="CHAIN_FIR", params=taps_d, decim=2, n=n, bps=8.0 + 8.0 / 2,
+                       workload="hip::fir_filter_ccf(firwin(127,0.45), decim 2), 2^%d input samples per batch" % a.legs_log2n),
+        "decim4": dict(kind="CHAIN_FIR", params=taps_d, decim=4, n=n, bps=8.0 + 8.0 / 4,
+                       workload="hip::fir_filter_ccf(firwin(127,0.45), decim 4), 2^%d input samples per batch" % a.legs_log2n),
+    }
+
+
+def chain_parity(name, spec, y, first, orc):
+    """Tail of the last batch vs the oracle: C2 bit-exact, the rest within the north-star 1e-5."""
+    n, m = spec["n"], y.size
+    if name == "c2":
+        ref = orc.mul_const_chain_cc(orc.synth(m, first + n - m), spec["params"])
+        ok = bool(np.array_equal(y.view(np.uint64), ref.view(np.uint64)))
+        return {"check": "last %d outputs bit-exact vs the oracle's chain" % m, "ok": ok,
+                "mismatches": int(np.count_nonzero(y.view(np.uint64) != ref.view(np.uint64)))}
+    if name == "c4":
+        ref = orc.channelizer1024(orc.synth(m, first + n - m), spec["params"])
+        ok, err, scale = orc.tol_ok(y, ref)
+        return {"check": "last %d frame(s) vs the oracle's double-precision DFT channelizer" % (m // 1024),
+                "max_abs_err": err, "scale": scale, "ok": bool(ok)}
+    D, taps = spec["decim"], spec["params"]
+    L1 = taps.size - 1  # the window lies inside the batch (its history: the batch's own samples)
+    xw = orc.synth(m * D + L1, first + n - m * D - L1)
+    ok, err, scale = orc.tol_ok(y, orc.fir_ccf(xw[L1:], taps, D, hist=xw[:L1]))
+    return {"check": "last %d outputs vs the oracle (double accumulation)" % m, "max_abs_err": err, "scale": scale,
+            "ok": bool(ok)}
+
+
+def run_chain_leg(a, name, spec, rank, device, barrier, dist, tdev, torch, orc, nsr, nsh):
+    """One config as a scheduler_hip flowgraph streaming K batches in one run (as the headline):
+    wall rate, HIP-event time of every launch of the (fused) block that does the work
+    (scheduler_hip kernel timing), the shader clock, and the last batch's tail against the oracle."""
+    n, D = spec["n"], spec["decim"]
+    first = rank * n
+    fb = nsr.ChainBench(getattr(nsr, spec["kind"]), spec["params"], n, device=device, decim=D, first_index=first,
+                        out_buf_bytes=max(64 << 20, n * 8 // D))
+    try:
+        t0 = time.perf_counter()
+        fb.set_batches(4)
+        while time.perf_counter() - t0 < a.legs_warmup_s:
+            fb.run()
+        steps = max(5, a.steps // 4)
+        fb.set_batches(steps)
+        barrier()
+        st0 = fb.stats()
+        t0 = time.perf_counter()
+        fb.run()
+        barrier()
+        el = time.perf_counter() - t0
+        if dist is not None:
+            t = torch.tensor([el], dtype=torch.float64, device=tdev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        st = fb.stats()
+        m = 4096 if name != "c4" else 2048
+        par = chain_parity(name, spec, fb.tail(m), first, orc)  # the timed run's last batch
+
+        def more():
+            fb.set_batches(16)
+            fb.run()
+
+        mhz = leg_clock(more, nsh)
+    finally:
+        fb.close()
+    launches = st["launches"] - st0["launches"]
+    kms = st["kernel_ms"] - st0["kernel_ms"]
+    in_samples = (st["samples"] - st0["samples"]) * D
+    avg_ms = kms / launches
+    achieved = spec["bps"] * (in_samples / launches) / (avg_ms * 1e-3) / 1e9
+    world = dist.get_world_size() if dist is not None else 1
+    return {"workload": spec["workload"], "block": st["block"], "launching_blocks": st["launching_blocks"],
+            "steps": steps, "value": round(world * n * steps / el / 1e6, 1), "unit": "MSamples/s (input)",
+            "ms_per_step": round(el / steps * 1e3, 4), "timed_launches": launches,
+            "avg_launch_us": round(avg_ms * 1e3, 2), "bytes_per_input_sample": spec["bps"],
+            "achieved_GBs": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "flowgraph_frac": round(spec["bps"] * n / (el / steps) / 1e9 / HBM_PEAK_GBS, 4),
+            "clock_mhz": mhz, "parity": par}
+
+
+def run_c1_leg(reps=7):
+    """BASELINE C1 on the host (the reference's bm_copy flowgraph): null_source -> head(2^20) ->
+    copy -> null_sink on scheduler_mt, 32 KiB buffers, median of `reps` runs."""
+    runs = [nsr_c1_run() for _ in range(reps)]
+    secs = sorted(r[0] for r in runs)
+    med = secs[len(secs) // 2]
+    return {"workload": "C1: null_source -> head(2^20) -> copy -> null_sink, scheduler_mt thread per block, "
+                        "vmcircbuf 32 KiB buffers (CPU only)", "value": round((1 << 20) / med / 1e6, 2),
+            "unit": "MSamples/s", "median_of": reps, "ms_per_run": round(med * 1e3, 3), "threads": runs[0][1],
+            "us_per_4096_item_call": round(med / ((1 << 20) / 4096) * 1e6, 2),
+            "note": "drain-based termination: the reference's fixed 100 ms sleep per run "
+                    "(runtime/lib/flowgraph_monitor.cpp:27) is not paid"}
+
+
+def nsr_c1_run():
+    from newsched_amd import nsr
+
+    return nsr.c1_run(1 << 20, 32768)
 
 
 def run_c5_fused_leg(a, first, device, barrier, dist, tdev, torch, orc, nsh):
@@ -377,13 +498,13 @@ def run_c5_fused_leg(a, first, device, barrier, dist, tdev, torch, orc, nsh):
                 plan(x, hist, hout, y, n_out, stream=s)
         s.synchronize()
 
-    mhz = leg_clock(more, nsh)
     m = 4096
     lo = first + n - 16 * m - C5_HALO
     xr = orc.synth(16 * m + C5_HALO, lo)
     for _ in range(4):
         xr = orc.fir_ccf(xr, taps, 2)
-    ok, err, _ = orc.tol_ok(y[-m:].cpu().numpy(), xr[-m:])
+    ok, err, _ = orc.tol_ok(y[-m:].cpu().numpy(), xr[-m:])  # the timed launches' output
+    mhz = leg_clock(more, nsh)
     kernel = plan.kernel
     plan.close()
     achieved = 8.5 * n / (avg_ms * 1e-3) / 1e9
@@ -424,6 +545,10 @@ def main():
     ap.add_argument("--c5-fused", choices=["on", "off"], default="on",
                     help="C5's chain as the fused kernel (k_fir_pfft2<16>) on resident input, every rank")
     ap.add_argument("--c5-fused-log2n", type=int, default=28)
+    ap.add_argument("--legs", choices=["on", "off"], default="on",
+                    help="the other single-GPU configs beside the headline: C1 (CPU), C2, C4, decimators D=2/4")
+    ap.add_argument("--legs-log2n", type=int, default=28)
+    ap.add_argument("--legs-warmup-s", type=float, default=0.3)
     ap.add_argument("--c5-log2n", type=int, default=26)
     ap.add_argument("--c5-steps", type=int, default=5)
     ap.add_argument("--c5-warmup", type=int, default=2)
@@ -513,6 +638,15 @@ def main():
         elapsed = float(t.item())
     st = fb.stats()
 
+    # parity on the measured path: the last 4096 outputs of the timed run vs the oracle, read
+    # before anything else runs the flowgraph again
+    m = 4096
+    y = fb.tail(m)
+    lo = first + n - m - (taps.size - 1)
+    xw = orc.synth(m + taps.size - 1, lo)
+    y_ref = orc.fir_ccf(xw[taps.size - 1:], taps, hist=xw[: taps.size - 1])
+    ok, err, scale = orc.tol_ok(y, y_ref)
+
     def more():  # untimed: the clock the FIR runs at under the same stream of batches
         fb.set_batches(24)
         fb.run()
@@ -528,13 +662,6 @@ def main():
     avg_launch_ms = kms / timed_launches
     achieved = BYTES_PER_SAMPLE * per_launch_samples / (avg_launch_ms * 1e-3) / 1e9  # GB/s
 
-    # parity on the measured path: the last 4096 outputs of the last run vs the oracle
-    m = 4096
-    y = fb.tail(m)
-    lo = first + n - m - (taps.size - 1)
-    xw = orc.synth(m + taps.size - 1, lo)
-    y_ref = orc.fir_ccf(xw[taps.size - 1:], taps, hist=xw[: taps.size - 1])
-    ok, err, scale = orc.tol_ok(y, y_ref)
     if dist is not None:  # every rank's shard tail must pass; report the worst error
         r = torch.tensor([0.0 if ok else 1.0, err], dtype=torch.float64, device=tdev)
         dist.all_reduce(r, op=dist.ReduceOp.MAX)
@@ -556,6 +683,9 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
+        "arith": "complex fp32 in and out; 127-tap products as a three-product fp16x2 operand split on the fp16 "
+                 "matrix cores with fp32 accumulation (k_fir_mfma12), chunks the split cannot hold on exact fp32 paths; "
+                 "the fp32-by-instruction form is the fp32_exact leg",
         "data": "synthetic: counter-based splitmix64 complex-float stream (BASELINE.md §2), HBM-resident before timing",
         "config": {
             "workload": "C3: 127-tap fir_filter_ccf (firwin(127,0.2) fp32 taps) over 2^%d-sample complex-float batches per GPU, "
@@ -586,7 +716,7 @@ def main():
             "overhead_us_per_step": round(step_us - avg_launch_ms * 1e3 * launches_per_run, 2),  # incl. the run's start / drain
             "clock_mhz": clock_mhz,  # shader clock over an untimed repeat (leg_clock)
         },
-        "parity": {"check": "last 4096 outputs of the last step vs oracle (double accumulation), every rank",
+        "parity": {"check": "last 4096 outputs of the timed run's last step vs oracle (double accumulation), every rank",
                    "max_abs_err": err, "scale": scale, "ok": bool(ok)},
     }
     cp = run_copy_leg(n, barrier, torch, nsh)
@@ -606,6 +736,15 @@ def main():
     if a.c5_fused == "on":
         out["c5_fused"] = run_c5_fused_leg(a, rank * (1 << a.c5_fused_log2n), device, barrier, dist, tdev, torch, orc, nsh)
 
+    if a.legs == "on":
+        for name, spec in chain_specs(a).items():
+            try:
+                out[name] = run_chain_leg(a, name, spec, rank, device, barrier, dist, tdev, torch, orc, nsr, nsh)
+            except Exception as e:  # reported, not fatal: the headline is already measured
+                out[name] = {"error": str(e)[:300]}
+        if rank == 0:
+            out["c1"] = run_c1_leg()
+
     if a.c5 == "on" or (a.c5 == "auto" and world > 1):
         out["c5_pipeline"] = run_c5(a, dist, backend, rank, world, device, torch, orc, nsr)
         abandoned = out["c5_pipeline"].pop("_abandoned_any")
@@ -614,6 +753,9 @@ def main():
         ncpu = 1 << a.cpu_log2n
         xs = orc.synth(1 << 20)  # vector_source data (repeated)
         secs, threads = nsr.cpu_fir_run(taps, xs, ncpu, fixed_buf_size=32768, with_threads=True)
+        n_wo = 1 << 24  # the FIR arithmetic alone: the same block's filter() on 4096-sample calls
+        wsecs, isa = nsr.cpu_fir_work_only(taps, xs, n_wo, chunk=4096)
+        calls = ncpu / 4096
         try:
             affinity = len(os.sched_getaffinity(0))
         except (AttributeError, OSError):
@@ -627,9 +769,15 @@ def main():
             "nproc": os.cpu_count(),
             "cpus_allowed": affinity,
             "kind": "port",
-            "sample": "2^%d samples through vector_source->head->fir_filter_ccf(127 taps, AVX-512 fp32)->null_sink, "
-                      "scheduler_mt thread-per-block (%d threads; the FIR on one core), vmcircbuf 32768 B default buffers; "
-                      "%.2f s on %s" % (a.cpu_log2n, threads, secs, cpu_model()),
+            "isa": isa,
+            "fir_work_only_msps": round(n_wo / wsecs / 1e6, 2),
+            "us_per_call": round(secs / calls * 1e6, 2),
+            "us_per_call_split": {"fir_work": round(wsecs / (n_wo / 4096) * 1e6, 2),
+                                  "scheduler_handoff": round(secs / calls * 1e6 - wsecs / (n_wo / 4096) * 1e6, 2)},
+            "sample": "2^%d samples through vector_source->head->fir_filter_ccf(127 taps, %s fp32)->null_sink, "
+                      "scheduler_mt thread-per-block (%d threads; the FIR on one core), vmcircbuf 32768 B default buffers "
+                      "(4096-item work() calls); %.2f s on %s. fir_work_only_msps: the same block's filter() alone on "
+                      "2^24 samples in 4096-sample calls, no scheduler" % (a.cpu_log2n, isa, threads, secs, cpu_model()),
         }
     if dist is not None and not abandoned:
         dist.barrier()

@@ -52,6 +52,11 @@ int nsh_device_sync(void);
 /* PCI bus id of `dev` ("dddd:bb:dd.f"): identifies a physical GPU across processes whose
  * device ordinals differ (per-rank HIP_VISIBLE_DEVICES makes every rank device 0). */
 int nsh_device_pci_id(int dev, char* buf, int len);
+/* *device = the GPU whose memory `ptr` points into (hipPointerGetAttributes, device memory
+ * only: VMM rings and hipMalloc), else -1 (NULL, pinned or pageable host memory). The rccl
+ * transport checks every buffer with it before handing it to librccl, so a wrong pointer is a
+ * thrown error of the edge instead of a fault inside an RCCL kernel. */
+int nsh_pointer_device(const void* ptr, int* device);
 
 /* ---- streams and events (opaque hipStream_t / hipEvent_t) ---------------------- */
 int nsh_stream_create(int dev, void** stream);
@@ -74,6 +79,12 @@ int nsh_stream_wait_event(void* stream, void* event);
  * the per-work() cudaEventRecord pairs a CUDA block would use for kernel timing (the reference
  * blocks do not time their kernels). */
 int nsh_time_next_launch(void* start_event, void* stop_event);
+/* Launches on the calling thread so far that recorded a pair set by nsh_time_next_launch (a pair
+ * spanning several launches of one entry point counts each launch that records one of its two
+ * events). A caller that armed a pair compares the count before and after the call it meant to
+ * time: unchanged means no launch took the pair (the call launched nothing; the pair was dropped
+ * unrecorded when the entry point returned). gr::schedulers::scheduler_hip's kernel timing. */
+int nsh_timed_launches(uint64_t* count);
 /* The shader clock while other work runs: one wave on `stream` (meant to be a second stream beside
  * the measured kernel's) reads the SQ cycle counter and the 100 MHz real-time counter, sleeps for
  * real_ticks (<= 2^32) ticks of the latter, reads both again and writes {cycles, ticks} to out_dev

@@ -52,6 +52,35 @@ const char* nsr_fir_bench_kernel(void* handle);
 int nsr_fir_bench_tail(void* handle, int64_t count, float* out_host);
 int nsr_fir_bench_destroy(void* handle);
 
+/* The other single-GPU BASELINE configurations as measurement flowgraphs, built like the C3
+ * bench: nop_source -> nop_head(n) -> [hip_buffer ring of 2n samples, PRELOADED with the synthetic
+ * stream x[first_index ..)] -> chain -> [hip_buffer] -> null_sink in one scheduler_hip domain, with
+ * the scheduler's kernel timing on (scheduler_hip::set_kernel_timing: every launching work() call
+ * records its own HIP event pair). kind:
+ *   NSR_CHAIN_MUL_CONST_CC  params = m (re, im) constants -> m x hip::multiply_const_cc (C2: m = 4;
+ *                           scheduler_hip fuses them into one launch per work())
+ *   NSR_CHAIN_CHANNELIZER   params = 1024 (re, im) weights W -> hip::fft_vcc(1024) ->
+ *                           hip::multiply_const_vcc(W) -> hip::fft_vcc(1024, inverse) (C4; fused into
+ *                           the channelizer); items are 1024-sample vectors, n a multiple of 2^18
+ *   NSR_CHAIN_FIR           params = taps -> hip::fir_filter_ccf(taps, decim) (the decimators)
+ * n counts complex samples per batch (a multiple of 256 items). */
+enum nsr_chain_kind { NSR_CHAIN_MUL_CONST_CC = 1, NSR_CHAIN_CHANNELIZER = 2, NSR_CHAIN_FIR = 3 };
+int nsr_chain_bench_create(int dev, int kind, const float* params, int nparams, int decim, int64_t n,
+                           uint64_t first_index, uint64_t seed, size_t out_buf_bytes, void** handle);
+int nsr_chain_bench_run(void* handle);
+int nsr_chain_bench_set_batches(void* handle, int64_t batches); /* as nsr_fir_bench_set_batches */
+/* Cumulative since create, for the block with the most kernel time (the fused block): summed
+ * kernel ms, timed launches, output samples, its alias; *n_launching_blocks = blocks that launched. */
+int nsr_chain_bench_stats(void* handle, double* kernel_ms, uint64_t* launches, uint64_t* samples, char* block,
+                          int len, int* n_launching_blocks);
+int nsr_chain_bench_tail(void* handle, int64_t count, float* out_host); /* last `count` output samples */
+int nsr_chain_bench_destroy(void* handle);
+
+/* BASELINE config C1 on the CPU (the reference's bm_copy flowgraph, schedulers/mt/bench/bm_copy.cpp:
+ * 143-154): null_source -> head(n) -> blocks::copy -> null_sink on scheduler_mt (thread per block,
+ * vmcircbuf edges of 2 * fixed_buf_size bytes). *seconds = wall time of fg->run(). */
+int nsr_c1_run(int64_t n, size_t fixed_buf_size, double* seconds, int* threads);
+
 /* C5 pipeline leg (BASELINE config 5): synth_source(first_index, n) -> 4 x
  * hip::fir_filter_ccf(taps, decim) -> null_sink, domain-partitioned over n_groups processes
  * (n_groups in {1, 2, 4}; group g runs stages [4g/G, 4(g+1)/G) in a scheduler_hip domain on
@@ -75,6 +104,14 @@ int nsr_c5_run(void* handle);
 int nsr_c5_transport(void* handle, char* buf, int len);
 /* The librccl file this process's rccl crossings bound (dladdr of ncclSend), "" if none. */
 int nsr_rccl_library(char* buf, int len);
+/* The rccl transport's library binding run in one process (domain_adapter_remote::rccl_self_test):
+ * the crossings' dlopen/dlsym table, a 1-rank communicator on `dev`, grouped ncclSend + ncclRecv
+ * of `bytes` from src to dst to `peer` (0 = self) on `stream`, drained and async-error checked.
+ * src / dst must be device memory of `dev` (refused before any RCCL call otherwise). Replaces
+ * nothing in the reference (its crossing is in-process, domain_adapter_direct.hpp:156-172): it
+ * checks the real librccl ABI (ncclUniqueId size, ncclCommInitRank order, ncclInt8 = 0) on a
+ * one-GPU box before a multi-GPU run depends on it. */
+int nsr_rccl_self_test(int dev, const void* src, void* dst, size_t bytes, void* stream, int peer);
 /* The last `count` outputs of the last run -> host (only the process of group n_groups-1). */
 int nsr_c5_tail(void* handle, int64_t count, float* out_host);
 int nsr_c5_destroy(void* handle);
@@ -85,6 +122,13 @@ int nsr_c5_destroy(void* handle);
  * *seconds = wall time of fg->run() (threads already created). */
 int nsr_cpu_fir_run(const float* taps, int ntaps, const float* x, int64_t nx, int64_t n, size_t fixed_buf_size,
                     double* seconds, int* threads);  /* *threads: scheduler_mt threads the run used */
+/* The same blocks::fir_filter_ccf arithmetic with no scheduler: n outputs in `chunk`-sample calls of
+ * fir_filter_ccf::filter() (what work() runs on a 4096-item scheduler_mt chunk), input read
+ * cyclically from x[0..nx) (nx a multiple of chunk), on the calling thread. *seconds = wall time;
+ * isa = the vector ISA the CPU blocks dispatched to (blocks::cpu_isa()). Splits the flowgraph
+ * baseline's time per work() call into FIR arithmetic and scheduler hand-off. */
+int nsr_cpu_fir_work_only(const float* taps, int ntaps, const float* x, int64_t nx, int64_t n, int chunk, double* seconds,
+                          char* isa, int len);
 
 #ifdef __cplusplus
 }

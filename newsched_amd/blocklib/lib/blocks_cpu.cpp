@@ -11,12 +11,28 @@ namespace gr {
 namespace blocks {
 
 namespace {
+// Function multiversioning by ISA FEATURE. GCC's target_clones("arch=skylake-avx512", "arch=haswell",
+// "default") -- what this file used up to round 5 -- dispatches "arch=" clones with
+// __builtin_cpu_is(<model>), which is false on every AMD EPYC and on Intel parts GCC does not name
+// that way (this container's Xeon included), so the baseline ran the SSE2 default clone. The clones
+// below are chosen with __builtin_cpu_supports on the features each one is compiled for.
+enum class isa { avx512, avx2, base };
+isa detect_isa()
+{
+    __builtin_cpu_init();
+    if (__builtin_cpu_supports("avx512f") && __builtin_cpu_supports("fma")) return isa::avx512;
+    if (__builtin_cpu_supports("avx2") && __builtin_cpu_supports("fma")) return isa::avx2;
+    return isa::base;
+}
+const isa g_isa = detect_isa();
+#define NSR_AVX512 __attribute__((target("avx512f,avx512vl,avx512dq,avx512bw,avx2,fma")))
+#define NSR_AVX2 __attribute__((target("avx2,fma")))
+
 // (ar kr - ai ki, ar ki + ai kr) with every product rounded: FMA contraction is switched
 // off for these two functions only, to match the reference formula bit for bit.
 #pragma GCC push_options
 #pragma GCC optimize("fp-contract=off")
-__attribute__((target_clones("arch=skylake-avx512", "arch=haswell", "default"))) void
-cmul_const(const float* in, float* out, size_t n, float kr, float ki)
+static inline __attribute__((always_inline)) void cmul_const_body(const float* in, float* out, size_t n, float kr, float ki)
 {
     for (size_t i = 0; i < n; ++i) {
         const float ar = in[2 * i], ai = in[2 * i + 1];
@@ -25,8 +41,7 @@ cmul_const(const float* in, float* out, size_t n, float kr, float ki)
         out[2 * i + 1] = p2 + p3;
     }
 }
-__attribute__((target_clones("arch=skylake-avx512", "arch=haswell", "default"))) void
-cmul_vec(const float* a, const float* b, float* out, size_t n)
+static inline __attribute__((always_inline)) void cmul_vec_body(const float* a, const float* b, float* out, size_t n)
 {
     for (size_t i = 0; i < n; ++i) {
         const float ar = a[2 * i], ai = a[2 * i + 1], br = b[2 * i], bi = b[2 * i + 1];
@@ -35,37 +50,73 @@ cmul_vec(const float* a, const float* b, float* out, size_t n)
         out[2 * i + 1] = p2 + p3;
     }
 }
+NSR_AVX512 void cmul_const_avx512(const float* in, float* out, size_t n, float kr, float ki) { cmul_const_body(in, out, n, kr, ki); }
+NSR_AVX2 void cmul_const_avx2(const float* in, float* out, size_t n, float kr, float ki) { cmul_const_body(in, out, n, kr, ki); }
+void cmul_const_base(const float* in, float* out, size_t n, float kr, float ki) { cmul_const_body(in, out, n, kr, ki); }
+NSR_AVX512 void cmul_vec_avx512(const float* a, const float* b, float* out, size_t n) { cmul_vec_body(a, b, out, n); }
+NSR_AVX2 void cmul_vec_avx2(const float* a, const float* b, float* out, size_t n) { cmul_vec_body(a, b, out, n); }
+void cmul_vec_base(const float* a, const float* b, float* out, size_t n) { cmul_vec_body(a, b, out, n); }
 #pragma GCC pop_options
 
-// Decim-1 rows: 32 complex outputs (4 x 16 interleaved floats) per step, taps broadcast,
-// fp32 FMA in tap order: out[m] = sum_k h[k] * x[m - k], x = ext shifted by L-1.
+void cmul_const(const float* in, float* out, size_t n, float kr, float ki)
+{
+    switch (g_isa) {
+    case isa::avx512: return cmul_const_avx512(in, out, n, kr, ki);
+    case isa::avx2: return cmul_const_avx2(in, out, n, kr, ki);
+    default: return cmul_const_base(in, out, n, kr, ki);
+    }
+}
+void cmul_vec(const float* a, const float* b, float* out, size_t n)
+{
+    switch (g_isa) {
+    case isa::avx512: return cmul_vec_avx512(a, b, out, n);
+    case isa::avx2: return cmul_vec_avx2(a, b, out, n);
+    default: return cmul_vec_base(a, b, out, n);
+    }
+}
+
+// Decim-1 rows: NV x 8 complex outputs (NV vectors of 16 interleaved floats) per step, fp32
+// accumulation: out[m] = sum_k h[k] * x[m - k], x = ext shifted by L-1. The taps go by residue
+// rho = k mod 8: tap rho + 8t at output vector r reads the input vector W[r - t] (one vector = 8
+// complex samples = the 8-tap stride), so for one residue each input vector is loaded ONCE, aligned
+// to the 8-sample grid of its residue, and feeds up to NV FMAs from a rolling window of NV
+// registers -- instead of one cache-line-splitting load per FMA. NV = 8 on AVX-512 (two FMA
+// pipes x four cycles of latency), 4 on AVX2 (the same registers in 256-bit halves).
 typedef float v16f __attribute__((vector_size(64)));
 
-__attribute__((target_clones("arch=skylake-avx512", "arch=haswell", "default"))) void
-fir_rows(const float* ext, const float* h, int L, int D, float* out, size_t n_out)
+template <int NV, int P>
+static inline __attribute__((always_inline)) void fir_step(v16f* a, v16f* w, float hk)
+{
+    for (int r = 0; r < NV; ++r) a[r] += hk * w[(r - P + 8 * NV) % NV];
+}
+
+template <int NV>
+static inline __attribute__((always_inline)) void fir_rows_body(const float* ext, const float* h, int L, int D, float* out,
+                                                                size_t n_out)
 {
     size_t m = 0;
     if (D == 1) {
-        for (; m + 32 <= n_out; m += 32) {
-            v16f a0 = {}, a1 = {}, a2 = {}, a3 = {};
+        for (; m + 8 * NV <= n_out; m += 8 * NV) {
+            v16f a[NV] = {};
             const float* base = ext + 2 * (m + (size_t)(L - 1));
-            for (int k = 0; k < L; ++k) {
-                const float* x = base - 2 * k;
-                v16f x0, x1, x2, x3;
-                std::memcpy(&x0, x, 64);
-                std::memcpy(&x1, x + 16, 64);
-                std::memcpy(&x2, x + 32, 64);
-                std::memcpy(&x3, x + 48, 64);
-                const float hk = h[k];
-                a0 += hk * x0;
-                a1 += hk * x1;
-                a2 += hk * x2;
-                a3 += hk * x3;
+            for (int rho = 0; rho < 8 && rho < L; ++rho) {
+                const float* W = base - 2 * rho; // W[j] = W + 16 j
+                const int T = (L - rho + 7) / 8;  // taps rho, rho + 8, ... < L
+                v16f w[NV];                       // W[j] in slot j mod NV
+                for (int r = 0; r < NV; ++r) std::memcpy(&w[r], W + 16 * r, 64);
+                // step t: a[r] += h[rho + 8t] W[r - t]; then W[-(t+1)] replaces W[NV-1-t]
+#define NSR_FIR_STEP(P)                                                                      \
+    if (t + P < T) {                                                                         \
+        fir_step<NV, P % NV>(a, w, h[rho + 8 * (t + P)]);                                    \
+        if (t + P + 1 < T) std::memcpy(&w[(NV - 1 - P % NV) % NV], W - 16 * (t + P + 1), 64); \
+    }
+                for (int t = 0; t < T; t += 8) {
+                    NSR_FIR_STEP(0) NSR_FIR_STEP(1) NSR_FIR_STEP(2) NSR_FIR_STEP(3)
+                    NSR_FIR_STEP(4) NSR_FIR_STEP(5) NSR_FIR_STEP(6) NSR_FIR_STEP(7)
+                }
+#undef NSR_FIR_STEP
             }
-            std::memcpy(out + 2 * m, &a0, 64);
-            std::memcpy(out + 2 * m + 16, &a1, 64);
-            std::memcpy(out + 2 * m + 32, &a2, 64);
-            std::memcpy(out + 2 * m + 48, &a3, 64);
+            for (int r = 0; r < NV; ++r) std::memcpy(out + 2 * m + 16 * r, &a[r], 64);
         }
     }
     for (; m < n_out; ++m) {
@@ -77,6 +128,23 @@ fir_rows(const float* ext, const float* h, int L, int D, float* out, size_t n_ou
         }
         out[2 * m] = ar;
         out[2 * m + 1] = ai;
+    }
+}
+NSR_AVX512 void fir_rows_avx512(const float* ext, const float* h, int L, int D, float* out, size_t n)
+{
+    fir_rows_body<8>(ext, h, L, D, out, n);
+}
+NSR_AVX2 void fir_rows_avx2(const float* ext, const float* h, int L, int D, float* out, size_t n)
+{
+    fir_rows_body<4>(ext, h, L, D, out, n);
+}
+void fir_rows_base(const float* ext, const float* h, int L, int D, float* out, size_t n) { fir_rows_body<4>(ext, h, L, D, out, n); }
+void fir_rows(const float* ext, const float* h, int L, int D, float* out, size_t n_out)
+{
+    switch (g_isa) {
+    case isa::avx512: return fir_rows_avx512(ext, h, L, D, out, n_out);
+    case isa::avx2: return fir_rows_avx2(ext, h, L, D, out, n_out);
+    default: return fir_rows_base(ext, h, L, D, out, n_out);
     }
 }
 } // namespace
@@ -137,21 +205,35 @@ bool fir_filter_ccf::start()
     return block::start();
 }
 
-work_return_code_t fir_filter_ccf::work(std::vector<block_work_input>& in, std::vector<block_work_output>& out)
+void fir_filter_ccf::filter(const gr_complex* x, gr_complex* y, int n_out)
 {
     const int L = (int)_taps.size();
-    const int n_out = out[0].n_items; // decim_block::do_work: in[0].n_items == D * n_out
     const size_t n_in = (size_t)n_out * _decim;
-    const gr_complex* x = static_cast<const gr_complex*>(in[0].buffer->read_ptr());
+    if (_ext.size() < (size_t)(L - 1)) _ext.assign((size_t)(L - 1), gr_complex(0, 0)); // not started: zeros
     _ext.resize((size_t)(L - 1) + n_in);
     std::memcpy(_ext.data() + (L - 1), x, n_in * sizeof(gr_complex));
-    fir_rows(reinterpret_cast<const float*>(_ext.data()), _taps.data(), L, _decim,
-             static_cast<float*>(out[0].buffer->write_ptr()), (size_t)n_out);
+    fir_rows(reinterpret_cast<const float*>(_ext.data()), _taps.data(), L, _decim, reinterpret_cast<float*>(y), (size_t)n_out);
     // keep the last L-1 inputs as history
     std::memmove(_ext.data(), _ext.data() + n_in, (size_t)(L - 1) * sizeof(gr_complex));
     _ext.resize((size_t)(L - 1));
+}
+
+work_return_code_t fir_filter_ccf::work(std::vector<block_work_input>& in, std::vector<block_work_output>& out)
+{
+    const int n_out = out[0].n_items; // decim_block::do_work: in[0].n_items == D * n_out
+    filter(static_cast<const gr_complex*>(in[0].buffer->read_ptr()), static_cast<gr_complex*>(out[0].buffer->write_ptr()),
+           n_out);
     out[0].n_produced = n_out;
     return work_return_code_t::WORK_OK;
+}
+
+const char* cpu_isa()
+{
+    switch (g_isa) {
+    case isa::avx512: return "avx512f+fma";
+    case isa::avx2: return "avx2+fma";
+    default: return "x86-64 baseline (sse2)";
+    }
 }
 
 } // namespace blocks

@@ -4,8 +4,12 @@
 
 #include <chrono>
 #include <cstring>
+#include <gnuradio/blocklib/blocks/copy.hpp>
 #include <gnuradio/blocklib/blocks/fir_filter_ccf.hpp>
 #include <gnuradio/blocklib/blocks/head.hpp>
+#include <gnuradio/blocklib/blocks/null_source.hpp>
+#include <gnuradio/blocklib/hip/fft.hpp>
+#include <gnuradio/blocklib/hip/multiply_const.hpp>
 #include <gnuradio/blocklib/blocks/nop.hpp>
 #include <gnuradio/blocklib/blocks/null_sink.hpp>
 #include <gnuradio/blocklib/blocks/vector_source.hpp>
@@ -77,6 +81,16 @@ struct c5_pipeline {
     std::shared_ptr<domain_adapter_remote_conf> da;
     std::vector<hip::fir_filter_ccf::sptr> stages;
     std::shared_ptr<hip_buffer> out_ring; // last group only
+    int dev = 0;
+};
+
+struct chain_bench {
+    flowgraph::sptr fg;
+    schedulers::scheduler_hip::sptr sched;
+    blocks::nop_head::sptr head;
+    std::shared_ptr<hip_buffer> out_ring;
+    int64_t n_items = 0; // per batch, in the input ring's items
+    size_t spi = 1;      // samples per item (1024 for the channelizer's vectors)
     int dev = 0;
 };
 
@@ -220,6 +234,150 @@ int nsr_fir_bench_destroy(void* handle)
     return guarded([&] { delete static_cast<fir_bench*>(handle); });
 }
 
+int nsr_chain_bench_create(int dev, int kind, const float* params, int nparams, int decim, int64_t n,
+                           uint64_t first_index, uint64_t seed, size_t out_buf_bytes, void** handle)
+{
+    return guarded([&] {
+        if (!params || nparams <= 0) throw std::invalid_argument("nsr_chain_bench_create: no parameters");
+        auto b = std::make_unique<chain_bench>();
+        b->dev = dev;
+        std::vector<block_sptr> chain;
+        switch (kind) {
+        case NSR_CHAIN_MUL_CONST_CC:
+            if (nparams % 2) throw std::invalid_argument("nsr_chain_bench_create: constants come as (re, im) pairs");
+            for (int i = 0; i < nparams; i += 2) chain.push_back(hip::multiply_const_cc::make(gr_complex(params[i], params[i + 1])));
+            break;
+        case NSR_CHAIN_CHANNELIZER: {
+            if (nparams != 2048) throw std::invalid_argument("nsr_chain_bench_create: the channelizer needs 1024 (re, im) weights");
+            std::vector<gr_complex> w(1024);
+            for (int k = 0; k < 1024; ++k) w[k] = gr_complex(params[2 * k], params[2 * k + 1]);
+            chain = { hip::fft_vcc::make(1024, true), hip::multiply_const_vcc::make(w), hip::fft_vcc::make(1024, false) };
+            b->spi = 1024;
+            break;
+        }
+        case NSR_CHAIN_FIR: {
+            auto f = hip::fir_filter_ccf::make(std::vector<float>(params, params + nparams), decim);
+            if (first_index > 0) {
+                std::vector<gr_complex> h((size_t)nparams - 1);
+                for (size_t j = 0; j < h.size(); ++j) h[j] = synth_at(first_index - h.size() + j, seed);
+                f->set_initial_history(h);
+            }
+            chain.push_back(f);
+            break;
+        }
+        default:
+            throw std::invalid_argument("nsr_chain_bench_create: unknown kind");
+        }
+        if (n <= 0 || n % (int64_t)(256 * b->spi) || (kind == NSR_CHAIN_FIR && n % decim))
+            throw std::invalid_argument("nsr_chain_bench_create: n must be a positive multiple of 256 items (and of decim)");
+        b->n_items = n / (int64_t)b->spi;
+        const size_t isz = sizeof(gr_complex) * b->spi;
+        auto src = blocks::nop_source::make(isz);
+        b->head = blocks::nop_head::make(isz, (size_t)b->n_items);
+        auto snk = blocks::null_sink::make(isz);
+        b->fg = flowgraph::make();
+        b->fg->connect(src, 0, b->head, 0)->set_custom_buffer(VMCIRC_BUFFER_ARGS);
+        const int64_t cap = 2 * b->n_items; // the resident input ring holds x twice
+        b->fg->connect(b->head, 0, chain[0], 0)
+            ->set_custom_buffer(
+                [cap, dev](size_t, size_t item, std::shared_ptr<buffer_properties>) -> buffer_sptr {
+                    return std::make_shared<hip_buffer>((size_t)cap, item, hip_buffer_type::D2D, dev);
+                },
+                hip_buffer_properties::make(hip_buffer_type::D2D, dev));
+        for (size_t i = 1; i < chain.size(); ++i) b->fg->connect(chain[i - 1], 0, chain[i], 0);
+        b->fg->connect(chain.back(), 0, snk, 0);
+        b->sched = schedulers::scheduler_hip::make("hipc" + std::to_string(dev), dev, out_buf_bytes);
+        b->fg->set_scheduler(b->sched);
+        b->fg->set_wait_spin_us(5000);
+        b->sched->set_flush_spin_us(5000);
+        b->fg->validate();
+        // the head's output edge (its consumer may be a fused block that replaced chain[0])
+        auto in_ring = std::dynamic_pointer_cast<hip_buffer>(b->sched->buffers()->get_output_buffers(b->head->output_stream_ports()[0])[0]);
+        b->out_ring = std::dynamic_pointer_cast<hip_buffer>(b->sched->buffers()->get_input_buffer(snk->input_stream_ports()[0]));
+        if (!in_ring || !b->out_ring) throw std::runtime_error("nsr_chain_bench_create: unexpected buffer types");
+        if ((int64_t)in_ring->capacity() != cap) throw std::runtime_error("nsr_chain_bench_create: ring capacity mismatch");
+        void* s = nullptr;
+        hip::check(nsh_stream_create(dev, &s), "nsr: stream");
+        char* base = (char*)in_ring->device_base();
+        hip::check(nsh_synth_cf32((float*)base, n, first_index, seed, s), "nsr: preload");
+        hip::check(nsh_synth_cf32((float*)(base + b->n_items * isz), n, first_index, seed, s), "nsr: preload");
+        hip::check(nsh_stream_sync(s), "nsr: preload");
+        nsh_stream_destroy(s);
+        b->sched->set_kernel_timing(true);
+        *handle = b.release();
+    });
+}
+
+int nsr_chain_bench_run(void* handle)
+{
+    return guarded([&] { static_cast<chain_bench*>(handle)->fg->run(); });
+}
+
+int nsr_chain_bench_set_batches(void* handle, int64_t batches)
+{
+    return guarded([&] {
+        auto b = static_cast<chain_bench*>(handle);
+        if (batches < 1) throw std::invalid_argument("nsr_chain_bench_set_batches: batches must be >= 1");
+        b->head->set_length((size_t)(batches * b->n_items));
+    });
+}
+
+int nsr_chain_bench_stats(void* handle, double* kernel_ms, uint64_t* launches, uint64_t* samples, char* block,
+                          int len, int* n_launching_blocks)
+{
+    return guarded([&] {
+        auto b = static_cast<chain_bench*>(handle);
+        const auto st = b->sched->kernel_stats();
+        schedulers::scheduler_hip::kernel_stat best;
+        for (auto& k : st)
+            if (k.kernel_ms >= best.kernel_ms) best = k;
+        if (kernel_ms) *kernel_ms = best.kernel_ms;
+        if (launches) *launches = best.launches;
+        if (samples) *samples = best.items * b->spi; // output samples (decimators: n / D per batch)
+        if (n_launching_blocks) *n_launching_blocks = (int)st.size();
+        if (block && len > 0) {
+            std::strncpy(block, best.block.c_str(), (size_t)len - 1);
+            block[len - 1] = 0;
+        }
+    });
+}
+
+int nsr_chain_bench_tail(void* handle, int64_t count, float* out_host)
+{
+    return guarded([&] {
+        auto b = static_cast<chain_bench*>(handle);
+        if (count <= 0 || count % (int64_t)b->spi) throw std::invalid_argument("nsr_chain_bench_tail: whole items only");
+        ring_tail(b->out_ring, b->dev, count / (int64_t)b->spi, out_host);
+    });
+}
+
+int nsr_chain_bench_destroy(void* handle)
+{
+    return guarded([&] { delete static_cast<chain_bench*>(handle); });
+}
+
+int nsr_c1_run(int64_t n, size_t fixed_buf_size, double* seconds, int* threads)
+{
+    return guarded([&] {
+        auto src = blocks::null_source::make(sizeof(gr_complex));
+        auto head = blocks::head::make(sizeof(gr_complex), (size_t)n);
+        auto cp = blocks::copy::make(sizeof(gr_complex));
+        auto snk = blocks::null_sink::make(sizeof(gr_complex));
+        auto fg = flowgraph::make();
+        fg->connect(src, 0, head, 0);
+        fg->connect(head, 0, cp, 0);
+        fg->connect(cp, 0, snk, 0);
+        auto sched = schedulers::scheduler_mt::make("mt", (unsigned)fixed_buf_size);
+        fg->set_scheduler(sched);
+        fg->validate();
+        if (threads) *threads = (int)sched->num_threads();
+        const auto t0 = std::chrono::steady_clock::now();
+        fg->run();
+        *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (snk->consumed() != (uint64_t)n) throw std::runtime_error("nsr_c1_run: short run");
+    });
+}
+
 int nsr_c5_create(int group, int n_groups, int dev, const float* taps, int ntaps, int decim, int64_t n,
                   uint64_t first_index, uint64_t seed, const char* rendezvous_dir, uint64_t nonce,
                   const char* transport, size_t buf_bytes, void** handle)
@@ -318,6 +476,11 @@ int nsr_rccl_library(char* buf, int len)
     });
 }
 
+int nsr_rccl_self_test(int dev, const void* src, void* dst, size_t bytes, void* stream, int peer)
+{
+    return guarded([&] { domain_adapter_remote::rccl_self_test(dev, src, dst, bytes, stream, peer); });
+}
+
 int nsr_c5_tail(void* handle, int64_t count, float* out_host)
 {
     return guarded([&] {
@@ -330,6 +493,30 @@ int nsr_c5_tail(void* handle, int64_t count, float* out_host)
 int nsr_c5_destroy(void* handle)
 {
     return guarded([&] { delete static_cast<c5_pipeline*>(handle); });
+}
+
+int nsr_cpu_fir_work_only(const float* taps, int ntaps, const float* x, int64_t nx, int64_t n, int chunk, double* seconds,
+                          char* isa, int len)
+{
+    return guarded([&] {
+        if (chunk <= 0 || nx < chunk || nx % chunk) throw std::invalid_argument("nsr_cpu_fir_work_only: nx must be a multiple of chunk");
+        auto fir = blocks::fir_filter_ccf::make(std::vector<float>(taps, taps + ntaps), 1);
+        fir->start();
+        std::vector<gr_complex> y((size_t)chunk);
+        const gr_complex* xc = (const gr_complex*)x;
+        const auto t0 = std::chrono::steady_clock::now();
+        int64_t off = 0;
+        for (int64_t done = 0; done < n; done += chunk) {
+            const int m = (int)std::min<int64_t>(chunk, n - done);
+            fir->filter(xc + off, y.data(), m);
+            off = (off + chunk) % nx;
+        }
+        *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (isa && len > 0) {
+            std::strncpy(isa, blocks::cpu_isa(), (size_t)len - 1);
+            isa[len - 1] = 0;
+        }
+    });
 }
 
 int nsr_cpu_fir_run(const float* taps, int ntaps, const float* x, int64_t nx, int64_t n, size_t fixed_buf_size,

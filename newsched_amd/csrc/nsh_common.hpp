@@ -42,6 +42,13 @@ inline launch_events& next_launch_events()
     static thread_local launch_events e;
     return e;
 }
+// Launches on this thread that recorded a pair (nsh_timed_launches): a caller that armed a pair
+// tells from the count whether a launch took it or it was dropped unrecorded.
+inline uint64_t& timed_launch_count()
+{
+    static thread_local uint64_t n = 0;
+    return n;
+}
 template <typename K, typename... A>
 inline void launch(K kernel, dim3 grid, dim3 block, uint32_t lds, hipStream_t s, A... args)
 {
@@ -49,6 +56,7 @@ inline void launch(K kernel, dim3 grid, dim3 block, uint32_t lds, hipStream_t s,
     if (e.start || e.stop) {
         const launch_events t = e;
         e = launch_events();
+        ++timed_launch_count();
         hipExtLaunchKernelGGL(kernel, grid, block, lds, s, t.start, t.stop, 0u, args...);
     } else {
         hipLaunchKernelGGL(kernel, grid, block, lds, s, args...);
@@ -67,9 +75,10 @@ template <typename K, typename... A>
 inline void launch_timed(K kernel, dim3 grid, dim3 block, uint32_t lds, hipStream_t s, hipEvent_t start, hipEvent_t stop,
                          A... args)
 {
-    if (start || stop)
+    if (start || stop) {
+        ++timed_launch_count();
         hipExtLaunchKernelGGL(kernel, grid, block, lds, s, start, stop, 0u, args...);
-    else
+    } else
         hipLaunchKernelGGL(kernel, grid, block, lds, s, args...);
 }
 // Clears the pending pair when an entry point returns, whatever the path (early returns, errors,

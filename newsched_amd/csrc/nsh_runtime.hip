@@ -73,6 +73,21 @@ int nsh_device_pci_id(int dev, char* buf, int len)
     return 0;
 }
 
+int nsh_pointer_device(const void* ptr, int* device)
+{
+    if (!device) return ::nsh::fail(hipErrorInvalidValue, "nsh_pointer_device: device is NULL");
+    *device = -1;
+    if (!ptr) return 0;
+    hipPointerAttribute_t a{};
+    const hipError_t e = hipPointerGetAttributes(&a, ptr);
+    if (e != hipSuccess) { // pageable host memory (never registered with HIP): not device memory
+        (void)hipGetLastError();
+        return 0;
+    }
+    if (a.type == hipMemoryTypeDevice) *device = a.device;
+    return 0;
+}
+
 int nsh_device_sync(void)
 {
     NSH_CK(hipDeviceSynchronize());
@@ -127,6 +142,12 @@ int nsh_time_next_launch(void* start_event, void* stop_event)
     auto& e = next_launch_events();
     e.start = reinterpret_cast<hipEvent_t>(start_event);
     e.stop = reinterpret_cast<hipEvent_t>(stop_event);
+    return 0;
+}
+int nsh_timed_launches(uint64_t* count)
+{
+    if (!count) return nsh::fail_msg("nsh_timed_launches: null count");
+    *count = timed_launch_count();
     return 0;
 }
 int nsh_clock_sample(void* out_dev, int64_t real_ticks, void* stream)

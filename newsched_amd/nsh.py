@@ -31,6 +31,7 @@ SIGNATURES = {
     "nsh_set_device": (_i, [_i]),
     "nsh_device_info": (_i, [_i, C.POINTER(_i), C.POINTER(_i), C.POINTER(_sz), C.c_char_p, _i]),
     "nsh_device_pci_id": (_i, [_i, C.c_char_p, _i]),
+    "nsh_pointer_device": (_i, [_vp, C.POINTER(_i)]),
     "nsh_device_sync": (_i, []),
     "nsh_stream_create": (_i, [_i, C.POINTER(_vp)]),
     "nsh_stream_destroy": (_i, [_vp]),
@@ -44,6 +45,7 @@ SIGNATURES = {
     "nsh_event_elapsed_ms": (_i, [_vp, _vp, C.POINTER(_f)]),
     "nsh_stream_wait_event": (_i, [_vp, _vp]),
     "nsh_time_next_launch": (_i, [_vp, _vp]),
+    "nsh_timed_launches": (_i, [C.POINTER(_u64)]),
     "nsh_clock_sample": (_i, [_vp, _i64, _vp]),
     "nsh_malloc": (_i, [_i, _sz, C.POINTER(_vp)]),
     "nsh_free": (_i, [_vp]),
@@ -120,6 +122,13 @@ def stream_ptr(stream=None) -> int:
 
     s = stream if stream is not None else torch.cuda.current_stream()
     return s.cuda_stream
+
+
+def pointer_device(p) -> int:
+    """The GPU whose device memory p points into, -1 for host memory / NULL (nsh_pointer_device)."""
+    d = C.c_int(-2)
+    check(lib().nsh_pointer_device(C.c_void_p(ptr(p)), C.byref(d)), "nsh_pointer_device")
+    return d.value
 
 
 # ---- thin typed wrappers over torch tensors (complex64 or float32 views) -------------

@@ -35,7 +35,20 @@ SIGNATURES = {
     "nsr_cpu_fir_run": (_i, [C.POINTER(C.c_float), _i, C.POINTER(C.c_float), _i64, _i64, _sz, C.POINTER(_d),
                              C.POINTER(_i)]),
     "nsr_rccl_library": (_i, [C.c_char_p, _i]),
+    "nsr_rccl_self_test": (_i, [_i, _vp, _vp, _sz, _vp, _i]),
+    "nsr_chain_bench_create": (_i, [_i, _i, C.POINTER(C.c_float), _i, _i, _i64, _u64, _u64, _sz, C.POINTER(_vp)]),
+    "nsr_chain_bench_run": (_i, [_vp]),
+    "nsr_chain_bench_set_batches": (_i, [_vp, _i64]),
+    "nsr_chain_bench_stats": (_i, [_vp, C.POINTER(_d), C.POINTER(_u64), C.POINTER(_u64), C.c_char_p, _i,
+                                   C.POINTER(_i)]),
+    "nsr_chain_bench_tail": (_i, [_vp, _i64, C.POINTER(C.c_float)]),
+    "nsr_chain_bench_destroy": (_i, [_vp]),
+    "nsr_c1_run": (_i, [_i64, _sz, C.POINTER(_d), C.POINTER(_i)]),
+    "nsr_cpu_fir_work_only": (_i, [C.POINTER(C.c_float), _i, C.POINTER(C.c_float), _i64, _i64, _i, C.POINTER(_d),
+                                   C.c_char_p, _i]),
 }
+
+CHAIN_MUL_CONST_CC, CHAIN_CHANNELIZER, CHAIN_FIR = 1, 2, 3
 
 
 def lib() -> C.CDLL:
@@ -114,6 +127,60 @@ class FirBench:
             pass
 
 
+class ChainBench:
+    """Measurement flowgraph of another single-GPU BASELINE config (see nsr_chain_bench_create):
+    kind CHAIN_MUL_CONST_CC (params: complex constants), CHAIN_CHANNELIZER (params: 1024 complex
+    weights), CHAIN_FIR (params: taps, with decim)."""
+
+    def __init__(self, kind, params, n, device=0, decim=1, first_index=0, seed=0x6E736368, out_buf_bytes=256 << 20):
+        if kind == CHAIN_FIR:
+            p = np.ascontiguousarray(np.asarray(params, np.float32))
+        else:
+            p = np.ascontiguousarray(np.asarray(params, np.complex64)).view(np.float32)
+        self.n = int(n)
+        h = C.c_void_p()
+        check(lib().nsr_chain_bench_create(device, kind, _f32p(p), int(p.size), int(decim), self.n, first_index, seed,
+                                           out_buf_bytes, C.byref(h)), "nsr_chain_bench_create")
+        self._h = h
+
+    def set_batches(self, batches: int):
+        check(lib().nsr_chain_bench_set_batches(self._h, int(batches)), "nsr_chain_bench_set_batches")
+
+    def run(self):
+        check(lib().nsr_chain_bench_run(self._h), "nsr_chain_bench_run")
+
+    def stats(self):
+        ms, la, sa, nb = C.c_double(), C.c_uint64(), C.c_uint64(), C.c_int()
+        buf = C.create_string_buffer(256)
+        check(lib().nsr_chain_bench_stats(self._h, C.byref(ms), C.byref(la), C.byref(sa), buf, 256, C.byref(nb)),
+              "nsr_chain_bench_stats")
+        return {"kernel_ms": ms.value, "launches": la.value, "samples": sa.value, "block": buf.value.decode(),
+                "launching_blocks": nb.value}
+
+    def tail(self, count):
+        out = np.empty(count, np.complex64)
+        check(lib().nsr_chain_bench_tail(self._h, count, _f32p(out.view(np.float32))), "nsr_chain_bench_tail")
+        return out
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().nsr_chain_bench_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def c1_run(n=1 << 20, fixed_buf_size=32768):
+    """(seconds, threads) of one C1 run: null_source -> head(n) -> copy -> null_sink on scheduler_mt."""
+    s, th = C.c_double(), C.c_int()
+    check(lib().nsr_c1_run(int(n), fixed_buf_size, C.byref(s), C.byref(th)), "nsr_c1_run")
+    return s.value, th.value
+
+
 class C5Pipeline:
     """One process's share of the C5 decimating pipeline (see nsr_c5_create). Every process of
     one pipeline passes the same rendezvous_dir (a fresh directory on this node) and nonce."""
@@ -164,8 +231,26 @@ def cpu_fir_run(taps, x, n, fixed_buf_size=32768, with_threads=False):
     return (s.value, th.value) if with_threads else s.value
 
 
+def cpu_fir_work_only(taps, x, n, chunk=4096):
+    """(seconds, isa) of n FIR outputs in chunk-sample filter() calls, no scheduler."""
+    t = np.ascontiguousarray(np.asarray(taps, np.float32))
+    xv = np.ascontiguousarray(np.asarray(x, np.complex64))
+    s = C.c_double()
+    buf = C.create_string_buffer(64)
+    check(lib().nsr_cpu_fir_work_only(_f32p(t), t.size, _f32p(xv.view(np.float32)), xv.size, int(n), int(chunk),
+                                      C.byref(s), buf, 64), "nsr_cpu_fir_work_only")
+    return s.value, buf.value.decode()
+
+
 def rccl_library() -> str:
     """The librccl file this process's rccl crossings bound ("" if none)."""
     buf = C.create_string_buffer(1024)
     check(lib().nsr_rccl_library(buf, 1024), "nsr_rccl_library")
     return buf.value.decode()
+
+
+def rccl_self_test(device, src_ptr, dst_ptr, nbytes, stream_ptr, peer=0):
+    """One-process send/recv to self through the rccl transport's library table (see
+    nsr_rccl_self_test); raises NshError with RCCL's text on any failure."""
+    check(lib().nsr_rccl_self_test(int(device), C.c_void_p(src_ptr), C.c_void_p(dst_ptr), int(nbytes),
+                                   C.c_void_p(stream_ptr), int(peer)), "nsr_rccl_self_test")

@@ -141,6 +141,13 @@ public:
     // The librccl file the rccl transport bound in this process (dladdr of ncclSend; "" before
     // the first rccl crossing): an already-loaded copy (torch's) if any, else /opt/rocm's.
     static std::string rccl_library();
+    // The rccl transport's library binding exercised in ONE process (no peer, no second GPU):
+    // through the same dlopen / dlsym table as the crossings, a 1-rank communicator on `device`
+    // (ncclGetUniqueId, ncclCommInitRank), a grouped ncclSend + ncclRecv of `bytes` from src to
+    // dst to `peer` (0 = self) on `stream`, the stream drained, ncclCommGetAsyncError, destroy.
+    // src / dst must be device memory of `device` (checked before any RCCL call). Every failure,
+    // RCCL's own codes included, throws with RCCL's error text.
+    static void rccl_self_test(int device, const void* src, void* dst, size_t bytes, void* stream, int peer = 0);
 
 private:
     domain_adapter_remote(remote_role role, int crossing, const remote_edge_options& opt);

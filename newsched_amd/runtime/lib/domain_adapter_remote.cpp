@@ -869,8 +869,11 @@ class rccl_transport : public transport
         int (*comm_destroy)(void*) = nullptr;
         const char* (*err_str)(int) = nullptr;
         int (*async_error)(void*, int*) = nullptr; // ncclCommGetAsyncError (optional)
+        int (*group_start)() = nullptr;            // ncclGroupStart / ncclGroupEnd (optional: the
+        int (*group_end)() = nullptr;              // crossings never group; rccl_self_test does)
         std::string path;                          // the file ncclSend came from
     };
+public:
     static api& lib()
     {
         static api a;
@@ -892,6 +895,8 @@ class rccl_transport : public transport
             a.recv = (int (*)(void*, size_t, int, int, void*, void*))dlsym(a.h, "ncclRecv");
             a.comm_init_rank = dlsym(a.h, "ncclCommInitRank");
             a.async_error = (int (*)(void*, int*))dlsym(a.h, "ncclCommGetAsyncError");
+            a.group_start = (int (*)())dlsym(a.h, "ncclGroupStart");
+            a.group_end = (int (*)())dlsym(a.h, "ncclGroupEnd");
             Dl_info di{};
             if (a.send && dladdr((void*)a.send, &di) && di.dli_fname) a.path = di.dli_fname;
             std::lock_guard<std::mutex> g(g_rccl_path_m);
@@ -901,6 +906,8 @@ class rccl_transport : public transport
             throw std::runtime_error("remote edge: librccl.so.1 not loadable");
         return a;
     }
+
+private:
     void ck(int r, const char* what)
     {
         if (r != 0)
@@ -921,7 +928,7 @@ public:
     };
     using init_fn = int (*)(void**, int, uid, int);
 
-    rccl_transport(channel& ch, bool sender, int device, bool dev_ring) : _sender(sender), _dev(dev_ring)
+    rccl_transport(channel& ch, bool sender, int device, bool dev_ring) : _sender(sender), _dev(dev_ring), _device(device)
     {
         auto& L = lib();
         if (_dev) hip::check(nsh_set_device(device), "remote edge: set device");
@@ -944,6 +951,7 @@ public:
                  std::function<void()>) override
     {
         check_async();
+        check_span(p, "ncclSend");
         // header first: the receiver posts the matching ncclRecv when it reads it
         write_data(ch, n, ntags, blob, [] {});
         ck(lib().send(p, bytes, /*ncclInt8*/ 0, /*peer*/ 1, _comm, stream()), "ncclSend");
@@ -961,13 +969,27 @@ public:
     void recv(channel&, void* p, size_t bytes) override
     {
         check_async();
+        check_span(p, "ncclRecv");
         ck(lib().recv(p, bytes, /*ncclInt8*/ 0, /*peer*/ 0, _comm, stream()), "ncclRecv");
     }
 
 private:
     void* stream() const { return _dev ? hip::current_stream() : nullptr; }
+    // a device-ring span handed to librccl must be device memory of this edge's GPU (VMM ring
+    // mappings included; tests/test_rccl_real.py): anything else is this edge's error, not a
+    // fault inside an RCCL kernel
+    void check_span(const void* p, const char* what) const
+    {
+        if (!_dev || _device < 0) return;
+        int d = -1;
+        hip::check(nsh_pointer_device(p, &d), "remote edge: pointer attributes");
+        if (d != _device)
+            throw std::runtime_error(std::string("remote edge: ") + what + ": span is not device memory of GPU " +
+                                     std::to_string(_device) + " (found " + std::to_string(d) + ")");
+    }
     bool _sender;
     bool _dev; // device ring (always, but for the host-ring test double)
+    int _device;
     void* _comm = nullptr;
 };
 
@@ -977,6 +999,52 @@ std::string domain_adapter_remote::rccl_library()
 {
     std::lock_guard<std::mutex> g(remote::g_rccl_path_m);
     return remote::g_rccl_path;
+}
+
+void domain_adapter_remote::rccl_self_test(int device, const void* src, void* dst, size_t bytes, void* stream, int peer)
+{
+    auto& L = remote::rccl_transport::lib(); // the crossings' own table: same dlopen order, same symbols
+    auto ck = [&L](int r, const char* what) {
+        if (r != 0)
+            throw std::runtime_error(std::string("rccl_self_test: ") + what + ": " +
+                                     (L.err_str ? L.err_str(r) : std::to_string(r)) + " (" + std::to_string(r) + ")");
+    };
+    if (!L.group_start || !L.group_end) throw std::runtime_error("rccl_self_test: ncclGroupStart/End not exported");
+    // the buffers go to RCCL kernels: anything but device memory of this GPU is refused here,
+    // before any RCCL call, instead of faulting inside one
+    for (const void* p : { src, (const void*)dst }) {
+        int d = -1;
+        hip::check(nsh_pointer_device(p, &d), "rccl_self_test: pointer attributes");
+        if (d != device)
+            throw std::invalid_argument("rccl_self_test: buffer " + std::to_string((uintptr_t)p) +
+                                        " is not device memory of GPU " + std::to_string(device) + " (found " +
+                                        std::to_string(d) + ")");
+    }
+    hip::check(nsh_set_device(device), "rccl_self_test: set device");
+    remote::rccl_transport::uid id{};
+    ck(L.get_unique_id(&id), "ncclGetUniqueId");
+    void* comm = nullptr;
+    ck(reinterpret_cast<remote::rccl_transport::init_fn>(L.comm_init_rank)(&comm, 1, id, 0), "ncclCommInitRank(nranks=1)");
+    std::string failure;
+    try {
+        ck(L.group_start(), "ncclGroupStart");
+        const int rs = L.send(src, bytes, /*ncclInt8*/ 0, peer, comm, stream);
+        const int rr = L.recv(dst, bytes, /*ncclInt8*/ 0, peer, comm, stream);
+        const int re = L.group_end(); // always closed, whatever the two calls returned
+        ck(rs, "ncclSend");
+        ck(rr, "ncclRecv");
+        ck(re, "ncclGroupEnd");
+        hip::check(nsh_stream_sync(stream), "rccl_self_test: stream sync");
+        int ae = 0;
+        if (L.async_error) {
+            ck(L.async_error(comm, &ae), "ncclCommGetAsyncError");
+            ck(ae, "asynchronous communicator error");
+        }
+    } catch (const std::exception& e) {
+        failure = e.what();
+    }
+    L.comm_destroy(comm);
+    if (!failure.empty()) throw std::runtime_error(failure);
 }
 
 // ---- adapter ---------------------------------------------------------------------------

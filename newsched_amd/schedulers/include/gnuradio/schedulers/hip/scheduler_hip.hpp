@@ -63,12 +63,30 @@ public:
     // What the last initialize() fused: blocks that replaced chains, and the chains.
     const hip::fusion_result& fusion_plan() const { return _plan; }
 
+    // Kernel timing of the partition's work() calls (off by default; switch it between runs).
+    // Each call gets an event pair that its kernel launch records as part of its own dispatch
+    // (nsh_time_next_launch, no extra stream packets); a call that launches nothing (nop blocks,
+    // sinks) is not counted (nsh_timed_launches). kernel_stats() waits for the recorded events
+    // and returns the totals per block (fused blocks under their own alias) since the last
+    // reset_kernel_stats(); call it between runs.
+    struct kernel_stat {
+        std::string block;
+        double kernel_ms = 0;   // summed start-to-end time of the timed launches
+        uint64_t launches = 0;  // work() calls that launched (and recorded their pair)
+        uint64_t items = 0;     // items those calls produced on their first output
+    };
+    void set_kernel_timing(bool on);
+    std::vector<kernel_stat> kernel_stats();
+    void reset_kernel_stats();
+
 protected:
     thread_hooks hooks_for_group(const block_group_properties&) override;
     std::vector<block_group_properties> plan_groups(flat_graph_sptr fg) override;
 
 private:
     void release_fused();
+    struct launch_timer;
+    std::shared_ptr<launch_timer> _timer;
     int _device;
     void* _stream = nullptr;
     bool _fusion = true;

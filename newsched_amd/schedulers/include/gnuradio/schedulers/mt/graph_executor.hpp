@@ -6,21 +6,31 @@
 #include <gnuradio/block.hpp>
 #include <gnuradio/executor.hpp>
 #include <gnuradio/schedulers/mt/buffer_management.hpp>
+#include <functional>
 #include <map>
 #include <set>
 
 namespace gr {
 namespace schedulers {
 
+// Called on the executing thread around each do_work() call: before(b), then after(b, n) with the
+// items the call produced on its first output (0 for a sink, -1 when do_work threw). scheduler_hip
+// times its partition's kernel launches with them.
+struct work_hooks {
+    std::function<void(const block_sptr&)> before;
+    std::function<void(const block_sptr&, int)> after;
+};
+
 class graph_executor : public executor
 {
 public:
     explicit graph_executor(const std::string& name) : executor(name) {}
 
-    void initialize(buffer_manager::sptr bufman, std::vector<block_sptr> blocks)
+    void initialize(buffer_manager::sptr bufman, std::vector<block_sptr> blocks, work_hooks hooks = {})
     {
         _bufman = std::move(bufman);
         d_blocks = std::move(blocks);
+        _hooks = std::move(hooks);
     }
 
     std::map<nodeid_t, executor_iteration_status> run_one_iteration(std::vector<block_sptr> blocks = {});
@@ -46,6 +56,7 @@ private:
     void finish(const block_sptr& b);
     std::vector<block_sptr> d_blocks;
     buffer_manager::sptr _bufman;
+    work_hooks _hooks;
     std::set<nodeid_t> _finished;
     static constexpr int s_min_items_to_process = 1;
     static constexpr int s_min_buf_items = 1;

@@ -21,6 +21,7 @@ struct thread_hooks {
     std::function<void()> on_thread_start; // e.g. bind device + partition stream
     std::function<void()> on_flush;        // e.g. drain the partition stream
     int queue_spin_us = 0;                 // spin this long on an empty queue before sleeping
+    work_hooks on_work;                    // around every do_work() call (e.g. kernel timing)
 };
 
 class thread_wrapper : public neighbor_interface, public std::enable_shared_from_this<thread_wrapper>

@@ -135,7 +135,17 @@ std::map<nodeid_t, executor_iteration_status> graph_executor::run_one_iteration(
         // ---- work ------------------------------------------------------------------
         work_return_code_t ret;
         while (true) {
-            ret = b->do_work(win, wout);
+            if (_hooks.before) _hooks.before(b);
+            try {
+                ret = b->do_work(win, wout);
+            } catch (...) {
+                if (_hooks.after) _hooks.after(b, -1);
+                throw;
+            }
+            if (_hooks.after)
+                _hooks.after(b, (ret == work_return_code_t::WORK_OK || ret == work_return_code_t::WORK_DONE) && !wout.empty()
+                                    ? std::max(wout[0].n_produced, 0)
+                                    : 0);
             if (ret == work_return_code_t::WORK_OK || ret == work_return_code_t::WORK_DONE) break;
             if (ret == work_return_code_t::WORK_INSUFFICIENT_INPUT_ITEMS) {
                 if (wout.empty()) break;

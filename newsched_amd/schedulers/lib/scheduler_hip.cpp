@@ -1,15 +1,110 @@
 // GPU scheduler domain (see scheduler_hip.hpp).
+#include <atomic>
 #include <chrono>
 #include <gnuradio/hip_context.hpp>
 #include <gnuradio/schedulers/hip/scheduler_hip.hpp>
+#include <map>
+#include <mutex>
 
 #include "nsh_hip.h"
 
 namespace gr {
 namespace schedulers {
 
+// Per-block event pairs of the timed work() calls. Written by the partition thread inside a run,
+// read (folded) by the caller between runs; the mutex keeps the two apart anyway.
+struct scheduler_hip::launch_timer {
+    struct pairs {
+        std::string alias;
+        std::vector<std::pair<void*, void*>> ev; // pool; [0, used) armed or recorded since the last fold
+        std::vector<uint64_t> items;             // per recorded pair
+        size_t used = 0;
+        kernel_stat done;                        // folded totals
+    };
+    std::atomic<bool> on{ false };
+    std::mutex m;
+    std::map<nodeid_t, pairs> blocks;
+    uint64_t count_before = 0;
+
+    ~launch_timer()
+    {
+        for (auto& kv : blocks)
+            for (auto& e : kv.second.ev) {
+                nsh_event_destroy(e.first);
+                nsh_event_destroy(e.second);
+            }
+    }
+    void fold(pairs& p)
+    {
+        for (size_t i = 0; i < p.used; ++i) {
+            float ms = 0;
+            hip::check(nsh_event_sync(p.ev[i].second), "scheduler_hip: kernel timing");
+            hip::check(nsh_event_elapsed_ms(p.ev[i].first, p.ev[i].second, &ms), "scheduler_hip: kernel timing");
+            p.done.kernel_ms += ms;
+            p.done.launches += 1;
+            p.done.items += p.items[i];
+        }
+        p.used = 0;
+        p.items.clear();
+    }
+    void before(const block_sptr& b)
+    {
+        if (!on.load(std::memory_order_relaxed)) return;
+        std::lock_guard<std::mutex> g(m);
+        auto& p = blocks[b->id()];
+        if (p.alias.empty()) p.alias = b->alias();
+        if (p.used >= 4096) fold(p); // a long unread series
+        if (p.used == p.ev.size()) {
+            std::pair<void*, void*> e{ nullptr, nullptr };
+            hip::check(nsh_event_create(&e.first), "scheduler_hip: kernel timing");
+            hip::check(nsh_event_create(&e.second), "scheduler_hip: kernel timing");
+            p.ev.push_back(e);
+        }
+        hip::check(nsh_timed_launches(&count_before), "scheduler_hip: kernel timing");
+        hip::check(nsh_time_next_launch(p.ev[p.used].first, p.ev[p.used].second), "scheduler_hip: kernel timing");
+    }
+    void after(const block_sptr& b, int produced)
+    {
+        if (!on.load(std::memory_order_relaxed)) return;
+        std::lock_guard<std::mutex> g(m);
+        uint64_t now = 0;
+        nsh_time_next_launch(nullptr, nullptr); // whatever happened, nothing stays armed
+        hip::check(nsh_timed_launches(&now), "scheduler_hip: kernel timing");
+        auto it = blocks.find(b->id());
+        if (it == blocks.end() || now == count_before || produced < 0) return; // nothing launched: pair unused
+        it->second.items.push_back((uint64_t)produced);
+        ++it->second.used;
+    }
+};
+
+void scheduler_hip::set_kernel_timing(bool on) { _timer->on.store(on); }
+
+std::vector<scheduler_hip::kernel_stat> scheduler_hip::kernel_stats()
+{
+    std::lock_guard<std::mutex> g(_timer->m);
+    std::vector<kernel_stat> out;
+    for (auto& kv : _timer->blocks) {
+        _timer->fold(kv.second);
+        if (kv.second.done.launches == 0) continue;
+        kernel_stat k = kv.second.done;
+        k.block = kv.second.alias;
+        out.push_back(k);
+    }
+    return out;
+}
+
+void scheduler_hip::reset_kernel_stats()
+{
+    std::lock_guard<std::mutex> g(_timer->m);
+    for (auto& kv : _timer->blocks) {
+        kv.second.used = 0;
+        kv.second.items.clear();
+        kv.second.done = kernel_stat();
+    }
+}
+
 scheduler_hip::scheduler_hip(const std::string name, int device, size_t fixed_buf_size)
-    : scheduler_mt(name, fixed_buf_size), _device(device)
+    : scheduler_mt(name, fixed_buf_size), _timer(std::make_shared<launch_timer>()), _device(device)
 {
     hip::check(nsh_stream_create(device, &_stream), "scheduler_hip: stream");
     _default_buf_factory = hip_buffer::make;
@@ -91,6 +186,9 @@ thread_hooks scheduler_hip::hooks_for_group(const block_group_properties&)
     // one thread per GPU partition: spinning briefly on its queue takes the futex wake-up out
     // of each run's start (the notification arrives within microseconds of the last one)
     h.queue_spin_us = 200;
+    auto t = _timer;
+    h.on_work.before = [t](const block_sptr& b) { t->before(b); };
+    h.on_work.after = [t](const block_sptr& b, int produced) { t->after(b, produced); };
     return h;
 }
 

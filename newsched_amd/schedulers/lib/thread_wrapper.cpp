@@ -15,7 +15,7 @@ thread_wrapper::thread_wrapper(int id, block_group_properties bgp, buffer_manage
       _on_finished(std::move(on_finished)), _id(id), _thread_index(thread_index)
 {
     _exec = std::make_unique<graph_executor>(bgp.name());
-    _exec->initialize(std::move(bufman), d_blocks);
+    _exec->initialize(std::move(bufman), d_blocks, _hooks.on_work);
     d_thread = std::thread(thread_body, this);
 }
 

@@ -218,29 +218,34 @@ TEST(SchedulerMTTest, RestartRunsAgain)
 
 TEST(SchedulerMTTest, CpuFirAcrossChunks)
 {
-    std::vector<float> h(127);
-    for (int k = 0; k < 127; ++k) h[k] = 0.02f * std::cos(0.1f * k) * (k % 7 == 3 ? -1.0f : 1.0f);
     std::vector<gr_complex> x(100003);
     for (size_t i = 0; i < x.size(); ++i) x[i] = gr_complex(std::sin(0.001f * i * i), std::cos(0.37f * i));
-    for (int D : { 1, 2, 4 }) {
-        auto src = blocks::vector_source_c::make(x);
-        auto fir = blocks::fir_filter_ccf::make(h, D);
-        auto snk = blocks::vector_sink_c::make();
-        auto fg = flowgraph::make();
-        fg->connect(src, 0, fir, 0);
-        fg->connect(fir, 0, snk, 0);
-        fg->set_scheduler(schedulers::scheduler_mt::make("mt", 4096)); // many small work() calls
-        fg->validate();
-        fg->run();
-        const auto y = snk->data();
-        const auto r = fir_ref(x, h, D);
-        EXPECT_EQ(y.size(), r.size());
-        double maxerr = 0, scale = 0;
-        for (size_t i = 0; i < std::min(y.size(), r.size()); ++i) {
-            maxerr = std::max(maxerr, (double)std::abs(y[i] - r[i]));
-            scale = std::max(scale, (double)std::abs(r[i]));
+    // every tap-residue shape of the rolling-window kernel (blocks_cpu.cpp): fewer taps than one
+    // 8-tap stride, exact multiples, one over, and the C3 / C5 length
+    for (int L : { 1, 2, 7, 8, 9, 16, 17, 63, 127, 128, 161 }) {
+        std::vector<float> h(L);
+        for (int k = 0; k < L; ++k) h[k] = 0.02f * std::cos(0.1f * k) * (k % 7 == 3 ? -1.0f : 1.0f);
+        for (int D : { 1, 2, 4 }) {
+            auto src = blocks::vector_source_c::make(x);
+            auto fir = blocks::fir_filter_ccf::make(h, D);
+            auto snk = blocks::vector_sink_c::make();
+            auto fg = flowgraph::make();
+            fg->connect(src, 0, fir, 0);
+            fg->connect(fir, 0, snk, 0);
+            fg->set_scheduler(schedulers::scheduler_mt::make("mt", 4096)); // many small work() calls
+            fg->validate();
+            fg->run();
+            const auto y = snk->data();
+            const auto r = fir_ref(x, h, D);
+            EXPECT_EQ(y.size(), r.size());
+            double maxerr = 0, scale = 0;
+            for (size_t i = 0; i < std::min(y.size(), r.size()); ++i) {
+                maxerr = std::max(maxerr, (double)std::abs(y[i] - r[i]));
+                scale = std::max(scale, (double)std::abs(r[i]));
+            }
+            if (!(maxerr <= 1e-5 * scale)) std::printf("  L=%d D=%d maxerr %.3g scale %.3g\n", L, D, maxerr, scale);
+            EXPECT_TRUE(maxerr <= 1e-5 * scale);
         }
-        EXPECT_TRUE(maxerr <= 1e-5 * scale);
     }
 }
 

@@ -13,7 +13,7 @@ import pytest
 from tests.conftest import ROOT
 
 
-ARGS = ["--steps", "3", "--warmup", "1", "--log2n", "22", "--out-buf-mib", "64", "--no-cpu"]
+ARGS = ["--steps", "3", "--warmup", "1", "--log2n", "22", "--out-buf-mib", "64", "--no-cpu", "--legs-log2n", "22"]
 
 
 def _json_line(stdout):
@@ -82,6 +82,16 @@ def test_bench_one_gpu(torch_cuda):
     cp = d["roofline"]["copy_measured"]  # the measured copy ceiling beside the spec peak
     assert cp["kernel"] == "k_copy_v4" and 0 < cp["frac_of_peak"] < 1 and d["roofline"]["frac_of_copy"] > 0
     assert d["config"]["workload"].startswith("C3")
+    # the other single-GPU configs beside the headline, each with its kernel roofline and parity
+    for leg in ("c2", "c4", "decim2", "decim4"):
+        L = d[leg]
+        assert "error" not in L, (leg, L)
+        assert L["parity"]["ok"], (leg, L)
+        assert L["timed_launches"] >= 5 and 0 < L["frac"] < 1.2 and L["value"] > 0, (leg, L)
+        assert L["launching_blocks"] == 1, (leg, L)  # fused: one launching block per flowgraph
+    assert d["c2"]["parity"]["mismatches"] == 0
+    assert "multiply_const" in d["c2"]["block"] and "channelizer" in d["c4"]["block"], d
+    assert d["c1"]["value"] > 0 and d["c1"]["threads"] == 4
 
 
 @pytest.mark.gpu
@@ -101,6 +111,32 @@ def test_fir_bench_stats_cumulative(torch_cuda):
         assert st["kernel_ms"] > prev["kernel_ms"]
         prev = st
     fb.close()
+
+
+@pytest.mark.gpu
+def test_chain_bench_kernel_timing(torch_cuda):
+    """scheduler_hip's kernel timing (nsr_chain_bench_stats): only launching work() calls are
+    counted -- the nop source / head and the sink are not -- and with fusion the four
+    multiply_const_cc blocks are one block with one launch per batch, timed every launch."""
+    import numpy as np
+    from newsched_amd import nsr
+    import bench
+
+    n = 1 << 20
+    cb = nsr.ChainBench(nsr.CHAIN_MUL_CONST_CC, bench.C2_KS, n, out_buf_bytes=16 << 20)
+    assert cb.stats()["launches"] == 0
+    cb.set_batches(3)
+    cb.run()
+    st = cb.stats()
+    assert st["launching_blocks"] == 1 and st["launches"] == 3 and st["samples"] == 3 * n, st
+    assert st["kernel_ms"] > 0
+    cb.close()
+    # the decimator: output samples counted (n / D per batch)
+    cb = nsr.ChainBench(nsr.CHAIN_FIR, bench.firwin(127, 0.45), n, decim=4, out_buf_bytes=16 << 20)
+    cb.run()
+    st = cb.stats()
+    assert st["launches"] >= 1 and st["samples"] == n // 4, st
+    cb.close()
 
 
 @pytest.mark.gpu
