@@ -389,7 +389,8 @@ def run_chain_leg(a, name, spec, rank, device, barrier, dist, tdev, torch, orc, 
     n, D = spec["n"], spec["decim"]
     first = rank * n
     fb = nsr.ChainBench(getattr(nsr, spec["kind"]), spec["params"], n, device=device, decim=D, first_index=first,
-                        out_buf_bytes=max(64 << 20, n * 8 // D))
+                        out_buf_bytes=max(64 << 20, n * 8))  # one launch per batch (decimators: the
+    # buffer manager sizes a decimating block's output edge at fixed_buf_size / D)
     try:
         t0 = time.perf_counter()
         fb.set_batches(4)
@@ -419,6 +420,8 @@ def run_chain_leg(a, name, spec, rank, device, barrier, dist, tdev, torch, orc, 
     finally:
         fb.close()
     launches = st["launches"] - st0["launches"]
+    if launches <= 0:
+        raise RuntimeError("no timed launches of %s (scheduler_hip kernel timing)" % st["block"])
     kms = st["kernel_ms"] - st0["kernel_ms"]
     in_samples = (st["samples"] - st0["samples"]) * D
     avg_ms = kms / launches

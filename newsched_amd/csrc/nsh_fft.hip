@@ -281,10 +281,10 @@ int nsh_fft1024_c2c(const float* in, float* out, int64_t nframes, int inverse, v
     const float2* tw = nullptr;
     if (int rc = twiddles(dev, &tw)) return rc;
     if (inverse)
-        hipLaunchKernelGGL(k_fft1024<true>, dim3(frame_grid(nframes, FPW, NSH_FFT_CAP)), dim3(NT), 0, nsh::S(stream),
+        nsh::launch(k_fft1024<true>, dim3(frame_grid(nframes, FPW, NSH_FFT_CAP)), dim3(NT), 0, nsh::S(stream),
                            (const float2*)in, (float2*)out, nframes, tw);
     else
-        hipLaunchKernelGGL(k_fft1024<false>, dim3(frame_grid(nframes, FPW, NSH_FFT_CAP)), dim3(NT), 0, nsh::S(stream),
+        nsh::launch(k_fft1024<false>, dim3(frame_grid(nframes, FPW, NSH_FFT_CAP)), dim3(NT), 0, nsh::S(stream),
                            (const float2*)in, (float2*)out, nframes, tw);
     NSH_CK_LAUNCH("nsh_fft1024_c2c");
     return 0;
@@ -299,7 +299,7 @@ int nsh_channelizer1024(const float* in, float* out, const float* w, int64_t nfr
     NSH_CK(hipGetDevice(&dev));
     const float2* tw = nullptr;
     if (int rc = twiddles(dev, &tw)) return rc;
-    hipLaunchKernelGGL(k_chan1024<CFPW>, dim3(frame_grid(nframes, CFPW, CFPW == 4 ? NSH_CHAN_CAP4 : NSH_CHAN_CAP)), dim3(64 * CFPW), 0, nsh::S(stream),
+    nsh::launch(k_chan1024<CFPW>, dim3(frame_grid(nframes, CFPW, CFPW == 4 ? NSH_CHAN_CAP4 : NSH_CHAN_CAP)), dim3(64 * CFPW), 0, nsh::S(stream),
                        (const float2*)in, (float2*)out, nframes, tw, (const float2*)w);
     NSH_CK_LAUNCH("nsh_channelizer1024");
     return 0;

@@ -155,17 +155,17 @@ int launch_map_c(const float* in, float* out, int64_t n, Op op, hipStream_t s, c
     if (a16) {
         const int64_t nv = n / 2;
         if (nv > 0) {
-            hipLaunchKernelGGL(k_map_c_v4<Op>, dim3(tile_grid(nv)), dim3(kBlock), 0, s,
+            nsh::launch(k_map_c_v4<Op>, dim3(tile_grid(nv)), dim3(kBlock), 0, s,
                                (const float4*)in, (float4*)out, nv, op);
             NSH_CK_LAUNCH(what);
         }
         if (n & 1) {
-            hipLaunchKernelGGL(k_map_c_v2<Op>, dim3(1), dim3(kBlock), 0, s,
+            nsh::launch(k_map_c_v2<Op>, dim3(1), dim3(kBlock), 0, s,
                                (const float2*)in + (n - 1), (float2*)out + (n - 1), (int64_t)1, op);
             NSH_CK_LAUNCH(what);
         }
     } else {
-        hipLaunchKernelGGL(k_map_c_v2<Op>, dim3(nsh::stream_grid(n, kBlock)), dim3(kBlock), 0, s,
+        nsh::launch(k_map_c_v2<Op>, dim3(nsh::stream_grid(n, kBlock)), dim3(kBlock), 0, s,
                            (const float2*)in, (float2*)out, n, op);
         NSH_CK_LAUNCH(what);
     }
@@ -224,17 +224,17 @@ int launch_bin(const float* a, const float* b, float* out, int64_t n, hipStream_
     if (a16) {
         const int64_t nv = n / 2;
         if (nv > 0) {
-            hipLaunchKernelGGL(k_bin_v4<OP>, dim3(tile_grid(nv)), dim3(kBlock), 0, s,
+            nsh::launch(k_bin_v4<OP>, dim3(tile_grid(nv)), dim3(kBlock), 0, s,
                                (const float4*)a, (const float4*)b, (float4*)out, nv);
             NSH_CK_LAUNCH(what);
         }
         if (n & 1) {
-            hipLaunchKernelGGL(k_bin_v2<OP>, dim3(1), dim3(kBlock), 0, s, (const float2*)a + (n - 1),
+            nsh::launch(k_bin_v2<OP>, dim3(1), dim3(kBlock), 0, s, (const float2*)a + (n - 1),
                                (const float2*)b + (n - 1), (float2*)out + (n - 1), (int64_t)1);
             NSH_CK_LAUNCH(what);
         }
     } else {
-        hipLaunchKernelGGL(k_bin_v2<OP>, dim3(nsh::stream_grid(n, kBlock)), dim3(kBlock), 0, s,
+        nsh::launch(k_bin_v2<OP>, dim3(nsh::stream_grid(n, kBlock)), dim3(kBlock), 0, s,
                            (const float2*)a, (const float2*)b, (float2*)out, n);
         NSH_CK_LAUNCH(what);
     }
@@ -294,7 +294,7 @@ int nsh_copy(const void* in, void* out, size_t bytes, void* stream)
     hipStream_t s = nsh::S(stream);
     if ((uintptr_t)in % 16 == 0 && (uintptr_t)out % 16 == 0 && bytes >= 16) {
         const int64_t nv = (int64_t)(bytes / 16);
-        hipLaunchKernelGGL(k_copy_v4, dim3(tile_grid(nv)), dim3(kBlock), 0, s, (const float4*)in, (float4*)out, nv);
+        nsh::launch(k_copy_v4, dim3(tile_grid(nv)), dim3(kBlock), 0, s, (const float4*)in, (float4*)out, nv);
         NSH_CK_LAUNCH("nsh_copy");
         const size_t done = (size_t)nv * 16;
         if (done < bytes)
@@ -319,17 +319,17 @@ int nsh_mul_const_ff(const float* in, float* out, int64_t n, float k, void* stre
     if ((uintptr_t)in % 16 == 0 && (uintptr_t)out % 16 == 0) {
         const int64_t nv = n / 4;
         if (nv) {
-            hipLaunchKernelGGL(k_mulc_f_v4, dim3(tile_grid(nv)), dim3(kBlock), 0, s,
+            nsh::launch(k_mulc_f_v4, dim3(tile_grid(nv)), dim3(kBlock), 0, s,
                                (const float4*)in, (float4*)out, nv, k);
             NSH_CK_LAUNCH("nsh_mul_const_ff");
         }
         if (n % 4) {
-            hipLaunchKernelGGL(k_mulc_f_v1, dim3(1), dim3(kBlock), 0, s, in + nv * 4, out + nv * 4, n % 4, k);
+            nsh::launch(k_mulc_f_v1, dim3(1), dim3(kBlock), 0, s, in + nv * 4, out + nv * 4, n % 4, k);
             NSH_CK_LAUNCH("nsh_mul_const_ff");
         }
         return 0;
     }
-    hipLaunchKernelGGL(k_mulc_f_v1, dim3(nsh::stream_grid(n, kBlock)), dim3(kBlock), 0, s, in, out, n, k);
+    nsh::launch(k_mulc_f_v1, dim3(nsh::stream_grid(n, kBlock)), dim3(kBlock), 0, s, in, out, n, k);
     NSH_CK_LAUNCH("nsh_mul_const_ff");
     return 0;
 }
@@ -375,10 +375,10 @@ int nsh_mul_const_vcc(const float* in, float* out, const float* k_dev, int vlen,
     hipStream_t s = nsh::S(stream);
     const unsigned grid = nsh::stream_grid(n, kBlock);
     if ((vlen & (vlen - 1)) == 0)
-        hipLaunchKernelGGL(k_mulc_vec<true>, dim3(grid), dim3(kBlock), 0, s, (const float2*)in, (float2*)out,
+        nsh::launch(k_mulc_vec<true>, dim3(grid), dim3(kBlock), 0, s, (const float2*)in, (float2*)out,
                            (const float2*)k_dev, vlen, n);
     else
-        hipLaunchKernelGGL(k_mulc_vec<false>, dim3(grid), dim3(kBlock), 0, s, (const float2*)in, (float2*)out,
+        nsh::launch(k_mulc_vec<false>, dim3(grid), dim3(kBlock), 0, s, (const float2*)in, (float2*)out,
                            (const float2*)k_dev, vlen, n);
     NSH_CK_LAUNCH("nsh_mul_const_vcc");
     return 0;
