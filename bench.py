@@ -389,8 +389,7 @@ def run_chain_leg(a, name, spec, rank, device, barrier, dist, tdev, torch, orc, 
     n, D = spec["n"], spec["decim"]
     first = rank * n
     fb = nsr.ChainBench(getattr(nsr, spec["kind"]), spec["params"], n, device=device, decim=D, first_index=first,
-                        out_buf_bytes=max(64 << 20, n * 8))  # one launch per batch (decimators: the
-    # buffer manager sizes a decimating block's output edge at fixed_buf_size / D)
+                        out_buf_bytes=max(64 << 20, n * 8))  # edges of a whole batch: one launch per batch
     try:
         t0 = time.perf_counter()
         fb.set_batches(4)

@@ -89,6 +89,7 @@ def test_bench_one_gpu(torch_cuda):
         assert L["parity"]["ok"], (leg, L)
         assert L["timed_launches"] >= 5 and 0 < L["frac"] < 1.2 and L["value"] > 0, (leg, L)
         assert L["launching_blocks"] == 1, (leg, L)  # fused: one launching block per flowgraph
+        assert L["timed_launches"] == L["steps"], (leg, L)  # one launch per batch
     assert d["c2"]["parity"]["mismatches"] == 0
     assert d["c2"]["block"].startswith("fused(multiply_const") and d["c4"]["block"].startswith("fused(fft_vcc"), d
     assert d["c1"]["value"] > 0 and d["c1"]["threads"] == 4
