@@ -414,6 +414,7 @@ int nsr_c5_create(int group, int n_groups, int dev, const float* taps, int ntaps
         o.transport = transport && *transport ? transport : "auto";
         o.device = dev;
         o.timeout_s = 120;
+        o.stall_timeout_s = 600; // a receiver wedged with its socket open: an error, not a hang
         b->da = domain_adapter_remote_conf::make(o);
         for (int g = 0; g < n_groups; ++g) {
             scheduler_sptr sc;

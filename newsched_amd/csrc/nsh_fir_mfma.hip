@@ -349,7 +349,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void k
             const unsigned k = blockIdx.x % XQ_N;
             const unsigned i = __hip_atomic_fetch_add(xq + XQ_LINE * k, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             // i < subcap always, on a queue whose counters were zeroed (xq_reset after a failed
-            // call): the bound keeps a stale counter from writing into the next sub-queue
+            // call): the bound keeps a stale counter from writing into the next sub-queue, and
+            // k_fir_exact12 refilters the whole launch if the count ever exceeds it
             if (i < (unsigned)xq_subcap(gridDim.x))
                 __hip_atomic_store(xq + XQ_E + k * xq_subcap(gridDim.x) + i, (unsigned)(ch << 1) | (m >= 0x7f800000u ? 1u : 0u),
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -445,20 +446,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NSH_X12_PER
         __hip_atomic_store(xq_next + XQ_LINE * tid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // every wave: the XQ_N counters (one per lane) and their inclusive prefix sum
     unsigned incl = __hip_atomic_load(xq + XQ_LINE * lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // a sub-queue that counted more appends than it holds lost entries (never on a queue whose
+    // counters were zeroed: xq_reset after a failed call): then every chunk of the
+    // launch is filtered again here in the fp32 direct form -- slow, but no output is left unwritten
+    const bool over = __ballot(incl > (unsigned)subcap) != 0;
     incl = min(incl, (unsigned)subcap); // entries past a sub-queue's capacity were never written
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
         const unsigned t = __shfl_up(incl, d);
         if (lane >= d) incl += t;
     }
-    const unsigned cnt = __builtin_amdgcn_readlane(incl, 63);
+    const int64_t nchunks = (n_out + geom12<Q>::CHUNK - 1) / geom12<Q>::CHUNK;
+    const unsigned cnt = over ? (unsigned)nchunks : __builtin_amdgcn_readlane(incl, 63);
     if (cnt == 0) return; // nothing queued (the common case)
     auto entry = [&](unsigned i) {
+        if (over) return (i << 1) | 1u; // chunk i, direct form
         const int k = __popcll(__ballot(incl <= i)); // sub-queue holding queued chunk i (prefix sums ascend)
         const unsigned start = k ? __shfl(incl, k - 1) : 0u;
         return __hip_atomic_load(xq + XQ_E + k * subcap + (i - start), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
-    const int64_t nchunks = (n_out + geom12<Q>::CHUNK - 1) / geom12<Q>::CHUNK;
     for (unsigned i = blockIdx.x; i < cnt; i += gridDim.x) {
         const unsigned e = entry(i);
         if ((int64_t)(e >> 1) >= nchunks) continue; // never for a queue this launch filled (defensive)
@@ -1182,15 +1188,17 @@ __global__ __launch_bounds__(256) void k_fir_exact13(const float2* __restrict__ 
     if (blockIdx.x == 0 && tid < 64)
         __hip_atomic_store(xq_next + XQ_LINE * tid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     unsigned incl = __hip_atomic_load(xq + XQ_LINE * lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool over = __ballot(incl > (unsigned)subcap) != 0; // lost entries: every chunk again (k_fir_exact12)
     incl = min(incl, (unsigned)subcap);
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
         const unsigned t = __shfl_up(incl, d);
         if (lane >= d) incl += t;
     }
-    const unsigned cnt = __builtin_amdgcn_readlane(incl, 63);
+    const unsigned cnt = over ? (unsigned)((n_out + G::CHUNK - 1) / G::CHUNK) : __builtin_amdgcn_readlane(incl, 63);
     if (cnt == 0) return; // nothing queued (the common case)
     auto entry = [&](unsigned i) {
+        if (over) return (i << 1) | 1u; // chunk i, direct form
         const int k = __popcll(__ballot(incl <= i));
         const unsigned start = k ? __shfl(incl, k - 1) : 0u;
         return __hip_atomic_load(xq + XQ_E + k * subcap + (i - start), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

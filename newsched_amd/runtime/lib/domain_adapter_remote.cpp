@@ -367,8 +367,10 @@ int self_connect_hook()
     return std::strcmp(f, "hello") == 0 ? 2 : 1;
 }
 
+// soft = true: at the timeout return nullptr instead of throwing (rendezvous mode re-reads the
+// published port then: the entry may have been stale)
 std::shared_ptr<channel> connect_retry(const std::string& host, int port, double timeout_s,
-                                       const std::atomic<bool>& cancel, int& force_self)
+                                       const std::atomic<bool>& cancel, int& force_self, bool soft = false)
 {
     const auto t0 = clk::now();
     const sockaddr_in a = resolve(host, port);
@@ -392,8 +394,10 @@ std::shared_ptr<channel> connect_retry(const std::string& host, int port, double
             ::close(fd);
         }
         if (cancel.load()) throw std::runtime_error("remote edge: cancelled");
-        if (since(t0) > timeout_s)
+        if (since(t0) > timeout_s) {
+            if (soft) return nullptr;
             throw std::runtime_error("remote edge: cannot connect to " + host + ":" + std::to_string(port));
+        }
         std::this_thread::sleep_for(std::chrono::milliseconds(20));
     }
 }
@@ -1208,10 +1212,17 @@ void domain_adapter_remote::buffer_ready()
             for (;;) { // rendezvous, connect, hello; a wrong peer is dropped and the rendezvous retried
                 const double left = _opt.timeout_s - since(t0);
                 if (left <= 0) throw out_of_time();
-                const int port = _opt.rendezvous_dir.empty()
-                                     ? _opt.base_port + _crossing
-                                     : rdv_lookup(_opt.rendezvous_dir, _crossing, _opt.nonce, left, _closing);
-                auto ch = connect_retry(_opt.host, port, left, _closing, force_self);
+                const bool rdv = !_opt.rendezvous_dir.empty();
+                const int port = rdv ? rdv_lookup(_opt.rendezvous_dir, _crossing, _opt.nonce, left, _closing)
+                                     : _opt.base_port + _crossing;
+                // rendezvous: a published port nobody listens on may be a stale entry with this job's
+                // nonce (a receiver that was re-created, or died before removing it): connect for a
+                // short slice, then read the entry again -- a fresh receiver has republished it
+                auto ch = connect_retry(_opt.host, port, rdv ? std::min(left, 1.0) : left, _closing, force_self, rdv);
+                if (!ch) {
+                    refused("nothing listens on published port " + std::to_string(port) + "; reading the entry again");
+                    continue;
+                }
                 ch->send_bytes(&mine, sizeof(mine));
                 if (!recv_hello(*ch, peer, _opt.timeout_s - since(t0), _closing)) {
                     if (_closing.load()) throw std::runtime_error("remote edge: cancelled");
@@ -1264,9 +1275,13 @@ void domain_adapter_remote::buffer_ready()
                 const double left = _opt.timeout_s - since(t0);
                 if (left <= 0) throw out_of_time();
                 auto ch = accept_one(_lfd, left, _closing);
-                if (!recv_hello(*ch, peer, _opt.timeout_s - since(t0), _closing)) {
+                // a real sender says hello as soon as it connects: a client silent for 2 s is dropped,
+                // so the accept loop reaches the next queued connection (the real sender waits in
+                // the backlog for our hello meanwhile)
+                if (!recv_hello(*ch, peer, std::min(_opt.timeout_s - since(t0), 2.0), _closing)) {
                     if (_closing.load()) throw std::runtime_error("remote edge: cancelled");
-                    refused("a client connected and sent no hello");
+                    refused("a client connected and sent no hello within 2 s");
+                    ch->reset_on_close();
                     continue;
                 }
                 const std::string why = refuse_reason(peer, R_SEND, _opt.nonce);

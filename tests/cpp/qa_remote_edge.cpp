@@ -11,7 +11,11 @@
 
 #include <chrono>
 #include <cstdlib>
+#include <arpa/inet.h>
 #include <dlfcn.h>
+#include <netinet/in.h>
+#include <sys/socket.h>
+#include <unistd.h>
 #include <thread>
 #include <gnuradio/blocklib/blocks/annotator.hpp>
 #include <gnuradio/blocklib/blocks/copy.hpp>
@@ -791,4 +795,108 @@ TEST(RemoteCpu, ForeignNonceRefused)
         EXPECT_TRUE(what.find("another job") != std::string::npos);
         EXPECT_TRUE(remote::peers_refused() >= 1);
     }
+}
+
+// A stale rendezvous entry with this job's nonce: before the receiver [rank 1]
+// exists, the sender [rank 0] finds <dir>/crossing0 naming a port nobody listens on (a receiver
+// that died before removing its entry). The receiver starts 1.5 s later and republishes; the
+// sender, which re-reads the entry after each 1 s connect slice, must pair with it and move the
+// data bit-exact -- instead of retrying the dead port until the timeout.
+TEST(RemoteCpu, StaleRendezvousEntry)
+{
+    auto o = opts();
+    if (o.rendezvous_dir.empty()) {
+        std::printf("  needs QA_RDV\n");
+        EXPECT_TRUE(false);
+        return;
+    }
+    if (rank() == 0) { // the stale entry: a port that was bound once and is closed now
+        const int fd = ::socket(AF_INET, SOCK_STREAM, 0);
+        sockaddr_in a{};
+        a.sin_family = AF_INET;
+        a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+        a.sin_port = 0;
+        ::bind(fd, reinterpret_cast<sockaddr*>(&a), sizeof(a));
+        socklen_t len = sizeof(a);
+        ::getsockname(fd, reinterpret_cast<sockaddr*>(&a), &len);
+        ::close(fd);
+        FILE* f = std::fopen((o.rendezvous_dir + "/crossing0").c_str(), "w");
+        std::fprintf(f, "%d %llu\n", (int)ntohs(a.sin_port), (unsigned long long)o.nonce);
+        std::fclose(f);
+    } else {
+        std::this_thread::sleep_for(std::chrono::milliseconds(1500));
+    }
+    const size_t n = 50000;
+    auto x = synth(n, 31);
+    auto src = blocks::vector_source_c::make(x);
+    auto cp0 = blocks::copy::make(sizeof(gr_complex));
+    auto cp1 = blocks::copy::make(sizeof(gr_complex));
+    auto snk = blocks::vector_sink_c::make(1, n);
+    auto fg = flowgraph::make();
+    fg->connect(src, 0, cp0, 0);
+    fg->connect(cp0, 0, cp1, 0);
+    fg->connect(cp1, 0, snk, 0);
+    auto s0 = sched_for(0, schedulers::scheduler_mt::make("r0", 8192));
+    auto s1 = sched_for(1, schedulers::scheduler_mt::make("r1", 8192));
+    fg->set_schedulers({ s0, s1 });
+    auto da = domain_adapter_remote_conf::make(o);
+    domain_conf_vec dc{ domain_conf(s0, { src, cp0 }, da), domain_conf(s1, { cp1, snk }, da) };
+    fg->partition(dc);
+    fg->run();
+    if (rank() == 1) EXPECT_TRUE(snk->data() == x);
+    if (rank() == 0) {
+        std::printf("  peers refused: %llu\n", (unsigned long long)remote::peers_refused());
+        EXPECT_TRUE(remote::peers_refused() >= 1); // the dead port was seen and left
+    }
+}
+
+// A silent client on the receiver's fixed port: rank 0 first connects a raw TCP
+// socket that never says hello and keeps it open, then starts the real sender. The receiver drops
+// the silent client after 2 s and pairs with the sender queued behind it (before, it waited for
+// the silent client until the timeout and both ends failed).
+TEST(RemoteCpu, SilentClientDropped)
+{
+    auto o = opts();
+    o.base_port += 180;
+    int silent = -1;
+    if (rank() == 0) {
+        sockaddr_in a{};
+        a.sin_family = AF_INET;
+        a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+        a.sin_port = htons((uint16_t)o.base_port);
+        for (int i = 0; i < 500 && silent < 0; ++i) { // until the receiver listens
+            const int fd = ::socket(AF_INET, SOCK_STREAM, 0);
+            if (::connect(fd, reinterpret_cast<sockaddr*>(&a), sizeof(a)) == 0)
+                silent = fd;
+            else {
+                ::close(fd);
+                std::this_thread::sleep_for(std::chrono::milliseconds(20));
+            }
+        }
+        EXPECT_TRUE(silent >= 0);
+        std::this_thread::sleep_for(std::chrono::milliseconds(200)); // queued first
+    }
+    const size_t n = 50000;
+    auto x = synth(n, 37);
+    auto src = blocks::vector_source_c::make(x);
+    auto cp0 = blocks::copy::make(sizeof(gr_complex));
+    auto cp1 = blocks::copy::make(sizeof(gr_complex));
+    auto snk = blocks::vector_sink_c::make(1, n);
+    auto fg = flowgraph::make();
+    fg->connect(src, 0, cp0, 0);
+    fg->connect(cp0, 0, cp1, 0);
+    fg->connect(cp1, 0, snk, 0);
+    auto s0 = sched_for(0, schedulers::scheduler_mt::make("r0", 8192));
+    auto s1 = sched_for(1, schedulers::scheduler_mt::make("r1", 8192));
+    fg->set_schedulers({ s0, s1 });
+    auto da = domain_adapter_remote_conf::make(o);
+    domain_conf_vec dc{ domain_conf(s0, { src, cp0 }, da), domain_conf(s1, { cp1, snk }, da) };
+    fg->partition(dc);
+    fg->run();
+    if (rank() == 1) {
+        EXPECT_TRUE(snk->data() == x);
+        std::printf("  peers refused: %llu\n", (unsigned long long)remote::peers_refused());
+        EXPECT_TRUE(remote::peers_refused() >= 1);
+    }
+    if (silent >= 0) ::close(silent);
 }

@@ -113,6 +113,21 @@ def test_foreign_nonce_refused():
     assert "another job" in outs[1]
 
 
+def test_stale_rendezvous_entry_is_read_again():
+    """a stale crossing entry carrying this job's nonce (a dead port) before the
+    receiver starts: the sender re-reads the entry after each short connect slice and pairs with
+    the receiver that republishes it; bit-exact, well inside the timeout."""
+    outs = run_pair("RemoteCpu.StaleRendezvousEntry", env_extra={"QA_TIMEOUT": "20"})
+    assert "nothing listens on published port" in outs[0]
+
+
+def test_silent_client_is_dropped():
+    """a client on the receiver's fixed port that never says hello is dropped after
+    2 s, and the real sender queued behind it pairs; bit-exact."""
+    outs = run_pair("RemoteCpu.SilentClientDropped", fixed_port=True, env_extra={"QA_TIMEOUT": "20"})
+    assert "sent no hello within 2 s" in outs[1]
+
+
 def test_rendezvous_dir_isolates_jobs():
     """Two pipelines of the same case at once, each with its own rendezvous directory and nonce:
     kernel-chosen ports, no collisions, both bit-exact."""
