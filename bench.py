@@ -426,13 +426,24 @@ def run_chain_leg(a, name, spec, rank, device, barrier, dist, tdev, torch, orc, 
     avg_ms = kms / launches
     achieved = spec["bps"] * (in_samples / launches) / (avg_ms * 1e-3) / 1e9
     world = dist.get_world_size() if dist is not None else 1
-    return {"workload": spec["workload"], "block": st["block"], "launching_blocks": st["launching_blocks"],
+    kernel = {"c2": "k_map_c_v4", "c4": "k_chan1024"}.get(name)
+    if kernel is None:  # the decimators: the kernel their plan resolves to
+        fp = nsh.FirPlan(spec["params"], D, device=device)
+        kernel = fp.kernel
+        fp.close()
+    out = {"workload": spec["workload"], "kernel": kernel, "block": st["block"], "launching_blocks": st["launching_blocks"],
             "steps": steps, "value": round(world * n * steps / el / 1e6, 1), "unit": "MSamples/s (input)",
             "ms_per_step": round(el / steps * 1e3, 4), "timed_launches": launches,
             "avg_launch_us": round(avg_ms * 1e3, 2), "bytes_per_input_sample": spec["bps"],
             "achieved_GBs": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBS, 4),
             "flowgraph_frac": round(spec["bps"] * n / (el / steps) / 1e9 / HBM_PEAK_GBS, 4),
             "clock_mhz": mhz, "parity": par}
+    tr, src = load_pmc_traffic(kernel, in_samples / launches, "pmc_legs.json")
+    if tr is not None:
+        out["traffic"] = int(tr)
+        out["traffic_source"] = ("HBM B/input sample from separate rocprofv3 --pmc passes (%s), scaled to this "
+                                 "launch size; not measured in this run" % src)
+    return out
 
 
 def run_c1_leg(reps=7):

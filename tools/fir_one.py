@@ -12,7 +12,7 @@ import torch
 from newsched_amd import nsh
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--algo", default="mfma", choices=["mfma", "direct", "f32", "casc"])
+ap.add_argument("--algo", default="mfma", choices=["mfma", "direct", "f32", "casc", "chan", "mul4"])
 ap.add_argument("--log2n", type=int, default=25)
 ap.add_argument("--reps", type=int, default=10)
 ap.add_argument("--decim", type=int, default=1)
@@ -24,7 +24,24 @@ nsh.synth(x, n, 0)
 y = torch.empty_like(x)
 hin = torch.zeros(126, dtype=torch.complex64, device="cuda")
 hout = torch.zeros_like(hin)
-if a.algo == "casc":  # C5's fused chain (nsh_fir_cascade_ccf): 4 x fir(firwin(127, 0.45), 2)
+if a.algo == "chan":  # C4's channelizer (nsh_channelizer1024), bench.py's weights
+    import bench
+
+    w = torch.from_numpy(bench.c4_weights()).cuda()
+    for _ in range(a.reps):
+        nsh.channelizer1024(x, y, w, n // 1024)
+
+    class p:
+        kernel = "k_chan1024"
+elif a.algo == "mul4":  # C2's fused chain (nsh_mul_const_chain_cc)
+    import bench
+
+    for _ in range(a.reps):
+        nsh.mul_const_chain_cc(x, y, n, bench.C2_KS)
+
+    class p:
+        kernel = "k_map_c_v4"
+elif a.algo == "casc":  # C5's fused chain (nsh_fir_cascade_ccf): 4 x fir(firwin(127, 0.45), 2)
     p = nsh.FirCascadePlan([(ss.firwin(127, 0.45).astype(np.float32), 2)] * 4)
     hc = torch.zeros(p.hist_len, dtype=torch.complex64, device="cuda")
     for _ in range(a.reps):

@@ -26,6 +26,9 @@ def kernel_key(name):
     m = re.search(r"(k_fir_\w+<[^>(]*>|k_copy_v4)", name)
     if m:
         return m.group(1).replace(" ", "")
+    m = re.search(r"(k_chan1024|k_map_c_v4|k_fft1024)", name)  # the stream / FFT kernels, by base name
+    if m:
+        return m.group(1)
     m = re.search(r"\d(k_fir_[a-z0-9_]+?)I((?:L[ib]-?\d+E)+)E", name)
     if m:
         return "%s<%s>" % (m.group(1), ",".join(re.findall(r"L[ib](-?\d+)E", m.group(2))))
