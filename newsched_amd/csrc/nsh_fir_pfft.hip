@@ -658,6 +658,9 @@ constexpr int IMG2 = 571; // odd: a 16-lane group's exchange-1 stores (16 phases
 // 4..7 arrive ~1.8k cycles early at B2 in the phase trace) measured 0.6-0.8 % faster than 0..3 in four two-library
 // A/Bs (r05zq; r05zo 2-3 %); 8..11 and 12..15 are 5-18 % slower (r05zp); after the wave's row loads
 // instead of before them, level or slower (r05zo).
+#ifndef NSH_PFFT2_REGX2
+#define NSH_PFFT2_REGX2 0
+#endif
 #ifndef NSH_PFFT2_INV_BASE
 #define NSH_PFFT2_INV_BASE 4
 #endif
@@ -922,12 +925,16 @@ __global__ __launch_bounds__(64 * P, 1) void k_fir_pfft2(pfft_args a)
 #pragma unroll
             for (int r = 1; r < 8; ++r) u[r] = cmul_tw(u[r], t2[r]);
             dft8<false>(u); // pass 2 -> dst[(j >> 3) 64 + (j & 7) + 8 r]
+#if NSH_PFFT2_REGX2
+            exchange2_regs(u); // probe: exchange 2 by lane swaps instead of the wave's image
+#else
             __builtin_amdgcn_wave_barrier();
 #pragma unroll
             for (int r = 0; r < 8; ++r) ib.x2[8 * r + (r >= 4 ? 3 : 0)] = u[r];
             __builtin_amdgcn_wave_barrier();
 #pragma unroll
             for (int r = 0; r < 8; ++r) u[r] = ib.b2[72 * r];
+#endif
 #pragma unroll
             for (int r = 1; r < 8; ++r) u[r] = cmul_tw(u[r], t3[r]);
             dft8<false>(u); // pass 3 -> X[j + 64 r]
