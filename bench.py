@@ -558,8 +558,10 @@ def main():
     ap.add_argument("--c5-fused", choices=["on", "off"], default="on",
                     help="C5's chain as the fused kernel (k_fir_pfft2<16>) on resident input, every rank")
     ap.add_argument("--c5-fused-log2n", type=int, default=28)
-    ap.add_argument("--legs", choices=["on", "off"], default="on",
-                    help="the other single-GPU configs beside the headline: C1 (CPU), C2, C4, decimators D=2/4")
+    ap.add_argument("--legs", choices=["auto", "on", "off"], default="auto",
+                    help="the other single-GPU configs beside the headline: C1 (CPU), C2, C4, decimators D=2/4 "
+                         "(auto: at world 1 only -- they are single-GPU configs, and a rank that fails one must "
+                         "not leave its peers waiting in the leg's barriers of a multi-GPU run)")
     ap.add_argument("--legs-log2n", type=int, default=28)
     ap.add_argument("--legs-warmup-s", type=float, default=0.3)
     ap.add_argument("--c5-log2n", type=int, default=26)
@@ -749,7 +751,7 @@ def main():
     if a.c5_fused == "on":
         out["c5_fused"] = run_c5_fused_leg(a, rank * (1 << a.c5_fused_log2n), device, barrier, dist, tdev, torch, orc, nsh)
 
-    if a.legs == "on":
+    if a.legs == "on" or (a.legs == "auto" and world == 1):
         for name, spec in chain_specs(a).items():
             try:
                 out[name] = run_chain_leg(a, name, spec, rank, device, barrier, dist, tdev, torch, orc, nsr, nsh)
