@@ -96,15 +96,34 @@ constexpr int WLDS = N + N / 16; // one wave's padded image
 __device__ __forceinline__ int pad(int i) { return i + (i >> 4); }
 
 template <bool INV>
-__device__ __forceinline__ cf twid(const cf* __restrict__ tw, int t)
+__device__ __forceinline__ cf conj_if(cf w)
 {
-    cf w = tw[t & (N - 1)];
     if (INV) w.y = -w.y;
     return w;
 }
 
+// The passes' twiddles, staged per workgroup in the order the lanes read them (round 6). Read from
+// the natural 1024-entry table, pass 2's W_1024^{4 k r} (k = lane & 15) put the 16 lanes of a read
+// group at stride 4 r entries -- 4- to 16-way LDS bank conflicts for every r (PMC: 36 % of the
+// channelizer's LDS-active cycles were conflict cycles) -- and pass 3's W^{2 j'} at stride 2.
+//   T2[r][k]      = W_1024^{4 k r}   (r, k < 16: a read group's lanes take 16 consecutive entries)
+//   T3[r - 1][j'] = W_1024^{r j'}    (r = 1..3, j' < 256: consecutive lanes, consecutive entries)
+// The values are the same floats as the natural table's, so the outputs are bit-identical.
+constexpr int T2N = 16 * 16, T3N = 3 * 256, TWN = T2N + T3N;
+__device__ __forceinline__ void stage_twiddles(cf* __restrict__ t, const float2* __restrict__ tw_g, int tid, int nt)
+{
+    for (int i = tid; i < TWN; i += nt) {
+        int e;
+        if (i < T2N)
+            e = (4 * (i & 15) * (i >> 4)) & (N - 1);
+        else
+            e = ((1 + (i - T2N) / 256) * ((i - T2N) & 255)) & (N - 1);
+        t[i] = cf{ tw_g[e].x, tw_g[e].y };
+    }
+}
+
 // Transform of one frame held as v[m] = x[lane + 64 m]; on return v[m] = X[lane + 64 m]
-// (pass 3 output kept in registers: m = b + 4 r for butterfly b, output r).
+// (pass 3 output kept in registers: m = b + 4 r for butterfly b, output r). tw: the staged T2 | T3.
 template <bool INV>
 __device__ __forceinline__ void fft_wave(cf (&v)[16], cf* __restrict__ img, const cf* __restrict__ tw)
 {
@@ -119,7 +138,7 @@ __device__ __forceinline__ void fft_wave(cf (&v)[16], cf* __restrict__ img, cons
 #pragma unroll
     for (int r = 0; r < 16; ++r) v[r] = img[pad(j + 64 * r)];
 #pragma unroll
-    for (int r = 1; r < 16; ++r) v[r] = cmulw(v[r], twid<INV>(tw, 4 * k2 * r));
+    for (int r = 1; r < 16; ++r) v[r] = cmulw(v[r], conj_if<INV>(tw[16 * r + k2]));
     dft16<INV>(v);
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -132,9 +151,9 @@ __device__ __forceinline__ void fft_wave(cf (&v)[16], cf* __restrict__ img, cons
     for (int b = 0; b < 4; ++b) {
         const int jp = j + 64 * b;
         cf a0 = img[pad(jp)], a1 = img[pad(jp + 256)], a2 = img[pad(jp + 512)], a3 = img[pad(jp + 768)];
-        a1 = cmulw(a1, twid<INV>(tw, jp));
-        a2 = cmulw(a2, twid<INV>(tw, 2 * jp));
-        a3 = cmulw(a3, twid<INV>(tw, 3 * jp));
+        a1 = cmulw(a1, conj_if<INV>(tw[T2N + jp]));
+        a2 = cmulw(a2, conj_if<INV>(tw[T2N + 256 + jp]));
+        a3 = cmulw(a3, conj_if<INV>(tw[T2N + 512 + jp]));
         dft4<INV>(a0, a1, a2, a3);
         o[b] = a0;
         o[b + 4] = a1;
@@ -172,9 +191,9 @@ template <bool INV>
 __global__ __launch_bounds__(NT) void k_fft1024(const float2* __restrict__ in, float2* __restrict__ out, int64_t nframes,
                                                 const float2* __restrict__ tw_g)
 {
-    __shared__ cf tw[N];
+    __shared__ cf tw[TWN];
     __shared__ cf img_all[FPW * WLDS];
-    for (int t = threadIdx.x; t < N; t += NT) tw[t] = cf{ tw_g[t].x, tw_g[t].y };
+    stage_twiddles(tw, tw_g, threadIdx.x, NT);
     __syncthreads();
     cf* img = img_all + (threadIdx.x >> 6) * WLDS;
     const int64_t stride = (int64_t)gridDim.x * FPW;
@@ -203,13 +222,11 @@ template <int FW>
 __global__ __launch_bounds__(64 * FW, FW == 4 ? 2 : 1) void k_chan1024(const float2* __restrict__ in, float2* __restrict__ out, int64_t nframes,
                                                     const float2* __restrict__ tw_g, const float2* __restrict__ w)
 {
-    __shared__ cf tw[N];
+    __shared__ cf tw[TWN];
     __shared__ cf wl[N];
     __shared__ cf img_all[FW * WLDS];
-    for (int t = threadIdx.x; t < N; t += 64 * FW) {
-        tw[t] = cf{ tw_g[t].x, tw_g[t].y };
-        wl[t] = cf{ w[t].x, w[t].y };
-    }
+    stage_twiddles(tw, tw_g, threadIdx.x, 64 * FW);
+    for (int t = threadIdx.x; t < N; t += 64 * FW) wl[t] = cf{ w[t].x, w[t].y };
     __syncthreads();
     cf* img = img_all + (threadIdx.x >> 6) * WLDS;
     const int j = threadIdx.x & 63;
