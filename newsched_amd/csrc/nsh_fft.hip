@@ -102,28 +102,42 @@ __device__ __forceinline__ cf conj_if(cf w)
     return w;
 }
 
-// The passes' twiddles, staged per workgroup in the order the lanes read them (round 6). Read from
-// the natural 1024-entry table, pass 2's W_1024^{4 k r} (k = lane & 15) put the 16 lanes of a read
-// group at stride 4 r entries -- 4- to 16-way LDS bank conflicts for every r (PMC: 36 % of the
-// channelizer's LDS-active cycles were conflict cycles) -- and pass 3's W^{2 j'} at stride 2.
+// The passes' twiddles, staged per workgroup. Read from the natural 1024-entry table (the default),
+// pass 2's W_1024^{4 k r} (k = lane & 15) puts the 16 lanes of a read group at stride 4 r entries --
+// 4- to 16-way LDS bank conflicts (PMC: 36 % of the channelizer's LDS-active cycles are conflict
+// cycles) -- and pass 3's W^{2 j'} at stride 2. NSH_FFT_TW_READORDER=1 (a probe, round 6) stages them
+// in the order the lanes read them instead, the same floats (bit-identical outputs):
 //   T2[r][k]      = W_1024^{4 k r}   (r, k < 16: a read group's lanes take 16 consecutive entries)
 //   T3[r - 1][j'] = W_1024^{r j'}    (r = 1..3, j' < 256: consecutive lanes, consecutive entries)
-// The values are the same floats as the natural table's, so the outputs are bit-identical.
-constexpr int T2N = 16 * 16, T3N = 3 * 256, TWN = T2N + T3N;
+// Conflict-free, and no faster: channelizer 765-769 vs 763-764 us, fft1024 707-708 vs 704 us per
+// 2^28 samples, both orders (profiles/r06e_chan_twiddle_layout_ab.log) -- LDS does not bound them.
+#ifndef NSH_FFT_TW_READORDER
+#define NSH_FFT_TW_READORDER 0
+#endif
+constexpr int T2N = 16 * 16, T3N = 3 * 256, TWN = NSH_FFT_TW_READORDER ? T2N + T3N : N;
 __device__ __forceinline__ void stage_twiddles(cf* __restrict__ t, const float2* __restrict__ tw_g, int tid, int nt)
 {
     for (int i = tid; i < TWN; i += nt) {
-        int e;
-        if (i < T2N)
-            e = (4 * (i & 15) * (i >> 4)) & (N - 1);
-        else
-            e = ((1 + (i - T2N) / 256) * ((i - T2N) & 255)) & (N - 1);
+        int e = i;
+        if (NSH_FFT_TW_READORDER)
+            e = i < T2N ? (4 * (i & 15) * (i >> 4)) & (N - 1) : ((1 + (i - T2N) / 256) * ((i - T2N) & 255)) & (N - 1);
         t[i] = cf{ tw_g[e].x, tw_g[e].y };
     }
 }
+// pass 2's W_1024^{4 k2 r} and pass 3's W_1024^{r jp} (r = 1..3) from the staged table
+template <bool INV>
+__device__ __forceinline__ cf tw_pass2(const cf* __restrict__ tw, int k2, int r)
+{
+    return conj_if<INV>(NSH_FFT_TW_READORDER ? tw[16 * r + k2] : tw[(4 * k2 * r) & (N - 1)]);
+}
+template <bool INV>
+__device__ __forceinline__ cf tw_pass3(const cf* __restrict__ tw, int jp, int r)
+{
+    return conj_if<INV>(NSH_FFT_TW_READORDER ? tw[T2N + 256 * (r - 1) + jp] : tw[(r * jp) & (N - 1)]);
+}
 
 // Transform of one frame held as v[m] = x[lane + 64 m]; on return v[m] = X[lane + 64 m]
-// (pass 3 output kept in registers: m = b + 4 r for butterfly b, output r). tw: the staged T2 | T3.
+// (pass 3 output kept in registers: m = b + 4 r for butterfly b, output r). tw: the staged table.
 template <bool INV>
 __device__ __forceinline__ void fft_wave(cf (&v)[16], cf* __restrict__ img, const cf* __restrict__ tw)
 {
@@ -138,7 +152,7 @@ __device__ __forceinline__ void fft_wave(cf (&v)[16], cf* __restrict__ img, cons
 #pragma unroll
     for (int r = 0; r < 16; ++r) v[r] = img[pad(j + 64 * r)];
 #pragma unroll
-    for (int r = 1; r < 16; ++r) v[r] = cmulw(v[r], conj_if<INV>(tw[16 * r + k2]));
+    for (int r = 1; r < 16; ++r) v[r] = cmulw(v[r], tw_pass2<INV>(tw, k2, r));
     dft16<INV>(v);
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -151,9 +165,9 @@ __device__ __forceinline__ void fft_wave(cf (&v)[16], cf* __restrict__ img, cons
     for (int b = 0; b < 4; ++b) {
         const int jp = j + 64 * b;
         cf a0 = img[pad(jp)], a1 = img[pad(jp + 256)], a2 = img[pad(jp + 512)], a3 = img[pad(jp + 768)];
-        a1 = cmulw(a1, conj_if<INV>(tw[T2N + jp]));
-        a2 = cmulw(a2, conj_if<INV>(tw[T2N + 256 + jp]));
-        a3 = cmulw(a3, conj_if<INV>(tw[T2N + 512 + jp]));
+        a1 = cmulw(a1, tw_pass3<INV>(tw, jp, 1));
+        a2 = cmulw(a2, tw_pass3<INV>(tw, jp, 2));
+        a3 = cmulw(a3, tw_pass3<INV>(tw, jp, 3));
         dft4<INV>(a0, a1, a2, a3);
         o[b] = a0;
         o[b + 4] = a1;
