@@ -388,7 +388,7 @@ int nsh_synth_cf32(float* out, int64_t n, uint64_t first_index, uint64_t seed, v
 {
     if (n > 0 && !out) return nsh::fail_msg("nsh_synth_cf32: null pointer");
     if (n <= 0) return 0;
-    hipLaunchKernelGGL(k_synth, dim3(nsh::stream_grid(n, kBlock)), dim3(kBlock), 0, nsh::S(stream),
+    nsh::launch(k_synth, dim3(nsh::stream_grid(n, kBlock)), dim3(kBlock), 0, nsh::S(stream),
                        (float2*)out, n, first_index, seed);
     NSH_CK_LAUNCH("nsh_synth_cf32");
     return 0;

@@ -173,6 +173,67 @@ TEST(HipDomain, MultiplyChainC2)
     }
 }
 
+// scheduler_hip's kernel timing (set_kernel_timing / kernel_stats, bench.py's legs): every work()
+// call that launches records its own event pair; calls that launch nothing (the synthetic source
+// here launches k_synth -- the sink does not) are not counted. Fusion on: the four multiply blocks
+// are one block with one launch per work() call; off: four blocks, each with the same count. Off
+// by default; reset clears; the outputs stay bit-exact with timing on.
+TEST(HipDomain, KernelTimingPerBlock)
+{
+    const size_t n = 1u << 20;
+    const std::vector<gr_complex> ks = { std::polar(1.0f, 0.1f), std::polar(1.0f, 0.2f), std::polar(1.0f, 0.3f),
+                                         std::polar(1.0f, 0.4f) };
+    auto x = synth(n);
+    std::vector<gr_complex> ref(x);
+    for (auto k : ks)
+        for (auto& v : ref) v = cmul(v, k);
+    for (int fused = 1; fused >= 0; --fused) {
+        auto src = hip::synth_source::make(0, n);
+        std::vector<hip::multiply_const_cc::sptr> m;
+        for (auto k : ks) m.push_back(hip::multiply_const_cc::make(k));
+        auto snk = blocks::vector_sink_c::make(1, n);
+        auto fg = flowgraph::make();
+        fg->connect(src, 0, m[0], 0);
+        for (size_t i = 1; i < m.size(); ++i) fg->connect(m[i - 1], 0, m[i], 0);
+        fg->connect(m.back(), 0, snk, 0)->set_custom_buffer(HIP_BUFFER_ARGS_D2H);
+        auto sched = schedulers::scheduler_hip::make("hip", 0, 1u << 20); // 128 Ki samples per call: 8 calls
+        sched->set_fusion(fused == 1);
+        fg->set_scheduler(sched);
+        fg->validate();
+        fg->run();
+        EXPECT_TRUE(sched->kernel_stats().empty()); // off by default
+        sched->set_kernel_timing(true);
+        fg->run();
+        EXPECT_TRUE(snk->data() == ref);
+        auto st = sched->kernel_stats();
+        // the source (k_synth) and the multiply blocks launch; the D2H sink's edge copy is not a work() launch
+        size_t mul_blocks = 0;
+        uint64_t src_calls = 0;
+        for (auto& k : st) {
+            EXPECT_TRUE(k.launches > 0 && k.kernel_ms > 0);
+            if (k.block.find("multiply_const") != std::string::npos) {
+                ++mul_blocks;
+                EXPECT_EQ(k.items, (uint64_t)n); // every sample once per block
+            } else if (k.block.find("synth") != std::string::npos) {
+                src_calls = k.launches;
+            } else {
+                std::printf("  unexpected launching block: %s\n", k.block.c_str());
+                EXPECT_TRUE(false);
+            }
+        }
+        EXPECT_EQ(mul_blocks, fused ? 1u : 4u);
+        for (auto& k : st)
+            if (k.block.find("multiply_const") != std::string::npos) EXPECT_EQ(k.launches, src_calls);
+        std::printf("  fused=%d: %zu launching blocks, %llu calls each\n", fused, st.size(), (unsigned long long)src_calls);
+        sched->reset_kernel_stats();
+        EXPECT_TRUE(sched->kernel_stats().empty());
+        sched->set_kernel_timing(false);
+        fg->run();
+        EXPECT_TRUE(sched->kernel_stats().empty());
+        EXPECT_TRUE(snk->data() == ref);
+    }
+}
+
 // Reference BasicBlockGrouping (schedulers/mt/test/qa_block_grouping.cpp:15-66) in the GPU
 // domain: 128 chained multiply_const(1) blocks are the identity. scheduler_hip fuses them
 // into 8 blocks of 16 stages (the fused kernel's limit).

@@ -141,6 +141,42 @@ def test_chain_bench_kernel_timing(torch_cuda):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("decim", [1, 2, 4])
+def test_chain_bench_time_shard(torch_cuda, decim):
+    """A leg's flowgraph on a time shard (first_index > 0, as rank r streams x[rN, (r+1)N)): the FIR's
+    initial history is the shard's regenerated halo, so EVERY output of the first batch -- the head
+    included -- equals the oracle's filter of the continuous stream; C2 / C4 tails start at the
+    shard's offset (bit-exact / 1e-5)."""
+    import numpy as np
+    from newsched_amd import nsr
+    from oracle import oracle as orc
+    import bench
+
+    n, first = 1 << 14, 3 * (1 << 14) + 1024
+    taps = bench.firwin(127, 0.45)
+    cb = nsr.ChainBench(nsr.CHAIN_FIR, taps, n, decim=decim, first_index=first, out_buf_bytes=1 << 20)
+    cb.run()
+    y = cb.tail(n // decim)
+    cb.close()
+    xw = orc.synth(n + 126, first - 126)
+    ok, err, scale = orc.tol_ok(y, orc.fir_ccf(xw[126:], taps, decim, hist=xw[:126]))
+    assert ok, (decim, err, scale)
+    if decim == 1:
+        cb = nsr.ChainBench(nsr.CHAIN_MUL_CONST_CC, bench.C2_KS, n, first_index=first, out_buf_bytes=1 << 20)
+        cb.run()
+        y = cb.tail(n)
+        cb.close()
+        assert np.array_equal(y, orc.mul_const_chain_cc(orc.synth(n, first), bench.C2_KS))
+        n4 = 1 << 18
+        cb = nsr.ChainBench(nsr.CHAIN_CHANNELIZER, bench.c4_weights(), n4, first_index=first, out_buf_bytes=4 << 20)
+        cb.run()
+        y = cb.tail(4096)
+        cb.close()
+        ok, err, scale = orc.tol_ok(y, orc.channelizer1024(orc.synth(4096, first + n4 - 4096), bench.c4_weights()))
+        assert ok, ("c4", err, scale)
+
+
+@pytest.mark.gpu
 def test_bench_c5_single_gpu(torch_cuda):
     """C5 at G = 1 (all four stages in one scheduler_hip domain) through the same leg."""
     out = subprocess.run([sys.executable, "bench.py", "--c5", "on", "--c5-log2n", "22"] + ARGS, cwd=ROOT,
