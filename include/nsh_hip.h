@@ -79,7 +79,9 @@ int nsh_stream_wait_event(void* stream, void* event);
  * the per-work() cudaEventRecord pairs a CUDA block would use for kernel timing (the reference
  * blocks do not time their kernels). */
 int nsh_time_next_launch(void* start_event, void* stop_event);
-/* Launches on the calling thread so far that recorded a pair set by nsh_time_next_launch (a pair
+/* (Every kernel entry point takes an armed pair with its launch and drops it, unrecorded, if it
+ * returns without launching: the stream kernels, fft / channelizer, synth, FIR and cascade.)
+ * Launches on the calling thread so far that recorded a pair set by nsh_time_next_launch (a pair
  * spanning several launches of one entry point counts each launch that records one of its two
  * events). A caller that armed a pair compares the count before and after the call it meant to
  * time: unchanged means no launch took the pair (the call launched nothing; the pair was dropped

@@ -304,6 +304,7 @@ extern "C" {
 
 int nsh_fft1024_c2c(const float* in, float* out, int64_t nframes, int inverse, void* stream)
 {
+    nsh::launch_events_guard timing_guard; // an armed event pair never outlives this call
     if (nframes <= 0) return 0;
     if (!in || !out) return nsh::fail_msg("nsh_fft1024_c2c: null pointer");
     if (in == out) return nsh::fail_msg("nsh_fft1024_c2c: in-place not supported");
@@ -323,6 +324,7 @@ int nsh_fft1024_c2c(const float* in, float* out, int64_t nframes, int inverse, v
 
 int nsh_channelizer1024(const float* in, float* out, const float* w, int64_t nframes, void* stream)
 {
+    nsh::launch_events_guard timing_guard; // an armed event pair never outlives this call
     if (nframes <= 0) return 0;
     if (!in || !out || !w) return nsh::fail_msg("nsh_channelizer1024: null pointer");
     if (in == out) return nsh::fail_msg("nsh_channelizer1024: in-place not supported");

@@ -289,6 +289,7 @@ extern "C" {
 
 int nsh_copy(const void* in, void* out, size_t bytes, void* stream)
 {
+    nsh::launch_events_guard timing_guard; // an armed event pair never outlives this call
     if (bytes && (!in || !out)) return nsh::fail_msg("nsh_copy: null pointer");
     if (bytes == 0) return 0;
     hipStream_t s = nsh::S(stream);
@@ -307,12 +308,14 @@ int nsh_copy(const void* in, void* out, size_t bytes, void* stream)
 
 int nsh_mul_const_cc(const float* in, float* out, int64_t n, float k_re, float k_im, void* stream)
 {
+    nsh::launch_events_guard timing_guard; // an armed event pair never outlives this call
     if (n > 0 && (!in || !out)) return nsh::fail_msg("nsh_mul_const_cc: null pointer");
     return launch_map_c(in, out, n, op_mulc{ make_float2(k_re, k_im) }, nsh::S(stream), "nsh_mul_const_cc");
 }
 
 int nsh_mul_const_ff(const float* in, float* out, int64_t n, float k, void* stream)
 {
+    nsh::launch_events_guard timing_guard; // an armed event pair never outlives this call
     if (n > 0 && (!in || !out)) return nsh::fail_msg("nsh_mul_const_ff: null pointer");
     if (n <= 0) return 0;
     hipStream_t s = nsh::S(stream);
@@ -336,6 +339,7 @@ int nsh_mul_const_ff(const float* in, float* out, int64_t n, float k, void* stre
 
 int nsh_mul_const_chain_cc(const float* in, float* out, int64_t n, const float* k_host, int m, void* stream)
 {
+    nsh::launch_events_guard timing_guard; // an armed event pair never outlives this call
     if (n > 0 && (!in || !out || (m > 0 && !k_host))) return nsh::fail_msg("nsh_mul_const_chain_cc: null pointer");
     hipStream_t s = nsh::S(stream);
     if (m <= 0) return nsh_copy(in, out, (size_t)n * 8, stream);
@@ -356,18 +360,21 @@ int nsh_mul_const_chain_cc(const float* in, float* out, int64_t n, const float* 
 
 int nsh_add_cc(const float* a, const float* b, float* out, int64_t n, void* stream)
 {
+    nsh::launch_events_guard timing_guard; // an armed event pair never outlives this call
     if (n > 0 && (!a || !b || !out)) return nsh::fail_msg("nsh_add_cc: null pointer");
     return launch_bin<0>(a, b, out, n, nsh::S(stream), "nsh_add_cc");
 }
 
 int nsh_mul_cc(const float* a, const float* b, float* out, int64_t n, void* stream)
 {
+    nsh::launch_events_guard timing_guard; // an armed event pair never outlives this call
     if (n > 0 && (!a || !b || !out)) return nsh::fail_msg("nsh_mul_cc: null pointer");
     return launch_bin<1>(a, b, out, n, nsh::S(stream), "nsh_mul_cc");
 }
 
 int nsh_mul_const_vcc(const float* in, float* out, const float* k_dev, int vlen, int64_t nitems, void* stream)
 {
+    nsh::launch_events_guard timing_guard; // an armed event pair never outlives this call
     if (nitems > 0 && (!in || !out || !k_dev)) return nsh::fail_msg("nsh_mul_const_vcc: null pointer");
     if (vlen <= 0 || nitems < 0) return nsh::fail_msg("nsh_mul_const_vcc: bad vlen or item count");
     const int64_t n = nitems * (int64_t)vlen;
@@ -386,6 +393,7 @@ int nsh_mul_const_vcc(const float* in, float* out, const float* k_dev, int vlen,
 
 int nsh_synth_cf32(float* out, int64_t n, uint64_t first_index, uint64_t seed, void* stream)
 {
+    nsh::launch_events_guard timing_guard; // an armed event pair never outlives this call
     if (n > 0 && !out) return nsh::fail_msg("nsh_synth_cf32: null pointer");
     if (n <= 0) return 0;
     nsh::launch(k_synth, dim3(nsh::stream_grid(n, kBlock)), dim3(kBlock), 0, nsh::S(stream),

@@ -1036,3 +1036,71 @@ def test_pfft_plan_timed(torch_cuda):
     for e in ev:
         L.nsh_event_destroy(e)
     plan.close()
+
+
+def test_timed_launches_counter_and_stream_kernels(torch_cuda):
+    """nsh_timed_launches counts the launches that took an armed pair (scheduler_hip's kernel
+    timing relies on it): an armed nsh_copy / nsh_mul_const_chain_cc / nsh_channelizer1024 records
+    the pair (+1, positive elapsed time); a call that launches nothing (0 bytes) leaves the count
+    and drops the pair when it returns, so the next, unarmed launch is not timed."""
+    import ctypes as C
+    torch = torch_cuda
+    L = nsh.lib()
+
+    def count():
+        c = C.c_uint64()
+        assert L.nsh_timed_launches(C.byref(c)) == 0
+        return c.value
+
+    n = 1 << 20
+    x = dev(torch, orc.synth(n, 11))
+    y = torch.empty_like(x)
+    w = dev(torch, orc.synth(1024, 12))
+    calls = [lambda: nsh.copy(x, y, 8 * n), lambda: nsh.mul_const_chain_cc(x, y, n, [0.5 + 0.5j, 1j]),
+             lambda: nsh.channelizer1024(x, y, w, n // 1024), lambda: nsh.synth(y, n, 7)]
+    for call in calls:
+        ev = [C.c_void_p(), C.c_void_p()]
+        for e in ev:
+            assert L.nsh_event_create(C.byref(e)) == 0
+        c0 = count()
+        assert L.nsh_time_next_launch(ev[0], ev[1]) == 0
+        call()
+        assert count() == c0 + 1
+        torch.cuda.synchronize()
+        ms = C.c_float()
+        assert L.nsh_event_elapsed_ms(ev[0], ev[1], C.byref(ms)) == 0 and ms.value > 0
+        for e in ev:
+            L.nsh_event_destroy(e)
+    ev = [C.c_void_p(), C.c_void_p()]
+    for e in ev:
+        assert L.nsh_event_create(C.byref(e)) == 0
+    c0 = count()
+    assert L.nsh_time_next_launch(ev[0], ev[1]) == 0
+    nsh.copy(x, y, 0)  # nothing to move: no launch, the pair is dropped on return
+    nsh.copy(x, y, 8 * n)  # unarmed
+    torch.cuda.synchronize()
+    assert count() == c0
+    ms = C.c_float()
+    assert L.nsh_event_elapsed_ms(ev[0], ev[1], C.byref(ms)) != 0  # never recorded
+    for e in ev:
+        L.nsh_event_destroy(e)
+
+
+def test_pointer_device(torch_cuda):
+    """nsh_pointer_device (the rccl transport's span check): device memory -> its GPU (hipMalloc and
+    a VMM double-mapped ring, both mappings), host memory (pageable, pinned) and NULL -> -1."""
+    import ctypes as C
+    torch = torch_cuda
+    L = nsh.lib()
+    t = torch.empty(1024, device="cuda")
+    assert nsh.pointer_device(t.data_ptr()) == 0
+    assert nsh.pointer_device(t.data_ptr() + 64) == 0
+    h = np.zeros(1024, np.float32)
+    assert nsh.pointer_device(h.ctypes.data) == -1
+    p = torch.empty(1024).pin_memory()
+    assert nsh.pointer_device(p.data_ptr()) == -1
+    assert nsh.pointer_device(0) == -1
+    b, act, dm = C.c_void_p(), C.c_size_t(), C.c_int()
+    nsh.check(L.nsh_ring_alloc(0, 1 << 20, C.byref(b), C.byref(act), C.byref(dm)), "ring")
+    assert nsh.pointer_device(b.value) == 0 and nsh.pointer_device(b.value + act.value + 8) == 0
+    nsh.check(L.nsh_ring_free(b), "ring free")
