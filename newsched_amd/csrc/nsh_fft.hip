@@ -232,8 +232,16 @@ __global__ __launch_bounds__(NT) void k_fft1024(const float2* __restrict__ in, f
 #define NSH_CHAN_FPW 4
 #endif
 constexpr int CFPW = NSH_CHAN_FPW; // channelizer frames (waves) per workgroup
+// probe knobs (round 6): the next frame prefetched into registers as in k_fft1024, and the launch
+// bounds' minimum workgroups per CU (2 lets the compiler take up to 256 VGPRs: 2 waves per SIMD)
+#ifndef NSH_CHAN_PREFETCH
+#define NSH_CHAN_PREFETCH 0
+#endif
+#ifndef NSH_CHAN_MINWG
+#define NSH_CHAN_MINWG 2
+#endif
 template <int FW>
-__global__ __launch_bounds__(64 * FW, FW == 4 ? 2 : 1) void k_chan1024(const float2* __restrict__ in, float2* __restrict__ out, int64_t nframes,
+__global__ __launch_bounds__(64 * FW, FW == 4 ? NSH_CHAN_MINWG : 1) void k_chan1024(const float2* __restrict__ in, float2* __restrict__ out, int64_t nframes,
                                                     const float2* __restrict__ tw_g, const float2* __restrict__ w)
 {
     __shared__ cf tw[TWN];
@@ -246,6 +254,22 @@ __global__ __launch_bounds__(64 * FW, FW == 4 ? 2 : 1) void k_chan1024(const flo
     const int j = threadIdx.x & 63;
     const int64_t stride = (int64_t)gridDim.x * FW;
     cf v[16];
+#if NSH_CHAN_PREFETCH
+    int64_t f = (int64_t)blockIdx.x * FW + (threadIdx.x >> 6);
+    if (f >= nframes) return;
+    cf nx[16];
+    load_frame16(v, in, f, nframes);
+    for (; f < nframes; f += stride) {
+        load_frame16(nx, in, f + stride, nframes);
+        fft_wave<false>(v, img, tw);
+#pragma unroll
+        for (int m = 0; m < 16; ++m) v[m] = cmul_rn(v[m], wl[j + 64 * m]);
+        fft_wave<true>(v, img, tw);
+        store_frame16(v, out, f, nframes);
+#pragma unroll
+        for (int m = 0; m < 16; ++m) v[m] = nx[m];
+    }
+#else
     for (int64_t f = (int64_t)blockIdx.x * FW + (threadIdx.x >> 6); f < nframes; f += stride) {
         load_frame16(v, in, f, nframes);
         fft_wave<false>(v, img, tw);
@@ -254,6 +278,7 @@ __global__ __launch_bounds__(64 * FW, FW == 4 ? 2 : 1) void k_chan1024(const flo
         fft_wave<true>(v, img, tw);
         store_frame16(v, out, f, nframes);
     }
+#endif
 }
 
 std::mutex g_tw_mtx;
