@@ -20,6 +20,7 @@ struct scheduler_hip::launch_timer {
         std::vector<uint64_t> items;             // per recorded pair
         size_t used = 0;
         kernel_stat done;                        // folded totals
+        uint64_t done_unrecorded = 0;            // pairs a block's own timing displaced
     };
     std::atomic<bool> on{ false };
     std::mutex m;
@@ -39,7 +40,18 @@ struct scheduler_hip::launch_timer {
         for (size_t i = 0; i < p.used; ++i) {
             float ms = 0;
             hip::check(nsh_event_sync(p.ev[i].second), "scheduler_hip: kernel timing");
-            hip::check(nsh_event_elapsed_ms(p.ev[i].first, p.ev[i].second, &ms), "scheduler_hip: kernel timing");
+            if (nsh_event_elapsed_ms(p.ev[i].first, p.ev[i].second, &ms) != 0) {
+                // never recorded: a block armed a pair of its own over ours (its own kernel timing,
+                // e.g. hip::fir_filter_ccf::enable_timing) and the launch took that one. Not counted,
+                // and the pair is replaced so no stale time can be read from it later.
+                nsh_event_destroy(p.ev[i].first);
+                nsh_event_destroy(p.ev[i].second);
+                p.ev[i] = { nullptr, nullptr };
+                hip::check(nsh_event_create(&p.ev[i].first), "scheduler_hip: kernel timing");
+                hip::check(nsh_event_create(&p.ev[i].second), "scheduler_hip: kernel timing");
+                ++p.done_unrecorded;
+                continue;
+            }
             p.done.kernel_ms += ms;
             p.done.launches += 1;
             p.done.items += p.items[i];

@@ -234,6 +234,40 @@ TEST(HipDomain, KernelTimingPerBlock)
     }
 }
 
+// Both timings on at once (documented as unsupported: the block's own pair displaces the
+// scheduler's): nothing throws, the block's own times are intact, and the scheduler does not count
+// the displaced pairs as launches of the FIR.
+TEST(HipDomain, KernelTimingDisplacedByBlockTiming)
+{
+    const size_t n = 1u << 18;
+    std::vector<float> h(127);
+    for (int k = 0; k < 127; ++k) h[k] = 0.01f * std::cos(0.05f * k);
+    auto src = hip::synth_source::make(0, n);
+    auto fir = hip::fir_filter_ccf::make(h, 1);
+    fir->enable_timing(true);
+    auto snk = blocks::vector_sink_c::make(1, n);
+    auto fg = flowgraph::make();
+    fg->connect(src, 0, fir, 0);
+    fg->connect(fir, 0, snk, 0)->set_custom_buffer(HIP_BUFFER_ARGS_D2H);
+    auto sched = schedulers::scheduler_hip::make("hip", 0, 256u << 10);
+    fg->set_scheduler(sched);
+    fg->validate();
+    sched->set_kernel_timing(true);
+    fg->run();
+    bool threw = false;
+    std::vector<schedulers::scheduler_hip::kernel_stat> st;
+    try {
+        st = sched->kernel_stats();
+    } catch (const std::exception& e) {
+        threw = true;
+        std::printf("  kernel_stats threw: %s\n", e.what());
+    }
+    EXPECT_TRUE(!threw);
+    for (auto& k : st) EXPECT_TRUE(k.block.find("fir_filter_ccf") == std::string::npos);
+    EXPECT_TRUE(fir->timed_launches() > 0 && fir->kernel_ms() > 0);
+    EXPECT_EQ(snk->data().size(), n);
+}
+
 // Reference BasicBlockGrouping (schedulers/mt/test/qa_block_grouping.cpp:15-66) in the GPU
 // domain: 128 chained multiply_const(1) blocks are the identity. scheduler_hip fuses them
 // into 8 blocks of 16 stages (the fused kernel's limit).
