@@ -266,9 +266,14 @@ def run_fp32_leg(a, n, taps, first, device, barrier, dist, tdev, torch, orc, nsr
     split, fp32 products and sums) -- what the ceiling is without split precision."""
     fb = nsr.FirBench(taps, n, device=device, algo=nsh.FIR_MFMA_F32, first_index=first,
                       out_buf_bytes=a.out_buf_mib << 20)
-    steps = max(5, a.steps // 4)
-    for _ in range(max(3, a.warmup // 2)):
+    steps = max(10, a.steps // 4)
+    # warm-up by time as well as by count: the chip comes from the headline's power-limited ~1.1 GHz
+    # and this MFMA-bound leg follows the clock; 3 launches (~4 ms) left it mid-ramp at --steps 20
+    # (r06l: 37.6 % at 2022 MHz there vs 42.8 % at 2168 MHz with the default --steps 100, r06g)
+    tw, runs = time.perf_counter(), 0
+    while runs < max(3, a.warmup // 2) or time.perf_counter() - tw < a.legs_warmup_s:
         fb.run()
+        runs += 1
     barrier()
     st0 = fb.stats()  # cumulative over the FIR's timed launches
     l0 = st0["launches"]
@@ -395,7 +400,7 @@ def run_chain_leg(a, name, spec, rank, device, barrier, dist, tdev, torch, orc, 
         fb.set_batches(4)
         while time.perf_counter() - t0 < a.legs_warmup_s:
             fb.run()
-        steps = max(5, a.steps // 4)
+        steps = max(10, a.steps // 4)
         fb.set_batches(steps)
         barrier()
         st0 = fb.stats()
@@ -487,7 +492,7 @@ def run_c5_fused_leg(a, first, device, barrier, dist, tdev, torch, orc, nsh):
     while time.perf_counter() - t0 < 0.5:
         plan(x, hist, hout, y, n_out, stream=s)
         s.synchronize()
-    steps = max(5, a.steps // 4)
+    steps = max(10, a.steps // 4)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
     barrier()
     t0 = time.perf_counter()
@@ -563,7 +568,8 @@ def main():
                          "(auto: at world 1 only -- they are single-GPU configs, and a rank that fails one must "
                          "not leave its peers waiting in the leg's barriers of a multi-GPU run)")
     ap.add_argument("--legs-log2n", type=int, default=28)
-    ap.add_argument("--legs-warmup-s", type=float, default=0.3)
+    ap.add_argument("--legs-warmup-s", type=float, default=0.5,
+                    help="untimed warm-up per leg (seconds, at least): the clock settles for that leg's kernel")
     ap.add_argument("--c5-log2n", type=int, default=26)
     ap.add_argument("--c5-steps", type=int, default=5)
     ap.add_argument("--c5-warmup", type=int, default=2)
