@@ -308,33 +308,44 @@ def run_fp32_leg(a, n, taps, first, device, barrier, dist, tdev, torch, orc, nsr
 def run_copy_leg(n, barrier, torch, nsh):
     """The measured STREAM-copy ceiling beside the spec peak: nsh_copy (k_copy_v4) of
     the headline's 2^log2n complex samples, i.e. the same 16 B per sample the FIR moves, timed with
-    HIP events on its stream after a short warm-up, best of 3 x 10 launches. Fresh buffers, not the
-    flowgraph's VMM rings: a kernel on those may run a few percent faster than this copy (r04ze:
-    C2's map kernel streamed at 1.08x it), so frac_of_copy can exceed 1."""
-    x = torch.empty(n, dtype=torch.complex64, device="cuda")
-    y = torch.empty_like(x)
-    nsh.synth(x, n, 0)
+    HIP events on its stream after a short warm-up, best of 3 x 10 launches. The copy's rate depends
+    on where its input and output sit relative to each other in HBM -- 70.4-77.7 % for the same code
+    as the output moves by 128 KiB steps inside one allocation (tools/probe/offset_sweep.py,
+    profiles/r06p_offset_sweep_fine.log), while the FIR kernels are flat (r06q, r06r) -- so the
+    input and output are carved from ONE allocation and the copy is timed at three output offsets
+    (2^log2n samples + 0 / 128 KiB / 1 MiB): `GBs` is the best, `by_offset` all three. (Earlier
+    rounds timed one pair of fresh buffers: a draw from that range.)"""
+    offs = [0, 128 << 10, 1 << 20]
+    buf = torch.empty(16 * n + max(offs) + 4096, dtype=torch.uint8, device="cuda")
+    base = buf.data_ptr()
+    nsh.synth(base, n, 0)
     s = torch.cuda.Stream()
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < 0.3:
-        nsh.copy(x, y, 8 * n, stream=s)
+        nsh.copy(base, base + 8 * n, 8 * n, stream=s)
         s.synchronize()
     reps = 10
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     barrier()
-    ms = None
-    for _ in range(3):  # best of 3
-        e0.record(s)
-        for _ in range(reps):
-            nsh.copy(x, y, 8 * n, stream=s)
-        e1.record(s)
-        s.synchronize()
-        m = e0.elapsed_time(e1) / reps
-        ms = m if ms is None else min(ms, m)
-    del x, y
-    gbs = BYTES_PER_SAMPLE * n / (ms * 1e-3) / 1e9
-    return {"kernel": "k_copy_v4", "avg_launch_us": round(ms * 1e3, 2), "GBs": round(gbs, 1),
-            "frac_of_peak": round(gbs / HBM_PEAK_GBS, 4)}
+    by = {}
+    for d in offs:
+        ms = None
+        for _ in range(3):  # best of 3
+            e0.record(s)
+            for _ in range(reps):
+                nsh.copy(base, base + 8 * n + d, 8 * n, stream=s)
+            e1.record(s)
+            s.synchronize()
+            m = e0.elapsed_time(e1) / reps
+            ms = m if ms is None else min(ms, m)
+        by[d] = ms
+    del buf
+    best = min(by.values())
+    gbs = BYTES_PER_SAMPLE * n / (best * 1e-3) / 1e9
+    return {"kernel": "k_copy_v4", "avg_launch_us": round(best * 1e3, 2), "GBs": round(gbs, 1),
+            "frac_of_peak": round(gbs / HBM_PEAK_GBS, 4),
+            "by_offset": {str(d): round(BYTES_PER_SAMPLE * n / (m * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) for d, m in by.items()},
+            "placement": "input and output in one allocation, output at 2^log2n samples + offset bytes; best of the offsets"}
 
 
 C2_KS = [complex(np.float32(np.cos(t)), np.float32(np.sin(t))) for t in (0.1, 0.2, 0.3, 0.4)]  # e^{j{.1,.2,.3,.4}}
