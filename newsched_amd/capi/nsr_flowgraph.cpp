@@ -61,6 +61,31 @@ gr_complex synth_at(uint64_t i, uint64_t seed)
                       (float)(int)(splitmix64(seed ^ (g + 1)) >> 40) * (1.0f / 8388608.0f) - 1.0f);
 }
 
+// The ntaps - 1 stream samples before first_index (a FIR's initial history); indices before the
+// stream's start are zeros, as the filter's own start-up history.
+std::vector<gr_complex> history_before(uint64_t first_index, int ntaps, uint64_t seed)
+{
+    std::vector<gr_complex> h((size_t)(ntaps > 1 ? ntaps - 1 : 0));
+    for (size_t j = 0; j < h.size(); ++j) {
+        const uint64_t back = h.size() - j; // first_index - back
+        h[j] = back <= first_index ? synth_at(first_index - back, seed) : gr_complex(0.f, 0.f);
+    }
+    return h;
+}
+
+// A resident input ring holds the batch x (n samples from first_index) twice, the second copy
+// `half` bytes after the first, so every run starts on a copy of x.
+void preload_twice(char* base, size_t half, int64_t n, uint64_t first_index, uint64_t seed, int dev)
+{
+    void* s = nullptr;
+    hip::check(nsh_stream_create(dev, &s), "nsr: stream");
+    int rc = nsh_synth_cf32((float*)base, n, first_index, seed, s);
+    if (rc == 0) rc = nsh_synth_cf32((float*)(base + half), n, first_index, seed, s);
+    const int rc2 = nsh_stream_sync(s); // also after a failed launch: nothing of ours left queued
+    nsh_stream_destroy(s);
+    hip::check(rc != 0 ? rc : rc2, "nsr: preload");
+}
+
 // Tail of a device ring's last `count` written items -> host.
 void ring_tail(const std::shared_ptr<hip_buffer>& r, int dev, int64_t count, float* out_host)
 {
@@ -115,7 +140,8 @@ int nsr_fir_bench_create(int dev, const float* taps, int ntaps, int algo, int64_
 {
     return guarded([&] {
         if (n <= 0 || n % 256) throw std::invalid_argument("nsr_fir_bench_create: n must be a positive multiple of 256");
-        auto b = new fir_bench();
+        if (!taps || ntaps <= 0) throw std::invalid_argument("nsr_fir_bench_create: no taps");
+        auto b = std::make_unique<fir_bench>();
         b->dev = dev;
         const size_t isz = sizeof(gr_complex);
         auto src = blocks::nop_source::make(isz);
@@ -125,11 +151,7 @@ int nsr_fir_bench_create(int dev, const float* taps, int ntaps, int algo, int64_
         b->fir = hip::fir_filter_ccf::make(std::vector<float>(taps, taps + ntaps), 1, algo);
         b->timing = timing != 0;
         b->fir->enable_timing(b->timing);
-        if (first_index > 0) {
-            std::vector<gr_complex> h((size_t)ntaps - 1);
-            for (size_t j = 0; j < h.size(); ++j) h[j] = synth_at(first_index - h.size() + j, seed);
-            b->fir->set_initial_history(h);
-        }
+        if (first_index > 0) b->fir->set_initial_history(history_before(first_index, ntaps, seed));
         auto snk = blocks::null_sink::make(isz);
         b->fg = flowgraph::make();
         // the nop edge is never touched: a host ring costs no memory traffic
@@ -153,14 +175,8 @@ int nsr_fir_bench_create(int dev, const float* taps, int ntaps, int algo, int64_
         b->out_ring = std::dynamic_pointer_cast<hip_buffer>(b->sched->buffers()->get_input_buffer(snk->input_stream_ports()[0]));
         if (!in_ring || !b->out_ring) throw std::runtime_error("nsr_fir_bench_create: unexpected buffer types");
         if ((int64_t)in_ring->capacity() != cap) throw std::runtime_error("nsr_fir_bench_create: ring capacity mismatch");
-        void* s = nullptr;
-        hip::check(nsh_stream_create(dev, &s), "nsr: stream");
-        char* base = (char*)in_ring->device_base();
-        hip::check(nsh_synth_cf32((float*)base, n, first_index, seed, s), "nsr: preload");
-        hip::check(nsh_synth_cf32((float*)(base + n * isz), n, first_index, seed, s), "nsr: preload");
-        hip::check(nsh_stream_sync(s), "nsr: preload");
-        nsh_stream_destroy(s);
-        *handle = b;
+        preload_twice((char*)in_ring->device_base(), n * isz, n, first_index, seed, dev);
+        *handle = b.release();
     });
 }
 
@@ -256,12 +272,9 @@ int nsr_chain_bench_create(int dev, int kind, const float* params, int nparams, 
             break;
         }
         case NSR_CHAIN_FIR: {
+            if (decim < 1) throw std::invalid_argument("nsr_chain_bench_create: decim must be >= 1");
             auto f = hip::fir_filter_ccf::make(std::vector<float>(params, params + nparams), decim);
-            if (first_index > 0) {
-                std::vector<gr_complex> h((size_t)nparams - 1);
-                for (size_t j = 0; j < h.size(); ++j) h[j] = synth_at(first_index - h.size() + j, seed);
-                f->set_initial_history(h);
-            }
+            if (first_index > 0) f->set_initial_history(history_before(first_index, nparams, seed));
             chain.push_back(f);
             break;
         }
@@ -296,13 +309,7 @@ int nsr_chain_bench_create(int dev, int kind, const float* params, int nparams, 
         b->out_ring = std::dynamic_pointer_cast<hip_buffer>(b->sched->buffers()->get_input_buffer(snk->input_stream_ports()[0]));
         if (!in_ring || !b->out_ring) throw std::runtime_error("nsr_chain_bench_create: unexpected buffer types");
         if ((int64_t)in_ring->capacity() != cap) throw std::runtime_error("nsr_chain_bench_create: ring capacity mismatch");
-        void* s = nullptr;
-        hip::check(nsh_stream_create(dev, &s), "nsr: stream");
-        char* base = (char*)in_ring->device_base();
-        hip::check(nsh_synth_cf32((float*)base, n, first_index, seed, s), "nsr: preload");
-        hip::check(nsh_synth_cf32((float*)(base + b->n_items * isz), n, first_index, seed, s), "nsr: preload");
-        hip::check(nsh_stream_sync(s), "nsr: preload");
-        nsh_stream_destroy(s);
+        preload_twice((char*)in_ring->device_base(), b->n_items * isz, n, first_index, seed, dev);
         b->sched->set_kernel_timing(true);
         *handle = b.release();
     });

@@ -177,6 +177,31 @@ def test_chain_bench_time_shard(torch_cuda, decim):
 
 
 @pytest.mark.gpu
+def test_chain_bench_shard_near_stream_start(torch_cuda):
+    """A shard that starts fewer than L - 1 samples into the stream: its history is the stream's
+    first samples preceded by zeros (before the round-6 fix the history indices wrapped below 0 and
+    regenerated unrelated samples), so the outputs equal the oracle's filter from the stream start."""
+    import numpy as np
+    from newsched_amd import nsh, nsr
+    from oracle import oracle as orc
+    import bench
+
+    n, first = 1 << 14, 40
+    taps = bench.firwin(127, 0.45)
+    for decim in (1, 4):
+        cb = nsr.ChainBench(nsr.CHAIN_FIR, taps, n, decim=decim, first_index=first, out_buf_bytes=1 << 20)
+        cb.run()
+        y = cb.tail(n // decim)
+        cb.close()
+        xs = orc.synth(first + n, 0)
+        ref = orc.fir_ccf(xs[first:], taps, decim, hist=np.concatenate([np.zeros(126 - first, np.complex64), xs[:first]]))
+        ok, err, scale = orc.tol_ok(y, ref)
+        assert ok, (decim, err, scale)
+    with pytest.raises(nsh.NshError, match="decim"):
+        nsr.ChainBench(nsr.CHAIN_FIR, taps, n, decim=0, out_buf_bytes=1 << 20)
+
+
+@pytest.mark.gpu
 def test_bench_c5_single_gpu(torch_cuda):
     """C5 at G = 1 (all four stages in one scheduler_hip domain) through the same leg."""
     out = subprocess.run([sys.executable, "bench.py", "--c5", "on", "--c5-log2n", "22"] + ARGS, cwd=ROOT,
