@@ -664,6 +664,17 @@ constexpr int IMG2 = 571; // odd: a 16-lane group's exchange-1 stores (16 phases
 #ifndef NSH_PFFT2_INV_BASE
 #define NSH_PFFT2_INV_BASE 4
 #endif
+// Probe (round 6): waves w >= NSH_PFFT2_LATE_FROM issue the next frame's row loads after their
+// products instead of after B1 (into the same registers: a second set spills). The phase
+// trace puts the youngest waves' load issue ~2.7k cycles after B1, behind the older waves' loads
+// in the CU's vector-memory queue, with their transforms waiting behind it; loading late, they
+// transform first and meet an idle queue while the older waves run the phase sum. Measured 12-17 %
+// slower (waves 4..15 / 8..15 / 12..15 late: 615-620 / 637-641 / 614 vs 542-549 us per 2^28
+// inputs, bit-identical, both orders, profiles/r06w_pfft2_late_loads_ab.log): the data's latency,
+// exposed before pass 1, costs more than the issue queue did. 16 = off (the product build).
+#ifndef NSH_PFFT2_LATE_FROM
+#define NSH_PFFT2_LATE_FROM 16
+#endif
 // Row-load cache policy: a frame's rows V .. M - 1 (V >= 384 for Q <= 128) are the next frame's
 // first rows, read again one frame later (mostly L2 hits); rows below V are read for the last
 // time. Load 3 holds rows 384 .. 511 and keeps the default policy; loads 0..2 stream
@@ -910,7 +921,11 @@ __global__ __launch_bounds__(64 * P, 1) void k_fir_pfft2(pfft_args a)
         // of frame f - 1 (waves 0..7; set s ^ 1 is rewritten only by frame f + 1's pass 1, after B2),
         // the next frame's pass 1
         if (inv2 && w == inv_wave(f - 2)) inverse(f - 2, ks2);
-        load_rows16<P>(nx, a, n_in, f + 1, f + 1 < f1, e0);
+#if NSH_PFFT2_LATE_FROM < 16
+        const bool late = w >= NSH_PFFT2_LATE_FROM; // wave-uniform
+        if (!late)
+#endif
+            load_rows16<P>(nx, a, n_in, f + 1, f + 1 < f1, e0);
         PFFT_T(3);
         const int64_t rowf = f * V;
         if (!bad) {
@@ -990,6 +1005,9 @@ __global__ __launch_bounds__(64 * P, 1) void k_fir_pfft2(pfft_args a)
                 if (rowf + t < a.n_out) a.out[rowf + t] = make_float2(last[Q + t].x, last[Q + t].y);
         }
         PFFT_T(4);
+#if NSH_PFFT2_LATE_FROM < 16
+        if (late) load_rows16<P>(nx, a, n_in, f + 1, f + 1 < f1, e0); // the same registers, loaded late
+#endif
         if (sum1 && w < P / 2) phase_sum(f - 1);
         if (f + 1 < f1) {
             unpack_rows(v, nx);
